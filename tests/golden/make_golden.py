@@ -1,0 +1,328 @@
+"""Generate golden fixtures by running the REFERENCE implementation itself.
+
+Runs only in the build container (it reads /root/reference, which does not
+exist on the GPU box).  The outputs are small .npz files committed next to this
+script; tests compare the oracle (and the HIP path) against them.
+
+How the reference is run: the hot-path modules are loaded by file path from
+/root/reference/open_universe into a synthetic package ``ouref`` (importing
+``open_universe`` itself pulls in datasets/Lightning).  Third-party modules
+that are absent from this image are replaced by in-memory stand-ins that never
+compute anything on the hot path, except ``torchaudio.transforms.MelSpectrogram``
+and ``Resample``, which are restated from torchaudio's documented algorithm
+(torchaudio is not installed).  Parity for the mel front end and the aux-path
+resampler is therefore pinned to that restatement, not to torchaudio bytes.
+
+Weights: ``open_universe_amd.utils.synthetic.synth_tensor`` keyed by parameter
+name (the trained HF checkpoint is unavailable offline).
+
+Usage:  python tests/golden/make_golden.py
+"""
+import importlib.util
+import math
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+REF = "/root/reference/open_universe"
+
+from open_universe_amd.configs import get_config  # noqa: E402
+from open_universe_amd.utils.synthetic import fill_module_, synth_audio  # noqa: E402
+from oracle import ou_oracle  # noqa: E402  (only for the torchaudio restatement)
+
+
+# ---------------------------------------------------------------------------
+# stand-ins for third-party packages missing from the image
+# ---------------------------------------------------------------------------
+class AttrDict(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+def to_attr(x):
+    if isinstance(x, dict):
+        return AttrDict({k: to_attr(v) for k, v in x.items()})
+    if isinstance(x, list):
+        return [to_attr(v) for v in x]
+    return x
+
+
+_REGISTRY = {}
+
+
+class _Dummy(torch.nn.Module):
+    def __init__(self, *a, **k):
+        super().__init__()
+
+
+def instantiate(cfg, _recursive_=False, **kw):
+    target = cfg["_target_"]
+    cls = _REGISTRY.get(target.rsplit(".", 1)[-1], _Dummy)
+    args = {k: v for k, v in cfg.items() if k != "_target_"}
+    args.update(kw)
+    if cls is _Dummy:
+        return _Dummy()
+    return cls(**args)
+
+
+def install_stubs():
+    hydra = types.ModuleType("hydra")
+    hydra_utils = types.ModuleType("hydra.utils")
+    hydra_utils.instantiate = instantiate
+    hydra.utils = hydra_utils
+    sys.modules["hydra"] = hydra
+    sys.modules["hydra.utils"] = hydra_utils
+
+    pl = types.ModuleType("pytorch_lightning")
+
+    class LightningModule(torch.nn.Module):
+        def save_hyperparameters(self, *a, **k):
+            pass
+
+    pl.LightningModule = LightningModule
+    sys.modules["pytorch_lightning"] = pl
+
+    te = types.ModuleType("torch_ema")
+
+    class ExponentialMovingAverage:
+        def __init__(self, params, decay):
+            self.shadow_params = [p.detach().clone() for p in params]
+            self.collected_params = None
+
+    te.ExponentialMovingAverage = ExponentialMovingAverage
+    sys.modules["torch_ema"] = te
+
+    oc = types.ModuleType("omegaconf")
+
+    class OmegaConf:
+        @staticmethod
+        def create(x):
+            return to_attr(x)
+
+        @staticmethod
+        def to_container(x, resolve=True):
+            return dict(x)
+
+    oc.OmegaConf = OmegaConf
+    sys.modules["omegaconf"] = oc
+    sys.modules["wandb"] = types.ModuleType("wandb")
+
+    ta = types.ModuleType("torchaudio")
+    tat = types.ModuleType("torchaudio.transforms")
+
+    class MelSpectrogram(torch.nn.Module):
+        """torchaudio.transforms.MelSpectrogram restated (see module doc)."""
+
+        def __init__(self, sample_rate=16000, n_fft=400, win_length=None,
+                     hop_length=None, f_min=0.0, f_max=None, pad=0, n_mels=128,
+                     center=True, **kw):
+            super().__init__()
+            assert center is False and pad == 0
+            self.n_fft, self.hop, self.n_mels, self.sr = n_fft, hop_length, n_mels, sample_rate
+            # same buffer names as torchaudio (state-dict compatibility)
+            self.spectrogram = torch.nn.Module()
+            self.spectrogram.register_buffer("window", torch.hann_window(n_fft))
+            self.mel_scale = torch.nn.Module()
+            self.mel_scale.register_buffer("fb", ou_oracle.melscale_fbanks(
+                n_fft // 2 + 1, 0.0, float(sample_rate // 2), n_mels, sample_rate))
+
+        def forward(self, x):
+            return ou_oracle.mel_spectrogram(x, self.n_fft, self.hop, self.n_mels, self.sr)
+
+    class Resample(torch.nn.Module):
+        """torchaudio.transforms.Resample(sinc_interp_hann) restated."""
+
+        def __init__(self, orig_freq=16000, new_freq=16000, **kw):
+            super().__init__()
+            self.orig, self.new = int(orig_freq), int(new_freq)
+            kern, self.width, _, _ = ou_oracle._sinc_resample_kernel(self.orig, self.new)
+            self.register_buffer("kernel", kern)
+
+        def forward(self, x):
+            return ou_oracle.resample(x, self.orig, self.new)
+
+    tat.MelSpectrogram = MelSpectrogram
+    tat.Resample = Resample
+    ta.transforms = tat
+    sys.modules["torchaudio"] = ta
+    sys.modules["torchaudio.transforms"] = tat
+
+
+def _load(modname, path):
+    spec = importlib.util.spec_from_file_location(modname, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[modname] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _pkg(name, path):
+    m = types.ModuleType(name)
+    m.__path__ = [path]
+    sys.modules[name] = m
+    return m
+
+
+def load_reference():
+    install_stubs()
+    _pkg("ouref", REF)
+    _pkg("ouref.networks", REF + "/networks")
+    _load("ouref.networks.bigvgan", REF + "/networks/bigvgan/__init__.py")
+    _load("ouref.layers", REF + "/layers/__init__.py") if os.path.exists(
+        REF + "/layers/__init__.py") else _pkg("ouref.layers", REF + "/layers")
+    _load("ouref.layers.dyn_range_comp", REF + "/layers/dyn_range_comp.py")
+    _load("ouref.utils", REF + "/utils/__init__.py")
+    _pkg("ouref.networks.universe", REF + "/networks/universe")
+    mods = {}
+    for m in ("blocks", "sigma_block", "score", "condition", "mdn", "universe",
+              "universe_NS", "universe_gan"):
+        mods[m] = _load(f"ouref.networks.universe.{m}", f"{REF}/networks/universe/{m}.py")
+    _REGISTRY.update(
+        ScoreNetwork=mods["score"].ScoreNetwork,
+        ConditionerNetwork=mods["condition"].ConditionerNetwork,
+        UniverseGAN=mods["universe_gan"].UniverseGAN,
+        Universe=mods["universe"].Universe,
+        MSELoss=torch.nn.MSELoss,
+    )
+    return mods
+
+
+# ---------------------------------------------------------------------------
+# reference model construction
+# ---------------------------------------------------------------------------
+def full_model_config(name, n_channels=None):
+    """Hot-path config + the training-only keys the constructors read."""
+    cfg = get_config(name, n_channels)
+    cfg.setdefault("losses", {})
+    cfg["losses"].update(
+        multi_period_discriminator={"mpd_reshapes": [2, 3, 5, 7, 11], "use_spectral_norm": False,
+                                    "discriminator_channel_mult": 1},
+        multi_resolution_discriminator={"resolutions": [[1024, 120, 600], [2048, 240, 1200], [512, 50, 240]],
+                                        "use_spectral_norm": False,
+                                        "discriminator_channel_mult": 1},
+        score_loss={"_target_": "torch.nn.MSELoss"},
+        weights={"score": 1.0, "signal": 1.0, "latent": 1.0, "mel_l1": 45.0},
+        mdn_n_comp=3,
+        mdn_alpha_per_sample=True,
+    )
+    cfg["training"] = {"audio_len": 2.0, "ema_decay": 0.0, "time_sampling": "time_uniform"}
+    cfg["validation"] = {"enh_losses": {}, "main_loss": "val/score", "n_bins": 5,
+                         "max_enh_batches": 4}
+    cfg["optimizer"] = {}
+    cfg["scheduler"] = {}
+    cfg["grad_clipper"] = {}
+    return cfg
+
+
+def build_ref_model(name, n_channels=None, seed=0):
+    cfg = to_attr(full_model_config(name, n_channels))
+    cls = _REGISTRY[cfg["_target_"].rsplit(".", 1)[-1]]
+    args = {k: v for k, v in cfg.items() if k != "_target_"}
+    model = cls(**args)
+    fill_module_(model, seed=seed)
+    model.eval()
+    return model
+
+
+def manifest(model):
+    sd = model.state_dict()
+    names = [k for k in sd.keys()]
+    shapes = [list(sd[k].shape) for k in names]
+    pid = {id(p): n for n, p in model.named_parameters()}
+    order = [pid[id(p)] for p in model.model_parameters()]
+    return names, shapes, order
+
+
+def tensors(d):
+    return {k: (v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v))
+            for k, v in d.items()}
+
+
+def main():
+    torch.set_num_threads(8)
+    load_reference()
+    out = {}
+
+    for name, nch, T, tag in (("pp16", None, 3360, "pp16"),
+                              ("pp16", 4, 4000, "pp16_c4"),
+                              ("orig16", 4, 3360, "orig16_c4"),
+                              ("pp24", 4, 5040, "pp24_c4")):
+        model = build_ref_model(name, nch)
+        names, shapes, order = manifest(model)
+        fs = model.fs
+        d = {}
+        d["manifest_names"] = np.array(names)
+        d["manifest_shapes"] = np.array([",".join(map(str, s)) for s in shapes])
+        d["param_order"] = np.array(order)
+
+        B = 2
+        mix = torch.stack([torch.from_numpy(synth_audio(T, fs, i)[0]) for i in range(B)])[:, None]
+        tgt = torch.stack([torch.from_numpy(synth_audio(T, fs, i)[1]) for i in range(B)])[:, None]
+        with torch.no_grad():
+            # conditioner on a padded, normalized input (what enhance feeds it)
+            xpad, _ = model.pad(mix)
+            (xn, _), *_ = model.normalize_batch((xpad, None))
+            conds, y_hat, hlat = model.condition_model(xn, x_wav=xn, train=True)
+            d["cond_in"] = xn
+            for i, c in enumerate(conds):
+                d[f"cond_out{i}"] = c
+            d["cond_yhat"] = y_hat
+            d["cond_h"] = hlat
+            # score network forward at two noise levels
+            sigma = torch.tensor([0.7, 0.02])
+            g = torch.Generator().manual_seed(5)
+            xs = torch.randn(xn.shape, generator=g) * 0.3
+            net = model.get_score_model()
+            d["score_x"] = xs
+            d["score_sigma"] = sigma
+            d["score_out"] = net(xs, sigma, conds)
+            # full enhance, default steps, seeded CPU generator
+            rng = torch.Generator().manual_seed(1028282)
+            d["enh_mix"] = mix
+            d["enh_out"] = model.enhance(mix[:, 0], rng=rng)
+            rng = torch.Generator().manual_seed(7)
+            d["enh2_out"] = model.enhance(mix, n_steps=3, rng=rng, keep_rms=True)
+            # sampler known-answer test: true score + noise at 20 dB
+            rng = torch.Generator().manual_seed(11)
+            d["enh_tgt"] = tgt
+            d["enh_fake_out"] = model.enhance(mix, target=tgt, fake_score_snr=20.0, rng=rng)
+            if tag in ("pp16_c4",):
+                rng = torch.Generator().manual_seed(3)
+                d["enh_ens_out"] = model.enhance(mix[0, 0], rng=rng, ensemble=3,
+                                                 ensemble_stat="median")
+                rng = torch.Generator().manual_seed(4)
+                d["enh_aux_out"] = model.enhance(mix, rng=rng, use_aux_signal=True)
+                rng = torch.Generator().manual_seed(6)
+                d["enh_warm_out"] = model.enhance(mix, rng=rng, warm_start=4)
+        out[tag] = tensors(d)
+        print(tag, "params", sum(p.numel() for p in model.model_parameters()),
+              "score_out rms", float(d["score_out"].square().mean().sqrt()),
+              "enh rms", float(d["enh_out"].square().mean().sqrt()))
+
+    for tag, d in out.items():
+        np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **d)
+    # PP24 full-width manifest only (too large to run cheaply)
+    for name in ("pp24", "orig16"):
+        model = build_ref_model(name)
+        names, shapes, order = manifest(model)
+        np.savez_compressed(os.path.join(HERE, f"{name}_manifest.npz"),
+                            manifest_names=np.array(names),
+                            manifest_shapes=np.array([",".join(map(str, s)) for s in shapes]),
+                            param_order=np.array(order))
+    print("written to", HERE)
+
+
+if __name__ == "__main__":
+    main()
