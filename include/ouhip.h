@@ -1,0 +1,317 @@
+/*
+ * ouhip.h -- C ABI of the MI355X (gfx950) kernels behind open_universe_amd's
+ * drop-in ``load_model()`` / ``model.enhance()`` surface.
+ *
+ * The reference (kolyangg/open-universe) is pure Python: its hot path is a
+ * sequence of ATen ops issued from ``Universe.enhance``
+ * (open_universe/networks/universe/universe.py:231-375) through the score and
+ * conditioner networks.  Each entry point below replaces a run of those ops;
+ * the reference interface it replaces is cited on each declaration.  The
+ * Python host (open_universe_amd/_lib.py) binds these with ctypes.
+ *
+ * Conventions
+ *  - All tensors are fp32 device pointers (caller-owned, hipMalloc'd or from
+ *    the torch caching allocator); sizes are element counts; activations are
+ *    NCW with the frame axis innermost (the reference's layout).
+ *  - ``stream`` is a hipStream_t passed as void* (0 = null stream).
+ *  - Every function returns 0 on success, a negative code on failure;
+ *    ou_last_error() returns a thread-local message.  Nothing allocates device
+ *    memory or synchronises, so every launch is hipGraph-capturable.
+ */
+#ifndef OUHIP_H
+#define OUHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OUHIP_ABI_VERSION 1
+
+int ou_abi_version(void);
+const char* ou_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * Fused implicit-GEMM 1-D convolution (kernels K1, K2, K3, K5, K8 of
+ * SURVEY.md section 2.3).  Replaces PReLU_Conv.forward
+ * (networks/universe/blocks.py:203-231) plus the ConvBlock arithmetic that
+ * follows it (blocks.py:353-416: (h+res)/sqrt2, (cond_out+input_cond)/sqrt2,
+ * film, conv stacks), the strided / transposed rate-change convolutions with
+ * their binomial anti-alias FIRs folded into the weights (blocks.py:123-134,
+ * 268-287), the 1x1 signal_cond_proj (score.py:166-171), the st_convs
+ * (condition.py:33-65), the GRU input projection and the STFT-as-GEMM of the
+ * mel front end (condition.py:85-108).
+ *
+ *   xv[c'][t] = prelu(in_scale[b] * x[b][c'/R][t*R + c'%R + shift])   (0 outside [0,in_len))
+ *   acc[m][u] = sum_{c',k} W[m][c'][k] * xv[c'][u + k - pad]          u in [0, n_frames)
+ *   m = ph*cout + co, t = u*rout + ph  (pixel shuffle; rout = 1 for plain convs)
+ *   v = acc + bias[co];  v = t < valid_len ? v : 0
+ *   v = (v + res1[b][co][t]) * s1;  v = film_g[b][co]*v + film_b[b][co];
+ *   v = (v + res2[b][co][t]) * s2;  y[b][co][t] = v   for t < out_len
+ * ---------------------------------------------------------------------- */
+typedef struct ou_conv_desc {
+    const float* x;            /* input signal                                   */
+    int64_t x_bstride;         /* elements between batch items                   */
+    int64_t x_cstride;         /* elements between channels                      */
+    int32_t cin;               /* underlying input channels                      */
+    int32_t in_len;            /* valid samples per channel                      */
+    int32_t frame;             /* R: frame-view factor (1 = plain NCW)           */
+    int32_t shift;             /* sample offset of frame 0                       */
+    const float* in_scale;     /* [B] per-item input multiplier, or NULL         */
+    float slope;               /* scalar PReLU slope (1.0 = identity)            */
+    const float* w;            /* weights packed by ou_conv_pack()               */
+    int32_t m;                 /* GEMM rows = rout * cout                        */
+    int32_t kt;                /* taps along frames: 1, 3, 4 or 5                */
+    int32_t pad;               /* left padding in frames                         */
+    int32_t cc;                /* channel chunk the weights were packed with     */
+    int32_t n_frames;          /* output frames u                                */
+    int32_t batch;
+    float* y;
+    int64_t y_bstride, y_cstride;
+    int32_t rout;              /* output phases (transposed conv), 1 otherwise   */
+    int32_t out_len;           /* store t < out_len                              */
+    int32_t valid_len;         /* t >= valid_len stored as 0 before res1         */
+    const float* bias;         /* [cout] or NULL                                 */
+    const float* res1;         /* residual 1 or NULL                             */
+    int64_t r1_bstride, r1_cstride;
+    float s1;
+    const float* film;         /* [B][2*cout] (gamma | beta) or NULL             */
+    int64_t film_bstride;
+    const float* res2;         /* residual 2 or NULL                             */
+    int64_t r2_bstride, r2_cstride;
+    float s2;
+    int32_t tile;              /* tile config (ou_conv_pick_tile), -1 = auto     */
+    int32_t _reserved;
+} ou_conv_desc;
+
+/* Pick the channel chunk for a layer: multiple of lcm(frame, 8). */
+int ou_conv_chunk(int kt, int frame);
+/* Number of floats of the packed weight buffer. */
+int64_t ou_conv_packed_size(int m, int cin_eff, int kt, int cc);
+/* Host-side packing: w_logical[m][cin_eff][kt] (row-major, host memory)
+ * -> packed[] in the per-lane MFMA fragment order the kernel streams. */
+int ou_conv_pack(const float* w_logical, int m, int cin_eff, int kt, int cc,
+                 float* packed);
+int ou_conv(const ou_conv_desc* d, void* stream);
+/* The tile configuration ou_conv would use for this descriptor (0..5). */
+int ou_conv_pick_tile(const ou_conv_desc* d);
+
+/* ------------------------------------------------------------------------
+ * Bidirectional GRU recurrence (kernel K6).  Replaces the recurrent part of
+ * torch.nn.GRU in ScoreEncoder (score.py:84-90,117-118) and
+ * ConditionerEncoder (condition.py:173-179,212-215).  The input projection
+ * gi = W_ih x + b_ih is produced beforehand by ou_conv (1x1) into
+ * gi[b][dir*3H + gate*H + j][t].  One persistent launch per layer: H/32
+ * workgroups per direction hold W_hh in registers and hand h_t between
+ * workgroups through 8-byte {tag, value} granules (bounded spins).
+ *   y[b][dir*H + j][t] = (h + res[b][dir*H + j][t]) * res_scale   (res optional)
+ * ---------------------------------------------------------------------- */
+typedef struct ou_gru_desc {
+    const float* gi;           /* [B][2*3H][T]                                    */
+    int64_t gi_bstride;
+    const float* w_hh;         /* [2][3H][H] (direction-major, torch layout)      */
+    const float* b_hh;         /* [2][3H]                                         */
+    float* y;                  /* [B][2H][T] (strides below)                      */
+    int64_t y_bstride, y_cstride;
+    const float* res;          /* optional residual, same layout as y             */
+    int64_t res_bstride, res_cstride;
+    float res_scale;
+    int32_t hidden;            /* H: 256 or 384                                   */
+    int32_t steps;             /* T                                               */
+    int32_t batch;
+    int32_t _pad;
+    uint64_t* granules;        /* workspace: ou_gru_workspace_bytes()             */
+    int32_t* status;           /* device int, set nonzero on spin timeout         */
+} ou_gru_desc;
+
+int64_t ou_gru_workspace_bytes(int hidden, int batch);
+int ou_gru(const ou_gru_desc* d, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Noise-level embedding + every FiLM projection of the score network for a
+ * list of sigma values (kernel K7).  Replaces SimpleTimeEmbedding /
+ * SigmaBlock (sigma_block.py:24-78) and the per-level
+ * Linear(noise_cond_dim -> 2C) calls (score.py:104-110,197-210).
+ *   g = embed(log10(sigma[i]));  out[i][r] = sum_k W[r][k] g[k] + bias[r]
+ * ---------------------------------------------------------------------- */
+typedef struct ou_embed_desc {
+    const float* sigma;        /* [n] noise levels (already scaled by edm.noise) */
+    int32_t n;
+    int32_t kind;              /* 0 = SimpleTimeEmbedding, 1 = SigmaBlock RFF    */
+    int32_t dim;               /* noise_cond_dim (512)                           */
+    float te_weight, te_bias;  /* SimpleTimeEmbedding scalars                    */
+    const float* rff_freq;     /* SigmaBlock: [n_rff]                            */
+    int32_t n_rff;
+    int32_t rows;              /* total projection rows                          */
+    const float* mlp_w[3];     /* SigmaBlock Linear weights (out x in)           */
+    const float* mlp_b[3];
+    float mlp_slope[3];
+    const float* w;            /* [rows][dim] concatenated projections           */
+    const float* bias;         /* [rows]                                         */
+    float* out;                /* [n][rows]                                      */
+    float* gbuf;               /* scratch [n][dim]                               */
+} ou_embed_desc;
+
+int ou_embed(const ou_embed_desc* d, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Score-network head fused with the EDM wrapper and the sampler update
+ * (kernel K9).  Replaces ScoreNetwork.forward's last two lines
+ * (score.py:290-296: prelu -> output_conv), Universe._edm_score_wrapper
+ * (universe.py:197-209) and the update lines of the diffusion loop
+ * (universe.py:334-343).
+ *   net = conv3(prelu2(prelu1(h)))[b][t] + bias
+ *   mode 0: out = net
+ *   else:   score = edm ? ((w_skip*x + w_out*net) - x) / s2 : net
+ *   mode 1: out = (x + c_score*score) + c_noise*(z*s_next)
+ *   mode 2: out = x + c_score*score
+ * ---------------------------------------------------------------------- */
+typedef struct ou_head_desc {
+    const float* h;            /* [B][C][T] decoder output                       */
+    int64_t h_bstride;
+    int32_t channels, length, batch, mode;
+    float slope1, slope2;
+    const float* w;            /* [C][3] folded output_conv weight               */
+    float bias;
+    int32_t edm, _pad;
+    float w_skip, w_out, s2, c_score, c_noise, s_next;
+    const float* x;            /* [B][T] current sample (may alias out)          */
+    const float* z;            /* [B][T] standard normal noise or NULL           */
+    float* out;                /* [B][T]                                         */
+} ou_head_desc;
+
+int ou_head(const ou_head_desc* d, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Row statistics and elementwise helpers around the sampler
+ * (kernel K9): normalize_batch (utils/norm.py:47-87), the mel
+ * normalization (condition.py:104-106), pad / unpad / peak-normalize /
+ * keep_rms (universe.py:259,267-270,349-357).
+ * ---------------------------------------------------------------------- */
+/* y[b][i] = (x[b][i] - mean_b) * (level / max(std_b, eps)); std unbiased. */
+int ou_normalize(const float* x, float* y, int batch, int64_t n, float level,
+                 float eps, void* stream);
+/* out[b] = 1 / max(sqrt(sum_i x[b][i]^2 / denom), eps)  (mel normalisation) */
+int ou_inv_rms(const float* x, float* out, int batch, int64_t n, float denom,
+               float eps, void* stream);
+/* out[b] = sqrt(mean_i x[b][i]^2)                                          */
+int ou_rms(const float* x, float* out, int batch, int64_t n, void* stream);
+/* y[b][f][t] = x[b][f][t]^2 + x[b][f+F][t]^2   (|STFT|^2 from re/im rows)   */
+int ou_power(const float* x, float* y, int batch, int nf, int frames, void* stream);
+/* y[b][t] = x[b][t - left] for t-left in [0, n_in), 0 otherwise; len n_out  */
+int ou_pad(const float* x, int64_t x_bstride, float* y, int batch, int n_in,
+           int n_out, int left, void* stream);
+/* y[i] = z[i] * scale (+ add[i])  (initial sample x0 = randn * sigma_0, or
+ * the warm start aux + randn * sigma_k, universe.py:322-331)              */
+int ou_scale(const float* z, float* y, int64_t n, float scale, const float* add,
+             void* stream);
+/* enhance() tail: crop [left, left+len) of x (stride x_bstride), optional
+ * keep_rms rescale (mix_rms[b] / max(rms(x_b), 1e-5)), then divide by the
+ * peak when it exceeds 1.                                                 */
+int ou_finish(const float* x, int64_t x_bstride, int left, float* y, int batch,
+              int len, const float* mix_rms, void* stream);
+/* Elementwise median / mean over an ensemble of E results, [E][n] -> [n]. */
+int ou_ensemble_reduce(const float* x, float* y, int ensemble, int64_t n,
+                       int mode /* 0 mean, 1 median */, void* stream);
+
+/* Alias-free Snake of the signal-decoupling layer (universe_gan.py:119-151;
+ * bigvgan/snake.py:131-157, alias_free_act.py:8-30): torchaudio-style 2x
+ * sinc up-sampling, Snake x + sin^2(a x)/(a + 1e-9), 2x down-sampling.  The
+ * Conv1d(C -> 1, k3) that follows is ou_head in mode 0 with unit slopes.
+ *   u[2s+i] = sum_k k_up[i][k] h[s+k-width_up];  y[t] = sum_k k_down[k] v[2t+k-width_down] */
+typedef struct ou_snake_desc {
+    const float* h;            /* [B][C][T]                                      */
+    int64_t h_bstride;
+    int32_t channels, length, batch, _pad0;
+    const float* alpha;        /* [C] exp(log_alpha)                             */
+    const float* k_up;         /* [2][taps_up]                                   */
+    int32_t taps_up, width_up;
+    const float* k_down;       /* [taps_down]                                    */
+    int32_t taps_down, width_down;
+    float* out;                /* [B][C][T]                                      */
+} ou_snake_desc;
+
+int ou_snake_aa(const ou_snake_desc* d, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Program: a recorded list of the launches above, replayed natively (and
+ * optionally as one hipGraph).  Built once per (shape, options) by the
+ * Python host; replaces the Python-level loop of Universe.enhance.
+ * ---------------------------------------------------------------------- */
+typedef struct ou_program ou_program;
+
+enum {
+    OU_OP_CONV = 1, OU_OP_GRU = 2, OU_OP_EMBED = 3, OU_OP_HEAD = 4,
+    OU_OP_NORMALIZE = 5, OU_OP_INV_RMS = 6, OU_OP_POWER = 7, OU_OP_PAD = 8,
+    OU_OP_SCALE = 9, OU_OP_FINISH = 10, OU_OP_RMS = 11, OU_OP_SNAKE = 12,
+    OU_OP_MEMSET = 13, OU_OP_ENSEMBLE = 14
+};
+
+/* Descriptors of the helper ops when recorded into a program. */
+typedef struct ou_memset_desc {
+    void* ptr;
+    int64_t bytes;
+} ou_memset_desc;
+typedef struct ou_norm_args {
+    const float* x;
+    float* y;
+    int32_t batch, _pad;
+    int64_t n;
+    float level, eps;
+} ou_norm_args;
+typedef struct ou_rms_args {
+    const float* x;
+    float* out;
+    int32_t batch, _pad;
+    int64_t n;
+    float denom, eps;
+} ou_rms_args;
+typedef struct ou_power_args {
+    const float* x;
+    float* y;
+    int32_t batch, nf, frames, _pad;
+} ou_power_args;
+typedef struct ou_pad_args {
+    const float* x;
+    int64_t x_bstride;
+    float* y;
+    int32_t batch, n_in, n_out, left;
+} ou_pad_args;
+typedef struct ou_scale_args {
+    const float* z;
+    float* y;
+    int64_t n;
+    float scale, _pad;
+    const float* add;
+} ou_scale_args;
+typedef struct ou_finish_args {
+    const float* x;
+    int64_t x_bstride;
+    int32_t left, batch, len, _pad;
+    float* y;
+    const float* mix_rms;
+} ou_finish_args;
+typedef struct ou_ensemble_args {
+    const float* x;
+    float* y;
+    int32_t ensemble, mode;
+    int64_t n;
+} ou_ensemble_args;
+
+ou_program* ou_program_create(void);
+void ou_program_destroy(ou_program* p);
+/* op-specific descriptor, copied into the program. */
+int ou_program_add(ou_program* p, int op, const void* desc, size_t desc_bytes);
+int ou_program_size(const ou_program* p);
+int ou_program_run(ou_program* p, void* stream);
+/* Capture the program into a hipGraph (on a private stream) and instantiate. */
+int ou_program_capture(ou_program* p);
+/* Launch the instantiated graph on ``stream``. */
+int ou_program_launch(ou_program* p, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OUHIP_H */

@@ -1,0 +1,250 @@
+"""ctypes binding of libouhip.so (the C ABI declared in include/ouhip.h).
+
+This is the "reference-side binding a maintainer would add": the reference is
+pure Python, so the natural FFI is ctypes over the C ABI.  The library is built
+in-tree (``__graft_entry__.build()`` / ``open_universe_amd/csrc/build.sh``) and
+loaded from ``open_universe_amd/libouhip.so``.  There is no fallback: if the
+library is missing, every compute entry point raises.
+"""
+import ctypes
+import os
+from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("OUHIP_LIB", os.path.join(_HERE, "libouhip.so"))
+ABI_VERSION = 1
+
+fp = c_void_p  # device pointers are passed as integers
+
+# op codes (ouhip.h)
+OP_CONV, OP_GRU, OP_EMBED, OP_HEAD = 1, 2, 3, 4
+OP_NORMALIZE, OP_INV_RMS, OP_POWER, OP_PAD = 5, 6, 7, 8
+OP_SCALE, OP_FINISH, OP_RMS, OP_SNAKE = 9, 10, 11, 12
+OP_MEMSET, OP_ENSEMBLE = 13, 14
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [
+        ("x", fp), ("x_bstride", c_int64), ("x_cstride", c_int64),
+        ("cin", c_int32), ("in_len", c_int32), ("frame", c_int32), ("shift", c_int32),
+        ("in_scale", fp), ("slope", c_float), ("w", fp),
+        ("m", c_int32), ("kt", c_int32), ("pad", c_int32), ("cc", c_int32),
+        ("n_frames", c_int32), ("batch", c_int32),
+        ("y", fp), ("y_bstride", c_int64), ("y_cstride", c_int64),
+        ("rout", c_int32), ("out_len", c_int32), ("valid_len", c_int32),
+        ("bias", fp),
+        ("res1", fp), ("r1_bstride", c_int64), ("r1_cstride", c_int64), ("s1", c_float),
+        ("film", fp), ("film_bstride", c_int64),
+        ("res2", fp), ("r2_bstride", c_int64), ("r2_cstride", c_int64), ("s2", c_float),
+        ("tile", c_int32), ("_reserved", c_int32),
+    ]
+
+
+class GruDesc(ctypes.Structure):
+    _fields_ = [
+        ("gi", fp), ("gi_bstride", c_int64), ("w_hh", fp), ("b_hh", fp),
+        ("y", fp), ("y_bstride", c_int64), ("y_cstride", c_int64),
+        ("res", fp), ("res_bstride", c_int64), ("res_cstride", c_int64),
+        ("res_scale", c_float), ("hidden", c_int32), ("steps", c_int32), ("batch", c_int32),
+        ("_pad", c_int32), ("granules", fp), ("status", fp),
+    ]
+
+
+class EmbedDesc(ctypes.Structure):
+    _fields_ = [
+        ("sigma", fp), ("n", c_int32), ("kind", c_int32), ("dim", c_int32),
+        ("te_weight", c_float), ("te_bias", c_float), ("rff_freq", fp), ("n_rff", c_int32),
+        ("rows", c_int32), ("mlp_w", fp * 3), ("mlp_b", fp * 3), ("mlp_slope", c_float * 3),
+        ("w", fp), ("bias", fp), ("out", fp), ("gbuf", fp),
+    ]
+
+
+class HeadDesc(ctypes.Structure):
+    _fields_ = [
+        ("h", fp), ("h_bstride", c_int64),
+        ("channels", c_int32), ("length", c_int32), ("batch", c_int32), ("mode", c_int32),
+        ("slope1", c_float), ("slope2", c_float), ("w", fp), ("bias", c_float),
+        ("edm", c_int32), ("_pad", c_int32),
+        ("w_skip", c_float), ("w_out", c_float), ("s2", c_float), ("c_score", c_float),
+        ("c_noise", c_float), ("s_next", c_float),
+        ("x", fp), ("z", fp), ("out", fp),
+    ]
+
+
+class SnakeDesc(ctypes.Structure):
+    _fields_ = [
+        ("h", fp), ("h_bstride", c_int64),
+        ("channels", c_int32), ("length", c_int32), ("batch", c_int32), ("_pad0", c_int32),
+        ("alpha", fp), ("k_up", fp), ("taps_up", c_int32), ("width_up", c_int32),
+        ("k_down", fp), ("taps_down", c_int32), ("width_down", c_int32), ("out", fp),
+    ]
+
+
+class MemsetArgs(ctypes.Structure):
+    _fields_ = [("ptr", fp), ("bytes", c_int64)]
+
+
+class NormArgs(ctypes.Structure):
+    _fields_ = [("x", fp), ("y", fp), ("batch", c_int32), ("_pad", c_int32), ("n", c_int64),
+                ("level", c_float), ("eps", c_float)]
+
+
+class RmsArgs(ctypes.Structure):
+    _fields_ = [("x", fp), ("out", fp), ("batch", c_int32), ("_pad", c_int32), ("n", c_int64),
+                ("denom", c_float), ("eps", c_float)]
+
+
+class PowerArgs(ctypes.Structure):
+    _fields_ = [("x", fp), ("y", fp), ("batch", c_int32), ("nf", c_int32),
+                ("frames", c_int32), ("_pad", c_int32)]
+
+
+class PadArgs(ctypes.Structure):
+    _fields_ = [("x", fp), ("x_bstride", c_int64), ("y", fp), ("batch", c_int32),
+                ("n_in", c_int32), ("n_out", c_int32), ("left", c_int32)]
+
+
+class ScaleArgs(ctypes.Structure):
+    _fields_ = [("z", fp), ("y", fp), ("n", c_int64), ("scale", c_float), ("_pad", c_float),
+                ("add", fp)]
+
+
+class FinishArgs(ctypes.Structure):
+    _fields_ = [("x", fp), ("x_bstride", c_int64), ("left", c_int32), ("batch", c_int32),
+                ("len", c_int32), ("_pad", c_int32), ("y", fp), ("mix_rms", fp)]
+
+
+class EnsembleArgs(ctypes.Structure):
+    _fields_ = [("x", fp), ("y", fp), ("ensemble", c_int32), ("mode", c_int32), ("n", c_int64)]
+
+
+OP_STRUCT = {
+    OP_CONV: ConvDesc, OP_GRU: GruDesc, OP_EMBED: EmbedDesc, OP_HEAD: HeadDesc,
+    OP_NORMALIZE: NormArgs, OP_INV_RMS: RmsArgs, OP_RMS: RmsArgs, OP_POWER: PowerArgs,
+    OP_PAD: PadArgs, OP_SCALE: ScaleArgs, OP_FINISH: FinishArgs, OP_SNAKE: SnakeDesc,
+    OP_MEMSET: MemsetArgs, OP_ENSEMBLE: EnsembleArgs,
+}
+
+# every symbol include/ouhip.h declares (checked by tests/test_abi.py)
+EXPORTS = {
+    "ou_abi_version": (c_int, []),
+    "ou_last_error": (ctypes.c_char_p, []),
+    "ou_conv_chunk": (c_int, [c_int, c_int]),
+    "ou_conv_packed_size": (c_int64, [c_int, c_int, c_int, c_int]),
+    "ou_conv_pack": (c_int, [POINTER(c_float), c_int, c_int, c_int, c_int, POINTER(c_float)]),
+    "ou_conv": (c_int, [POINTER(ConvDesc), c_void_p]),
+    "ou_conv_pick_tile": (c_int, [POINTER(ConvDesc)]),
+    "ou_gru_workspace_bytes": (c_int64, [c_int, c_int]),
+    "ou_gru": (c_int, [POINTER(GruDesc), c_void_p]),
+    "ou_embed": (c_int, [POINTER(EmbedDesc), c_void_p]),
+    "ou_head": (c_int, [POINTER(HeadDesc), c_void_p]),
+    "ou_normalize": (c_int, [fp, fp, c_int, c_int64, c_float, c_float, c_void_p]),
+    "ou_inv_rms": (c_int, [fp, fp, c_int, c_int64, c_float, c_float, c_void_p]),
+    "ou_rms": (c_int, [fp, fp, c_int, c_int64, c_void_p]),
+    "ou_power": (c_int, [fp, fp, c_int, c_int, c_int, c_void_p]),
+    "ou_pad": (c_int, [fp, c_int64, fp, c_int, c_int, c_int, c_int, c_void_p]),
+    "ou_scale": (c_int, [fp, fp, c_int64, c_float, fp, c_void_p]),
+    "ou_finish": (c_int, [fp, c_int64, c_int, fp, c_int, c_int, fp, c_void_p]),
+    "ou_ensemble_reduce": (c_int, [fp, fp, c_int, c_int64, c_int, c_void_p]),
+    "ou_snake_aa": (c_int, [POINTER(SnakeDesc), c_void_p]),
+    "ou_program_create": (c_void_p, []),
+    "ou_program_destroy": (None, [c_void_p]),
+    "ou_program_add": (c_int, [c_void_p, c_int, c_void_p, c_size_t]),
+    "ou_program_size": (c_int, [c_void_p]),
+    "ou_program_run": (c_int, [c_void_p, c_void_p]),
+    "ou_program_capture": (c_int, [c_void_p]),
+    "ou_program_launch": (c_int, [c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+class OuHipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libouhip.so (raises if it is missing -- no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OuHipError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
+            "g.build()'` or open_universe_amd/csrc/build.sh")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in EXPORTS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.ou_abi_version() != ABI_VERSION:
+        raise OuHipError("libouhip ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = load().ou_last_error()
+        raise OuHipError(f"{what}: ouhip error {rc}: {msg.decode() if msg else ''}")
+
+
+def conv_chunk(kt, frame):
+    return load().ou_conv_chunk(kt, frame)
+
+
+def conv_pack(w_logical, cc):
+    """w_logical: float32 numpy array [m][cin_eff][kt] -> packed numpy array."""
+    import numpy as np
+
+    w = np.ascontiguousarray(w_logical, dtype=np.float32)
+    m, cin, kt = w.shape
+    n = load().ou_conv_packed_size(m, cin, kt, cc)
+    out = np.empty(n, dtype=np.float32)
+    check(load().ou_conv_pack(w.ctypes.data_as(POINTER(c_float)), m, cin, kt, cc,
+                              out.ctypes.data_as(POINTER(c_float))), "conv_pack")
+    return out
+
+
+class Program:
+    """A recorded launch list (ou_program) with optional hipGraph replay."""
+
+    def __init__(self):
+        self.lib = load()
+        self.h = self.lib.ou_program_create()
+        self.keep = []          # tensors whose memory the program references
+        self.captured = False
+
+    def add(self, op, desc):
+        assert isinstance(desc, OP_STRUCT[op])
+        check(self.lib.ou_program_add(self.h, op, ctypes.byref(desc), ctypes.sizeof(desc)),
+              f"program_add(op={op})")
+
+    def __len__(self):
+        return self.lib.ou_program_size(self.h)
+
+    def run(self, stream):
+        check(self.lib.ou_program_run(self.h, c_void_p(stream)), "program_run")
+
+    def capture(self):
+        check(self.lib.ou_program_capture(self.h), "program_capture")
+        self.captured = True
+
+    def launch(self, stream):
+        check(self.lib.ou_program_launch(self.h, c_void_p(stream)), "program_launch")
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.ou_program_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def run_now(op, desc, stream):
+    """Launch one op immediately (used by layer-level tests)."""
+    lib = load()
+    fns = {OP_CONV: lib.ou_conv, OP_GRU: lib.ou_gru, OP_EMBED: lib.ou_embed,
+           OP_HEAD: lib.ou_head, OP_SNAKE: lib.ou_snake_aa}
+    check(fns[op](ctypes.byref(desc), c_void_p(stream)), f"op {op}")

@@ -1,0 +1,204 @@
+// ou_gru.hip -- bidirectional GRU recurrence for gfx950.
+//
+// Replaces the recurrent half of torch.nn.GRU(batch_first, bidirectional) in
+// ScoreEncoder (networks/universe/score.py:84-90,117-118) and
+// ConditionerEncoder (networks/universe/condition.py:173-179,212-215).  The
+// input projection gi = W_ih x + b_ih is one dense GEMM over all frames and is
+// done beforehand by ou_conv (1x1); this kernel runs the serial part:
+//   r = sig(gi_r + W_hr h + b_hr), z = sig(gi_z + W_hz h + b_hz)
+//   n = tanh(gi_n + r * (W_hn h + b_hn)),  h' = (1 - z) n + z h      (torch order)
+//
+// MI355X mapping.  W_hh is 3H x H fp32 = 786 KB per direction for H = 256 --
+// more than one CU's register file + LDS (512 KB + 160 KB).  So each direction
+// is split over G = H/32 workgroups ("a chain"); a workgroup owns 32 hidden
+// units, i.e. 96 rows of W_hh, held in VGPRs for the whole sequence (96 fp32
+// per lane at H = 256).  Per time step every workgroup needs the full h_{t-1}:
+// it is exchanged through 8-byte {tag = step + 1, value} granules written with
+// agent-scope relaxed (sc1) stores and polled with sc1 loads -- the payload is
+// its own flag, so no fence is needed (cdna_hip_programming.md Guideline 16,
+// recipe R2).  Granules are double-buffered by step parity, which is enough
+// because no workgroup can publish step t+2 before every workgroup has read
+// step t.  Spins are bounded; on timeout the kernel sets *status and exits.
+//
+// Lane layout inside a wave: lane = u*8 + kg: u = one of the wave's 8 hidden
+// units, kg = which H/8 slice of the dot product the lane owns.  The 3 partial
+// dot products are reduced across the 8 kg lanes with xor-shuffles.
+#include <hip/hip_runtime.h>
+
+#include "../../include/ouhip.h"
+#include "ou_common.h"
+
+namespace {
+
+constexpr int kUnitsPerWG = 32;
+constexpr int kMaxBatchPerWG = 4;
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+template <int H, int NB>
+__global__ __launch_bounds__(256) void gru_kernel(ou_gru_desc d, int nb)
+{
+    constexpr int KPL = H / 8;           // k-slice per lane
+    constexpr int SEG = KPL + 4;         // padded LDS segment (bank spread)
+    __shared__ __attribute__((aligned(16))) float hs[NB][8 * SEG];
+    __shared__ int abort_flag;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int kg = lane & 7;
+    const int u = lane >> 3;
+    const int j = blockIdx.x * kUnitsPerWG + wave * 8 + u;   // hidden unit
+    const int dir = blockIdx.y;
+    const int b0 = blockIdx.z * nb;
+    const int nbh = min(nb, d.batch - b0);
+    const int T = d.steps;
+    if (tid == 0) abort_flag = 0;
+
+    // W_hh rows of this unit (gates r, z, n), k-slice of this lane, in VGPRs
+    const float* wbase = d.w_hh + (int64_t)dir * 3 * H * H;
+    float wr[KPL], wz[KPL], wn[KPL];
+#pragma unroll
+    for (int k = 0; k < KPL; k += 4) {
+        const float4 a = *(const float4*)(wbase + (int64_t)(0 * H + j) * H + kg * KPL + k);
+        const float4 bq = *(const float4*)(wbase + (int64_t)(1 * H + j) * H + kg * KPL + k);
+        const float4 c = *(const float4*)(wbase + (int64_t)(2 * H + j) * H + kg * KPL + k);
+        wr[k] = a.x; wr[k + 1] = a.y; wr[k + 2] = a.z; wr[k + 3] = a.w;
+        wz[k] = bq.x; wz[k + 1] = bq.y; wz[k + 2] = bq.z; wz[k + 3] = bq.w;
+        wn[k] = c.x; wn[k + 1] = c.y; wn[k + 2] = c.z; wn[k + 3] = c.w;
+    }
+    const float bhr = d.b_hh[dir * 3 * H + 0 * H + j];
+    const float bhz = d.b_hh[dir * 3 * H + 1 * H + j];
+    const float bhn = d.b_hh[dir * 3 * H + 2 * H + j];
+
+    uint64_t* gran = d.granules;   // [B][2 dir][2 parity][H]
+    auto gidx = [&](int b, int par, int k) -> int64_t {
+        return (((int64_t)b * 2 + dir) * 2 + par) * H + k;
+    };
+
+    for (int t = 0; t < T; ++t) {
+        const int time = dir == 0 ? t : T - 1 - t;
+        // prefetch this step's input projections (only the kg==0 lanes use them)
+        float gir[NB], giz[NB], gin[NB];
+        if (kg == 0) {
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) {
+                if (bb >= nbh) break;
+                const float* g = d.gi + (int64_t)(b0 + bb) * d.gi_bstride +
+                                 (int64_t)(dir * 3 * H) * T + time;
+                gir[bb] = g[(int64_t)(0 * H + j) * T];
+                giz[bb] = g[(int64_t)(1 * H + j) * T];
+                gin[bb] = g[(int64_t)(2 * H + j) * T];
+            }
+        }
+        // gather h_{t-1}
+        if (t == 0) {
+            for (int i = tid; i < nbh * H; i += 256) {
+                const int bb = i / H, k = i - bb * H;
+                hs[bb][(k / KPL) * SEG + (k % KPL)] = 0.f;
+            }
+        } else {
+            const uint32_t want = (uint32_t)t;   // tag of h_{t-1}
+            const int par = (t - 1) & 1;
+            for (int i = tid; i < nbh * H; i += 256) {
+                const int bb = i / H, k = i - bb * H;
+                uint64_t* p = gran + gidx(b0 + bb, par, k);
+                uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                uint32_t spins = 0;
+                while ((uint32_t)(v >> 32) != want) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 22)) {   // ~seconds: the chain is dead
+                        atomicExch(d.status, 1);
+                        abort_flag = 1;
+                        break;
+                    }
+                    v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                hs[bb][(k / KPL) * SEG + (k % KPL)] = __uint_as_float((uint32_t)v);
+            }
+        }
+        __syncthreads();
+        if (abort_flag) return;   // uniform across the workgroup
+
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) {
+            if (bb >= nbh) break;
+            const float* hv = &hs[bb][kg * SEG];
+            float sr = 0.f, sz = 0.f, sn = 0.f;
+#pragma unroll
+            for (int k = 0; k < KPL; k += 4) {
+                const float4 hq = *(const float4*)(hv + k);
+                sr = fmaf(wr[k], hq.x, sr); sz = fmaf(wz[k], hq.x, sz); sn = fmaf(wn[k], hq.x, sn);
+                sr = fmaf(wr[k + 1], hq.y, sr); sz = fmaf(wz[k + 1], hq.y, sz); sn = fmaf(wn[k + 1], hq.y, sn);
+                sr = fmaf(wr[k + 2], hq.z, sr); sz = fmaf(wz[k + 2], hq.z, sz); sn = fmaf(wn[k + 2], hq.z, sn);
+                sr = fmaf(wr[k + 3], hq.w, sr); sz = fmaf(wz[k + 3], hq.w, sz); sn = fmaf(wn[k + 3], hq.w, sn);
+            }
+#pragma unroll
+            for (int off = 1; off < 8; off <<= 1) {
+                sr += __shfl_xor(sr, off);
+                sz += __shfl_xor(sz, off);
+                sn += __shfl_xor(sn, off);
+            }
+            if (kg == 0) {
+                const float hprev = hs[bb][(j / KPL) * SEG + (j % KPL)];
+                const float r = sigmoidf_(gir[bb] + (sr + bhr));
+                const float z = sigmoidf_(giz[bb] + (sz + bhz));
+                const float n = tanhf(gin[bb] + r * (sn + bhn));
+                const float hn = (1.0f - z) * n + z * hprev;
+                const int b = b0 + bb;
+                if (t + 1 < T) {
+                    const uint64_t g = ((uint64_t)(uint32_t)(t + 1) << 32) | __float_as_uint(hn);
+                    __hip_atomic_store(gran + gidx(b, t & 1, j), g, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+                float out = hn;
+                const int64_t c = (int64_t)(dir * H + j);
+                if (d.res)
+                    out = (hn + d.res[(int64_t)b * d.res_bstride + c * d.res_cstride + time]) *
+                          d.res_scale;
+                d.y[(int64_t)b * d.y_bstride + c * d.y_cstride + time] = out;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+extern "C" int64_t ou_gru_workspace_bytes(int hidden, int batch)
+{
+    return (int64_t)batch * 2 * 2 * hidden * sizeof(uint64_t);
+}
+
+extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
+{
+    if (!dp) return ou_fail(-1, "gru: null descriptor");
+    const ou_gru_desc& d = *dp;
+    if (!d.gi || !d.w_hh || !d.b_hh || !d.y || !d.granules || !d.status || d.steps <= 0 ||
+        d.batch <= 0)
+        return ou_fail(-1, "gru: invalid descriptor");
+    hipStream_t s = (hipStream_t)stream;
+    OU_HIP_CHECK(hipMemsetAsync(d.granules, 0, ou_gru_workspace_bytes(d.hidden, d.batch), s),
+                 "gru: memset");
+    const int nb = d.batch >= kMaxBatchPerWG ? kMaxBatchPerWG : (d.batch >= 2 ? 2 : 1);
+    dim3 grid(d.hidden / kUnitsPerWG, 2, (d.batch + nb - 1) / nb);
+    // every workgroup of a chain must be resident at once: at most a few
+    // hundred 256-thread workgroups, far below 256 CUs x 4.
+    if (grid.x * grid.y * grid.z > 512) return ou_fail(-2, "gru: grid too large for residency");
+#define OU_GRU_CASE(HH)                                                                \
+    case HH:                                                                           \
+        if (nb == 1) hipLaunchKernelGGL((gru_kernel<HH, 1>), grid, dim3(256), 0, s, d, nb); \
+        else if (nb == 2) hipLaunchKernelGGL((gru_kernel<HH, 2>), grid, dim3(256), 0, s, d, nb); \
+        else hipLaunchKernelGGL((gru_kernel<HH, 4>), grid, dim3(256), 0, s, d, nb);      \
+        break;
+    switch (d.hidden) {
+        OU_GRU_CASE(32)
+        OU_GRU_CASE(64)
+        OU_GRU_CASE(128)
+        OU_GRU_CASE(256)
+        OU_GRU_CASE(384)
+    default: return ou_fail(-1, "gru: unsupported hidden size %d", d.hidden);
+    }
+#undef OU_GRU_CASE
+    return ou_check_launch("gru");
+}

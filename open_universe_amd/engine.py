@@ -1,0 +1,675 @@
+"""MI355X execution engine for the UNIVERSE / UNIVERSE++ enhancement path.
+
+The engine turns a reference-named state dict into device-resident, pre-packed
+weights (weight norm folded, anti-alias FIRs folded into the rate-change
+convolutions, GEMM operands packed in MFMA fragment order) and records the
+whole ``enhance()`` launch sequence for one (batch, length, options) shape as
+an ``ou_program`` that is replayed natively or as one hipGraph.
+
+The layer walk mirrors the reference modules it replaces:
+  ConvBlock                networks/universe/blocks.py:234-416
+  ScoreNetwork / enc / dec networks/universe/score.py:27-298
+  ConditionerNetwork       networks/universe/condition.py:68-377
+  Universe.enhance         networks/universe/universe.py:231-375
+"""
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import dsp
+
+NF2 = np.float32(1.0 / math.sqrt(2.0))
+
+
+# ---------------------------------------------------------------------------
+# weights
+# ---------------------------------------------------------------------------
+def _np(t):
+    return t.detach().to("cpu", torch.float32).numpy()
+
+
+def fold_weight(sd, prefix):
+    """weight_norm(dim=0): w = v * (g / ||v||), norm over all dims but 0,
+    in float32 as torch._weight_norm does (blocks.py:40-46)."""
+    if prefix + ".weight_g" in sd:
+        g = sd[prefix + ".weight_g"].detach().to("cpu", torch.float32)
+        v = sd[prefix + ".weight_v"].detach().to("cpu", torch.float32)
+        n = v.reshape(v.shape[0], -1).norm(dim=1).reshape((-1,) + (1,) * (v.dim() - 1))
+        return (v * (g / n)).numpy()
+    return _np(sd[prefix + ".weight"])
+
+
+@dataclass
+class ConvW:
+    """A prepared convolution: packed weights + geometry (see ou_conv_desc)."""
+    m: int
+    cin: int
+    kt: int
+    frame: int
+    pad: int
+    rout: int
+    slope: float
+    cc: int
+    w: torch.Tensor
+    bias: Optional[torch.Tensor]
+    shift: int = 0
+
+    @property
+    def cout(self):
+        return self.m // self.rout
+
+
+@dataclass
+class ConvSpec:
+    """Logical (unpacked) convolution in the ou_conv formulation:
+    w[m][cin*frame][kt] over the frame view, plus geometry and epilogue bias."""
+    w: np.ndarray
+    cin: int
+    frame: int
+    pad: int
+    rout: int
+    slope: float
+    bias: Optional[np.ndarray]
+    shift: int = 0
+
+
+def make_conv(spec, device):
+    w_logical = np.ascontiguousarray(spec.w, dtype=np.float32)
+    m, cin_eff, kt = w_logical.shape
+    assert cin_eff == spec.cin * spec.frame, (cin_eff, spec.cin, spec.frame)
+    cc = L.conv_chunk(kt, spec.frame)
+    packed = torch.from_numpy(L.conv_pack(w_logical, cc)).to(device)
+    b = None if spec.bias is None else torch.from_numpy(np.ascontiguousarray(spec.bias, np.float32)).to(device)
+    return ConvW(m, spec.cin, kt, spec.frame, spec.pad, spec.rout, float(spec.slope), cc, packed, b,
+                 spec.shift)
+
+
+def _slope(sd, p):
+    return float(sd[p + ".prelu.weight"].reshape(-1)[0])
+
+
+def _bias(sd, key):
+    b = sd.get(key)
+    return None if b is None else _np(b)
+
+
+def spec_same(sd, p, k):
+    """PReLU_Conv(C, C, k, padding='same') (blocks.py:293-316)."""
+    w = fold_weight(sd, p + ".conv")
+    return ConvSpec(w, w.shape[1], 1, (k - 1) // 2, 1, _slope(sd, p), _bias(sd, p + ".conv.bias"))
+
+
+def spec_plain(sd, p, k, slope=1.0):
+    """Plain Conv1d (no activation): input_conv, 1x1 signal_cond_proj, mel conv."""
+    w = fold_weight(sd, p)
+    return ConvSpec(w, w.shape[1], 1, (k - 1) // 2, 1, slope, _bias(sd, p + ".bias"))
+
+
+def spec_down(sd, p, r, antialias):
+    """Strided PReLU_Conv(C, 2C, r, stride=r) (blocks.py:203-231, 268-275).
+    Frame view: channel c' = ci*r + p.  With anti-aliasing the 2r+1-tap
+    binomial FIR (applied before the conv, blocks.py:217-218) is folded into a
+    3r-tap kernel = 3 frames (-1, 0, +1)."""
+    w = fold_weight(sd, p + ".conv")  # (Cout, Cin, r)
+    cout, cin, _ = w.shape
+    if antialias:
+        fir = dsp.binomial_taps(2 * r + 1).astype(np.float64)
+        wf = np.zeros((cout, cin, 3 * r), dtype=np.float64)
+        for kk in range(r):
+            wf[:, :, kk:kk + 2 * r + 1] += w[:, :, kk:kk + 1].astype(np.float64) * fir[None, None, :]
+        wl = wf.reshape(cout, cin, 3, r).transpose(0, 1, 3, 2).reshape(cout, cin * r, 3)
+        return ConvSpec(wl, cin, r, 1, 1, _slope(sd, p), _bias(sd, p + ".bias"))
+    return ConvSpec(w.reshape(cout, cin * r, 1), cin, r, 0, 1, _slope(sd, p),
+                    _bias(sd, p + ".conv.bias"))
+
+
+def spec_up(sd, p, r, antialias):
+    """Transposed PReLU_Conv(2C, C, r, stride=r) (+ FIR after, blocks.py:221-225)
+    as a polyphase convolution over input frames producing r*C rows that the
+    kernel's epilogue pixel-shuffles.  weight_norm dim 0 of a ConvTranspose1d
+    weight (Cin, Cout, r) is per input channel; fold_weight handles it."""
+    w = fold_weight(sd, p + ".conv").astype(np.float64)  # (Cin, Cout, r)
+    cin, cout, _ = w.shape
+    if antialias:
+        fir = dsp.binomial_taps(2 * r + 1).astype(np.float64)
+        wl = np.zeros((r, cout, cin, 3), dtype=np.float64)
+        for ph in range(r):
+            for j in range(2 * r + 1):
+                s_ = ph + j - r
+                d = s_ // r
+                e = s_ - d * r
+                wl[ph, :, :, d + 1] += fir[j] * w[:, :, e].T
+        return ConvSpec(wl.reshape(r * cout, cin, 3), cin, 1, 1, r, _slope(sd, p), _bias(sd, p + ".bias"))
+    wl = w.transpose(2, 1, 0).reshape(r * cout, cin, 1)
+    return ConvSpec(wl, cin, 1, 0, r, _slope(sd, p), _bias(sd, p + ".conv.bias"))
+
+
+def prep_same(sd, p, k, device):
+    return make_conv(spec_same(sd, p, k), device)
+
+
+def prep_plain(sd, p, k, device, slope=1.0):
+    return make_conv(spec_plain(sd, p, k, slope), device)
+
+
+def prep_down(sd, p, r, antialias, device):
+    return make_conv(spec_down(sd, p, r, antialias), device)
+
+
+def prep_strided(sd, p, r, device):
+    """st_convs: PReLU_Conv(Ci, Co, r, stride=r), no FIR (condition.py:53-59)."""
+    return make_conv(spec_down(sd, p, r, False), device)
+
+
+def prep_up(sd, p, r, antialias, device):
+    return make_conv(spec_up(sd, p, r, antialias), device)
+
+
+@dataclass
+class BlockW:
+    """ConvBlock weights (blocks.py:234-351)."""
+    C: int
+    kind: str
+    rate: Optional[int]
+    conv1: ConvW
+    conv2: ConvW
+    conv3: ConvW
+    rate_conv: Optional[ConvW] = None
+
+
+def prep_block(sd, p, kind, rate, antialias, device):
+    c1 = prep_same(sd, p + ".conv1", 5, device)
+    c2 = prep_same(sd, p + ".conv2", 3, device)
+    c3 = prep_same(sd, p + ".conv3", 3, device)
+    rc = None
+    if kind == "down":
+        rc = prep_down(sd, p + ".rate_change_conv", rate, antialias, device)
+    elif kind == "up":
+        rc = prep_up(sd, p + ".rate_change_conv", rate, antialias, device)
+    return BlockW(c1.m, kind, rate, c1, c2, c3, rc)
+
+
+@dataclass
+class GruW:
+    hidden: int
+    layers: List  # per layer: (ConvW input projection, w_hh dev [2][3H][H], b_hh dev [2][3H])
+
+
+def prep_gru(sd, p, num_layers, device):
+    layers = []
+    for l in range(num_layers):
+        s, sr = f"_l{l}", f"_l{l}_reverse"
+        w_ih = np.concatenate([_np(sd[p + ".weight_ih" + s]), _np(sd[p + ".weight_ih" + sr])], 0)
+        b_ih = np.concatenate([_np(sd[p + ".bias_ih" + s]), _np(sd[p + ".bias_ih" + sr])], 0)
+        proj = make_conv(ConvSpec(w_ih[:, :, None], w_ih.shape[1], 1, 0, 1, 1.0, b_ih), device)
+        w_hh = torch.stack([sd[p + ".weight_hh" + s], sd[p + ".weight_hh" + sr]]).float().contiguous().to(device)
+        b_hh = torch.stack([sd[p + ".bias_hh" + s], sd[p + ".bias_hh" + sr]]).float().contiguous().to(device)
+        layers.append((proj, w_hh, b_hh))
+    H = int(sd[p + ".weight_hh_l0"].shape[1])
+    return GruW(H, layers)
+
+
+# ---------------------------------------------------------------------------
+# activations
+# ---------------------------------------------------------------------------
+class Act:
+    """A (B, C, T) fp32 device tensor viewed as pointer + strides."""
+
+    def __init__(self, t):
+        assert t.dtype == torch.float32 and t.dim() == 3
+        self.t = t
+        self.ptr = t.data_ptr()
+        self.bs, self.cs = t.stride(0), t.stride(1)
+        self.B, self.C, self.T = t.shape
+
+
+def new_act(B, C, T, device):
+    return Act(torch.empty((B, C, T), dtype=torch.float32, device=device))
+
+
+def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=None,
+              valid_len=None, in_scale=0, res1: Act = None, s1=1.0, film=0, film_bs=0,
+              res2: Act = None, s2=1.0, batch=None):
+    d = L.ConvDesc()
+    d.x, d.x_bstride, d.x_cstride = x.ptr, x.bs, x.cs
+    d.cin, d.in_len = cw.cin, x.T if in_len is None else in_len
+    d.frame, d.shift = cw.frame, cw.shift
+    d.in_scale, d.slope = in_scale or 0, cw.slope
+    d.w, d.m, d.kt, d.pad, d.cc = cw.w.data_ptr(), cw.m, cw.kt, cw.pad, cw.cc
+    if n_frames is None:
+        n_frames = -(-d.in_len // cw.frame) if cw.rout == 1 else x.T
+    d.n_frames = n_frames
+    d.batch = x.B if batch is None else batch
+    d.y, d.y_bstride, d.y_cstride = y.ptr, y.bs, y.cs
+    d.rout = cw.rout
+    d.out_len = y.T if out_len is None else out_len
+    d.valid_len = (1 << 30) if valid_len is None else valid_len
+    d.bias = cw.bias.data_ptr() if cw.bias is not None else 0
+    if res1 is not None:
+        d.res1, d.r1_bstride, d.r1_cstride, d.s1 = res1.ptr, res1.bs, res1.cs, s1
+    d.film, d.film_bstride = film or 0, film_bs
+    if res2 is not None:
+        d.res2, d.r2_bstride, d.r2_cstride, d.s2 = res2.ptr, res2.bs, res2.cs, s2
+    d.tile = -1
+    # shape guards: the kernel trusts these (an out-of-bounds store faults the GPU)
+    assert x.C == cw.cin, ("conv input channels", x.C, cw.cin)
+    assert y.C == cw.cout, ("conv output channels", y.C, cw.cout)
+    assert 0 < d.in_len <= x.T, ("conv in_len", d.in_len, x.T)
+    assert 0 < d.out_len <= y.T, ("conv out_len", d.out_len, y.T)
+    assert d.batch <= min(x.B, y.B)
+    for r in (res1, res2):
+        if r is not None:
+            assert r.C == cw.cout and r.T >= d.out_len and r.B >= d.batch, ("residual", r.t.shape)
+    return d
+
+
+def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film_bs=0,
+              sc: Act = None, res2: Act = None, s2=1.0, cond_out: Act = None, skip_tail=False):
+    """ConvBlock main stage (blocks.py:393-407):
+       cond_out = conv1(h); c = (cond_out + sc)/sqrt2; c = film(c); c = conv3(conv2(c));
+       out = (h + c)/sqrt2 [; out = (out + res2) * s2]"""
+    c1_out = cond_out if cond_out is not None else tA
+    prog.add(L.OP_CONV, conv_desc(bw.conv1, h, c1_out, res1=sc, s1=NF2, film=film, film_bs=film_bs))
+    if skip_tail:
+        return
+    prog.add(L.OP_CONV, conv_desc(bw.conv2, c1_out, tB))
+    prog.add(L.OP_CONV, conv_desc(bw.conv3, tB, out, res1=h, s1=NF2, res2=res2, s2=s2))
+
+
+def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, res: Act = None,
+            res_scale=1.0):
+    proj, w_hh, b_hh = gw.layers[layer]
+    H = gw.hidden
+    assert gi.C == 6 * H and gi.T == x.T and y.C == 2 * H and y.T == x.T and y.B == x.B
+    if res is not None:
+        assert res.C == 2 * H and res.T == x.T
+    assert granules.numel() * 8 >= L.load().ou_gru_workspace_bytes(H, x.B)
+    prog.add(L.OP_CONV, conv_desc(proj, x, gi))
+    d = L.GruDesc()
+    d.gi, d.gi_bstride = gi.ptr, gi.bs
+    d.w_hh, d.b_hh = w_hh.data_ptr(), b_hh.data_ptr()
+    d.y, d.y_bstride, d.y_cstride = y.ptr, y.bs, y.cs
+    if res is not None:
+        d.res, d.res_bstride, d.res_cstride, d.res_scale = res.ptr, res.bs, res.cs, res_scale
+    d.hidden, d.steps, d.batch = gw.hidden, x.T, x.B
+    d.granules, d.status = granules.data_ptr(), status.data_ptr()
+    prog.add(L.OP_GRU, d)
+
+
+def level_lengths(T, rates):
+    Ts = [T]
+    for r in rates:
+        Ts.append(-(-Ts[-1] // r))
+    return Ts
+
+
+# ---------------------------------------------------------------------------
+# engine
+# ---------------------------------------------------------------------------
+class Engine:
+    def __init__(self, model_cfg, sd, device, parts=("score", "cond", "sdl"), _record_only=False):
+        self.device = torch.device(device)
+        if self.device.type != "cuda" and not _record_only:
+            raise L.OuHipError("open_universe_amd runs on a HIP device (got %s)" % device)
+        L.load()
+        self.cfg = model_cfg
+        self.scfg = model_cfg.get("score_model")
+        self.ccfg = model_cfg.get("condition_model")
+        self.edm = model_cfg.get("edm")
+        self.level_db = (model_cfg.get("normalization_kwargs") or {}).get("level_db", 0.0)
+        base = self.scfg if self.scfg is not None else self.ccfg
+        self.rates = list(base["rate_factors"])
+        self.nch = base["n_channels"]
+        self.extra = base.get("extra_conv_block", False)
+        if not self.extra:
+            raise NotImplementedError("the HIP engine targets extra_conv_block=True configs")
+        self.tot_ds = math.prod(self.rates)
+        sp = "_edm_model" if self.edm is not None else "score_model"
+        dev = self.device
+        self.has_sdl = False
+        with torch.no_grad():
+            if "score" in parts:
+                self._prep_score(sd, sp, dev)
+            if "cond" in parts:
+                self._prep_cond(sd, "condition_model", dev)
+            if "sdl" in parts:
+                self._prep_sdl(sd, "signal_decoupling_layer", dev)
+        self.status = torch.zeros(4, dtype=torch.int32, device=dev)
+
+    # -------------------------------------------------------------- weights
+    def _prep_score(self, sd, p, dev):
+        cfg = self.scfg
+        aa = cfg.get("use_antialiasing", False)
+        rates = self.rates
+        n_lvl = len(rates) + (1 if self.extra else 0)
+        self.s_input = prep_plain(sd, p + ".input_conv", cfg.get("fb_kernel_size", 3), dev)
+        self.s_enc = []
+        for i in range(n_lvl):
+            q = f"{p}.encoder.ds_modules.{i}"
+            if i < len(rates):
+                self.s_enc.append(prep_block(sd, q, "down", rates[i], aa, dev))
+            else:
+                self.s_enc.append(prep_block(sd, q, "none", None, aa, dev))
+        self.s_gru = prep_gru(sd, p + ".encoder.gru", 1, dev)
+        ups = rates[::-1]
+        self.s_dec, self.s_sc = [], []
+        for l in range(n_lvl):
+            q = f"{p}.decoder.up_modules.{l}"
+            if self.extra and l == 0:
+                self.s_dec.append(prep_block(sd, q, "none", None, aa, dev))
+            else:
+                self.s_dec.append(prep_block(sd, q, "up", ups[l - (1 if self.extra else 0)], aa, dev))
+            self.s_sc.append(prep_plain(sd, f"{p}.decoder.signal_cond_proj.{l}", 1, dev))
+        # FiLM projections, concatenated: encoder levels then decoder levels
+        ws, bs, self.film_off = [], [], []
+        off = 0
+        for name in [f"{p}.encoder.cond_proj.{i}" for i in range(n_lvl)] + \
+                    [f"{p}.decoder.noise_cond_proj.{l}" for l in range(n_lvl)]:
+            w = fold_weight(sd, name)
+            ws.append(w)
+            bs.append(_np(sd[name + ".bias"]))
+            self.film_off.append(off)
+            off += w.shape[0]
+        self.film_rows = off
+        self.emb_w = torch.from_numpy(np.concatenate(ws, 0)).to(dev).contiguous()
+        self.emb_b = torch.from_numpy(np.concatenate(bs, 0)).to(dev).contiguous()
+        self.emb_dim = self.emb_w.shape[1]
+        te = cfg.get("time_embedding")
+        self.emb_kind = 0 if te == "simple" else 1
+        if self.emb_kind == 0:
+            self.te_w = float(sd[p + ".sigma_block.weight"].reshape(-1)[0])
+            self.te_b = float(sd[p + ".sigma_block.bias"].reshape(-1)[0])
+        else:
+            q = p + ".sigma_block"
+            self.rff = sd[q + ".freq"].float().contiguous().to(dev)
+            self.mlp = [(sd[f"{q}.layer{i}.lin.weight"].float().contiguous().to(dev),
+                         sd[f"{q}.layer{i}.lin.bias"].float().contiguous().to(dev),
+                         _slope(sd, f"{q}.layer{i}")) for i in (1, 2, 3)]
+        # head: score.prelu -> output_conv (PReLU_Conv C -> 1, k3)
+        self.head_s1 = float(sd[p + ".prelu.weight"].reshape(-1)[0])
+        self.head_s2 = _slope(sd, p + ".output_conv")
+        self.head_w = torch.from_numpy(fold_weight(sd, p + ".output_conv.conv").reshape(-1).copy()).to(dev)
+        hb = sd.get(p + ".output_conv.conv.bias")
+        self.head_b = 0.0 if hb is None else float(hb.reshape(-1)[0])
+        assert fold_weight(sd, p + ".output_conv.conv").shape[0] == 1
+
+    def _prep_cond(self, sd, p, dev):
+        cfg = self.ccfg
+        rates = list(cfg["rate_factors"])
+        aa_dec = cfg.get("use_antialiasing", False)
+        n_lvl = len(rates) + (1 if cfg.get("extra_conv_block", False) else 0)
+        self.c_extra = cfg.get("extra_conv_block", False)
+        self.c_gru_res = cfg.get("encoder_gru_residual", False)
+        # mel front end (condition.py:68-114)
+        ds = math.prod(rates)
+        n_fft = cfg.get("n_mel_oversample", 4) * ds
+        self.mel_hop, self.mel_nfft = ds, n_fft
+        self.mel_nmels = cfg.get("n_mels", 80)
+        nfreq = n_fft // 2 + 1
+        self.mel_nfreq = nfreq
+        self.mel_pl = (n_fft - ds) // 2
+        win = dsp.hann_periodic(n_fft).astype(np.float64)
+        n = np.arange(n_fft)
+        f = np.arange(nfreq)
+        ang = 2.0 * math.pi * np.outer(f, n) / n_fft
+        dft = np.concatenate([win * np.cos(ang), win * np.sin(ang)], 0)  # (2F, n_fft)
+        kt = n_fft // ds
+        # w_logical[m][p][kk] = dft[m][kk*hop + p]
+        wl = dft.reshape(2 * nfreq, kt, ds).transpose(0, 2, 1)
+        self.c_stft = make_conv(ConvSpec(wl, 1, ds, 0, 1, 1.0, None, shift=-self.mel_pl), dev)
+        fb = dsp.melscale_fbanks(nfreq, 0.0, float(24000 // 2), self.mel_nmels, 24000)
+        self.c_fb = make_conv(ConvSpec(fb.T[:, :, None], nfreq, 1, 0, 1, 1.0, None), dev)
+        self.c_melconv = prep_plain(sd, p + ".input_mel.conv", 3, dev)
+        self.c_melblock = prep_block(sd, p + ".input_mel.conv_block", "none", None, False, dev)
+        self.c_input = prep_plain(sd, p + ".input_conv", cfg.get("fb_kernel_size", 3), dev)
+        self.c_enc, self.c_st = [], []
+        st_rates = [rates[-1]]
+        for r in rates[-2::-1]:
+            st_rates.append(st_rates[-1] * r)
+        self.c_st_rates = st_rates[::-1]
+        for i in range(n_lvl):
+            q = f"{p}.encoder.ds_modules.{i}"
+            if i < len(rates):
+                self.c_enc.append(prep_block(sd, q, "down", rates[i], False, dev))
+            else:
+                self.c_enc.append(prep_block(sd, q, "none", None, False, dev))
+            if i < len(rates) - 1:
+                self.c_st.append(prep_strided(sd, f"{p}.encoder.st_convs.{i}", self.c_st_rates[i], dev))
+        self.c_cb1 = prep_block(sd, p + ".encoder.conv_block1", "none", None, False, dev)
+        self.c_cb2 = prep_block(sd, p + ".encoder.conv_block2", "none", None, False, dev)
+        self.c_gru = prep_gru(sd, p + ".encoder.gru", 2, dev)
+        self.c_dec_in = prep_block(sd, p + ".decoder.input_conv_block", "none", None, False, dev)
+        ups = rates[::-1]
+        self.c_dec = []
+        for l in range(n_lvl):
+            q = f"{p}.decoder.up_modules.{l}"
+            if self.c_extra and l == 0:
+                self.c_dec.append(prep_block(sd, q, "none", None, False, dev))
+            else:
+                self.c_dec.append(prep_block(sd, q, "up", ups[l - (1 if self.c_extra else 0)], aa_dec, dev))
+
+    def _prep_sdl(self, sd, p, dev):
+        self.has_sdl = (p + ".conv.weight") in sd
+        if not self.has_sdl:
+            return
+        a = sd[p + ".prelu.act.act.alpha"].float()
+        self.sdl_alpha = torch.exp(a).contiguous().to(dev)
+        ku, wu = dsp.sinc_resample_kernel(1, 2)
+        kd, wd = dsp.sinc_resample_kernel(2, 1)
+        self.sdl_kup = torch.from_numpy(ku.reshape(-1).copy()).to(dev)
+        self.sdl_kdown = torch.from_numpy(kd.reshape(-1).copy()).to(dev)
+        self.sdl_taps = (ku.shape[1], wu, kd.shape[1], wd)
+        self.sdl_w = sd[p + ".conv.weight"].float().reshape(-1).contiguous().to(dev)
+        self.sdl_b = float(sd[p + ".conv.bias"].reshape(-1)[0])
+
+    # -------------------------------------------------------------- buffers
+    def alloc_score(self, B, T):
+        dev = self.device
+        Ts = level_lengths(T, self.rates)
+        n_lvl = len(self.s_enc)
+        Cs = [self.nch * 2 ** i for i in range(len(self.rates) + 1)]
+        bufs = {"T": Ts, "C": Cs}
+        for i in range(n_lvl):
+            li = min(i, len(self.rates))
+            for k in ("E", "A", "B", "V"):
+                bufs[f"{k}{i}"] = new_act(B, Cs[li], Ts[li], dev)
+        H = self.s_gru.hidden
+        bufs["GI"] = new_act(B, 6 * H, Ts[len(self.rates)], dev)
+        bufs["gran"] = torch.zeros(L.load().ou_gru_workspace_bytes(H, B) // 8, dtype=torch.int64, device=dev)
+        return bufs
+
+    def score_levels(self):
+        """decoder level l -> encoder level index i it mirrors."""
+        n = len(self.s_enc)
+        return [n - 1 - l for l in range(n)]
+
+    def rec_score(self, prog, bufs, x: Act, film_base, film_bs, in_scale=0, sc_list=None):
+        """ScoreNetwork.forward up to (not including) the head
+        (score.py:278-290).  Returns the decoder output Act."""
+        n_lvl = len(self.s_enc)
+        nr = len(self.rates)
+        fb = lambda j: film_base + 4 * self.film_off[j]
+        # input conv (score.py:244-246, 285)
+        prog.add(L.OP_CONV, conv_desc(self.s_input, x, bufs["E0"], in_scale=in_scale))
+        # encoder (score.py:105-115)
+        for i in range(n_lvl):
+            bw = self.s_enc[i]
+            rec_block(prog, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
+                      film=fb(i), film_bs=film_bs)
+            if bw.kind == "down":
+                prog.add(L.OP_CONV, conv_desc(bw.rate_conv, bufs[f"V{i}"], bufs[f"E{i+1}"]))
+        # bottleneck GRU, fused with the decoder's first residual add
+        top = n_lvl - 1
+        rec_gru(prog, self.s_gru, 0, bufs[f"V{top}"], bufs["GI"], bufs[f"V{top}"],
+                bufs["gran"], self.status, res=bufs[f"V{top}"], res_scale=NF2)
+        # decoder (score.py:197-211)
+        h = None
+        for l in range(n_lvl):
+            i = top - l
+            bw = self.s_dec[l]
+            if bw.kind == "up":
+                li = min(i, nr)
+                prog.add(L.OP_CONV, conv_desc(bw.rate_conv, h, bufs[f"V{i}"], n_frames=h.T,
+                                              out_len=bufs["T"][li], valid_len=bw.rate * h.T,
+                                              res1=bufs[f"V{i}"], s1=NF2))
+            rec_block(prog, bw, bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
+                      film=fb(n_lvl + l), film_bs=film_bs, sc=sc_list[l])
+            h = bufs[f"A{i}"]
+        return h
+
+    def rec_sc(self, prog, conds, scs):
+        for l, (c, s) in enumerate(zip(conds, scs)):
+            prog.add(L.OP_CONV, conv_desc(self.s_sc[l], c, s))
+
+    def alloc_sc(self, B, T):
+        Ts = level_lengths(T, self.rates)
+        n_lvl = len(self.s_enc)
+        out = []
+        for l in range(n_lvl):
+            i = n_lvl - 1 - l
+            li = min(i, len(self.rates))
+            out.append(new_act(B, self.s_dec[l].C, Ts[li], self.device))
+        return out
+
+    def rec_embed(self, prog, sigma_dev, n, film_out, gbuf):
+        d = L.EmbedDesc()
+        d.sigma, d.n, d.kind, d.dim = sigma_dev.data_ptr(), n, self.emb_kind, self.emb_dim
+        if self.emb_kind == 0:
+            d.te_weight, d.te_bias = self.te_w, self.te_b
+        else:
+            d.rff_freq, d.n_rff = self.rff.data_ptr(), self.rff.numel()
+            for k, (w, b, s) in enumerate(self.mlp):
+                d.mlp_w[k], d.mlp_b[k], d.mlp_slope[k] = w.data_ptr(), b.data_ptr(), s
+        d.rows = self.film_rows
+        d.w, d.bias, d.out, d.gbuf = self.emb_w.data_ptr(), self.emb_b.data_ptr(), film_out.data_ptr(), gbuf.data_ptr()
+        prog.add(L.OP_EMBED, d)
+
+    def head_desc(self, h: Act, out_ptr, B, T, mode=0, x_ptr=0, z_ptr=0, coef=None):
+        d = L.HeadDesc()
+        d.h, d.h_bstride = h.ptr, h.bs
+        d.channels, d.length, d.batch, d.mode = h.C, T, B, mode
+        d.slope1, d.slope2 = self.head_s1, self.head_s2
+        d.w, d.bias = self.head_w.data_ptr(), self.head_b
+        d.edm = 1 if self.edm is not None else 0
+        if coef:
+            for k, v in coef.items():
+                setattr(d, k, float(v))
+        d.x, d.z, d.out = x_ptr, z_ptr, out_ptr
+        return d
+
+    # -------------------------------------------------------------- conditioner
+    def alloc_cond(self, B, T, need_aux=False):
+        dev = self.device
+        rates = list(self.ccfg["rate_factors"])
+        Ts = level_lengths(T, rates)
+        Cs = [self.ccfg["n_channels"] * 2 ** i for i in range(len(rates) + 1)]
+        U = -(-T // self.mel_hop)
+        bufs = {"T": Ts, "C": Cs, "U": U}
+        bufs["SPEC"] = new_act(B, 2 * self.mel_nfreq, U, dev)
+        bufs["POW"] = new_act(B, self.mel_nfreq, U, dev)
+        bufs["MEL"] = new_act(B, self.mel_nmels, U, dev)
+        bufs["INV"] = torch.empty(B, dtype=torch.float32, device=dev)
+        CL = Cs[-1]
+        for k in ("M0", "MA", "MB", "XMEL", "SUM", "OUT", "LA", "LB", "CB1", "G1", "G2", "H", "D0", "Y4"):
+            bufs[k] = new_act(B, CL, U, dev)
+        n_lvl = len(self.c_enc)
+        for i in range(len(rates)):
+            for k in ("E", "A", "B", "V"):
+                bufs[f"{k}{i}"] = new_act(B, Cs[i], Ts[i], dev)
+        bufs[f"E{len(rates)}"] = new_act(B, CL, Ts[len(rates)], dev)
+        H = self.c_gru.hidden
+        bufs["GI"] = new_act(B, 6 * H, U, dev)
+        bufs["gran"] = torch.zeros(L.load().ou_gru_workspace_bytes(H, B) // 8, dtype=torch.int64, device=dev)
+        # decoder: conditions per level + Y (block outputs) per level
+        conds, ys = [], []
+        for l in range(n_lvl):
+            i = n_lvl - 1 - l
+            li = min(i, len(rates))
+            C = self.c_dec[l].C
+            conds.append(new_act(B, C, Ts[li], dev))
+            ys.append(new_act(B, C, Ts[li], dev))
+        bufs["COND"] = conds
+        bufs["Y"] = ys
+        bufs["HUP"] = [new_act(B, self.c_dec[l].C, Ts[min(n_lvl - 1 - l, len(rates))], dev) for l in range(n_lvl)]
+        bufs["TB"] = [new_act(B, self.c_dec[l].C, Ts[min(n_lvl - 1 - l, len(rates))], dev) for l in range(n_lvl)]
+        return bufs
+
+    def rec_cond(self, prog, bufs, x: Act, need_aux=False):
+        """ConditionerNetwork.forward (condition.py:346-377)."""
+        rates = list(self.ccfg["rate_factors"])
+        nr = len(rates)
+        n_lvl = len(self.c_enc)
+        B, U = x.B, bufs["U"]
+        # MelAdapter (condition.py:85-114): |STFT|^2 -> mel -> global norm -> conv -> ConvBlock
+        prog.add(L.OP_CONV, conv_desc(self.c_stft, x, bufs["SPEC"], n_frames=U))
+        pa = L.PowerArgs(x=bufs["SPEC"].ptr, y=bufs["POW"].ptr, batch=B, nf=self.mel_nfreq, frames=U)
+        prog.add(L.OP_POWER, pa)
+        prog.add(L.OP_CONV, conv_desc(self.c_fb, bufs["POW"], bufs["MEL"]))
+        ra = L.RmsArgs(x=bufs["MEL"].ptr, out=bufs["INV"].data_ptr(), batch=B,
+                       n=self.mel_nmels * U, denom=float(U), eps=1e-5)
+        prog.add(L.OP_INV_RMS, ra)
+        prog.add(L.OP_CONV, conv_desc(self.c_melconv, bufs["MEL"], bufs["M0"], in_scale=bufs["INV"].data_ptr()))
+        rec_block(prog, self.c_melblock, bufs["M0"], bufs["XMEL"], bufs["MA"], bufs["MB"])
+        # encoder (condition.py:189-220)
+        prog.add(L.OP_CONV, conv_desc(self.c_input, x, bufs["E0"]))
+        nsum = 0
+        for i in range(n_lvl):
+            bw = self.c_enc[i]
+            if i < nr:
+                rec_block(prog, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"])
+                prog.add(L.OP_CONV, conv_desc(bw.rate_conv, bufs[f"V{i}"], bufs[f"E{i+1}"]))
+                if i < nr - 1:
+                    prev = bufs["XMEL"] if nsum == 0 else bufs["SUM"]
+                    prog.add(L.OP_CONV, conv_desc(self.c_st[i], bufs[f"V{i}"], bufs["SUM"],
+                                                  n_frames=U, res1=prev, s1=1.0))
+                    nsum += 1
+            else:
+                n_out = nsum + 1
+                nf = np.float32(1.0 / math.sqrt(n_out + 1))
+                rec_block(prog, bw, bufs[f"E{i}"], bufs["OUT"], bufs["LA"], bufs["LB"],
+                          res2=bufs["SUM"], s2=nf)
+        if not self.c_extra:
+            raise NotImplementedError("conditioner without extra_conv_block")
+        rec_block(prog, self.c_cb1, bufs["OUT"], bufs["CB1"], bufs["LA"], bufs["LB"])
+        rec_gru(prog, self.c_gru, 0, bufs["CB1"], bufs["GI"], bufs["G1"], bufs["gran"], self.status)
+        res = bufs["CB1"] if self.c_gru_res else None
+        rec_gru(prog, self.c_gru, 1, bufs["G1"], bufs["GI"], bufs["G2"], bufs["gran"], self.status,
+                res=res, res_scale=NF2)
+        rec_block(prog, self.c_cb2, bufs["G2"], bufs["H"], bufs["LA"], bufs["LB"])
+        # decoder (condition.py:264-270)
+        rec_block(prog, self.c_dec_in, bufs["H"], bufs["D0"], bufs["LA"], bufs["LB"])
+        h = bufs["D0"]
+        for l in range(n_lvl):
+            bw = self.c_dec[l]
+            i = n_lvl - 1 - l
+            li = min(i, nr)
+            if bw.kind == "up":
+                hup = bufs["HUP"][l]
+                prog.add(L.OP_CONV, conv_desc(bw.rate_conv, h, hup, n_frames=h.T,
+                                              out_len=bufs["T"][li], valid_len=bw.rate * h.T))
+                h = hup
+            last = l == n_lvl - 1
+            rec_block(prog, bw, h, bufs["Y"][l], None, bufs["TB"][l], cond_out=bufs["COND"][l],
+                      skip_tail=last and not need_aux)
+            h = bufs["Y"][l]
+        return bufs["COND"], bufs["Y"][-1]
+
+    # -------------------------------------------------------------- aux path
+    def rec_aux(self, prog, y: Act, tmp: Act, out_ptr, B, T):
+        """UniverseGAN.aux_to_wav (universe_gan.py:147-151)."""
+        d = L.SnakeDesc()
+        d.h, d.h_bstride = y.ptr, y.bs
+        d.channels, d.length, d.batch = y.C, T, B
+        tu, wu, td, wd = self.sdl_taps
+        d.alpha, d.k_up, d.taps_up, d.width_up = self.sdl_alpha.data_ptr(), self.sdl_kup.data_ptr(), tu, wu
+        d.k_down, d.taps_down, d.width_down, d.out = self.sdl_kdown.data_ptr(), td, wd, tmp.ptr
+        prog.add(L.OP_SNAKE, d)
+        h = L.HeadDesc()
+        h.h, h.h_bstride, h.channels, h.length, h.batch, h.mode = tmp.ptr, tmp.bs, tmp.C, T, B, 0
+        h.slope1 = h.slope2 = 1.0
+        h.w, h.bias, h.out = self.sdl_w.data_ptr(), self.sdl_b, out_ptr
+        prog.add(L.OP_HEAD, h)

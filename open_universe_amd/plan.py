@@ -1,0 +1,245 @@
+"""Launch plans: one recorded ``ou_program`` per (shape, options).
+
+* :class:`EnhancePlan`   -- Universe.enhance (universe.py:231-375), whole sampler
+* :class:`ScorePlan`     -- ScoreNetwork.forward (score.py:278-298)
+* :class:`CondPlan`      -- ConditionerNetwork.forward (condition.py:346-377)
+
+Buffers are allocated once per plan (caller-owned device memory from the torch
+allocator); the recorded program holds raw pointers into them, so a plan can be
+replayed as a single hipGraph.  All arithmetic on the sampler's scalars
+(sigma schedule, EDM weights, update coefficients) is done here once, in
+float32 exactly as the reference's tensor ops round them.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .engine import Act, new_act
+
+f32 = np.float32
+
+
+def sigma_schedule(diff, n_steps):
+    """get_std_dev over the reversed linspace (universe.py:307-311,380-386),
+    evaluated with float32 tensor ops like the reference."""
+    if diff.get("schedule", "geometric") != "geometric":
+        raise NotImplementedError()
+    time = torch.linspace(0, 1, n_steps, dtype=torch.float32).flip(dims=[0])
+    s_min, s_max = diff["sigma_min"], diff["sigma_max"]
+    return (s_min * (s_max / s_min) ** time).numpy().astype(np.float32)
+
+
+def edm_weights(s, level_db, data_level_db=None):
+    """_get_edm_weights (universe.py:175-189) for a float32 sigma."""
+    lvl = level_db if data_level_db is None else data_level_db
+    sd = 10.0 ** (lvl / 20.0)
+    s = f32(s)
+    s2 = f32(s * s)
+    den = f32(s2 + f32(sd**2))
+    sn = f32(np.sqrt(den))
+    return {
+        "skip": f32(f32(sd**2) / den),
+        "in": f32(f32(1.0) / sn),
+        "out": f32(f32(s * f32(sd)) / sn),
+    }
+
+
+class _PlanBase:
+    def __init__(self, eng):
+        self.eng = eng
+        self.dev = eng.device
+        self.prog = L.Program()
+
+    def _launch(self, stream, use_graph):
+        if use_graph:
+            if not self.prog.captured:
+                self.prog.capture()
+            self.prog.launch(stream)
+        else:
+            self.prog.run(stream)
+
+    def check(self):
+        st = self.eng.status
+        if int(st.max().item()) != 0:
+            st.zero_()
+            raise L.OuHipError("GRU recurrence timed out (workgroup hand-off never completed)")
+
+
+class EnhancePlan(_PlanBase):
+    """The whole enhance() for a fixed (batch, length, n_steps, options)."""
+
+    def __init__(self, eng, batch, mix_len, n_steps, epsilon, keep_rms=False,
+                 use_aux_signal=False, warm_start=None, diff=None):
+        super().__init__(eng)
+        dev, B = self.dev, batch
+        self.B, self.mix_len, self.n_steps = B, mix_len, n_steps
+        tot = eng.tot_ds
+        self.pad = tot - mix_len % tot
+        Tp = mix_len + self.pad
+        self.Tp = Tp
+        self.use_aux = use_aux_signal
+        self.warm = warm_start
+        diff = diff or eng.cfg["diffusion"]
+        # sampler constants (universe.py:301-305)
+        delta_t = 1.0 / (n_steps - 1)
+        gamma = (diff["sigma_max"] / diff["sigma_min"]) ** -delta_t
+        eta = 1 - gamma**epsilon
+        beta = math.sqrt(1 - gamma ** (2 * (epsilon - 1.0)))
+        sig = sigma_schedule(diff, n_steps)
+        self.sigma = sig
+        edm = eng.edm
+        n_start = 0 if warm_start is None else int(warm_start)
+        self.n_start = n_start
+        # buffers
+        self.MIX = torch.empty((B, 1, mix_len), dtype=torch.float32, device=dev)
+        self.XP = new_act(B, 1, Tp, dev)
+        self.XN = new_act(B, 1, Tp, dev)
+        self.X = new_act(B, 1, Tp, dev)
+        n_noise = 0 if use_aux_signal else 1 + (n_steps - 1 - n_start)
+        self.n_noise = n_noise
+        self.NZ = torch.empty((max(n_noise, 1), B, 1, Tp), dtype=torch.float32, device=dev)
+        self.OUT = torch.empty((B, mix_len), dtype=torch.float32, device=dev)
+        self.MIXRMS = torch.empty(B, dtype=torch.float32, device=dev)
+        cb = eng.alloc_cond(B, Tp, need_aux=use_aux_signal or warm_start is not None)
+        self.cb = cb
+        p = self.prog
+        # ---- record ----
+        mixact = Act(self.MIX)
+        if keep_rms:
+            p.add(L.OP_RMS, L.RmsArgs(x=mixact.ptr, out=self.MIXRMS.data_ptr(), batch=B,
+                                      n=mix_len, denom=float(mix_len), eps=0.0))
+        p.add(L.OP_PAD, L.PadArgs(x=mixact.ptr, x_bstride=mix_len, y=self.XP.ptr, batch=B,
+                                  n_in=mix_len, n_out=Tp, left=self.pad // 2))
+        level = 10 ** (eng.level_db / 20.0)
+        p.add(L.OP_NORMALIZE, L.NormArgs(x=self.XP.ptr, y=self.XN.ptr, batch=B, n=Tp,
+                                         level=level, eps=1e-5))
+        conds, yaux = eng.rec_cond(p, cb, self.XN, need_aux=use_aux_signal or warm_start is not None)
+        if use_aux_signal or warm_start is not None:
+            self.AUXT = new_act(B, yaux.C, Tp, dev)
+            self.SIG = new_act(B, 1, Tp, dev)
+            if eng.has_sdl:
+                eng.rec_aux(p, yaux, self.AUXT, self.SIG.ptr, B, Tp)
+            else:
+                raise NotImplementedError("aux signal without a signal-decoupling layer")
+        if use_aux_signal:
+            x_final = self.SIG
+        else:
+            self.SC = eng.alloc_sc(B, Tp)
+            eng.rec_sc(p, conds, self.SC)
+            # FiLM parameters for every step at once (noise embedding, K7)
+            steps = list(range(n_start, n_steps))
+            snet = np.array([(f32(edm["noise"]) * sig[n]) if edm is not None else sig[n]
+                             for n in range(n_steps)], dtype=np.float32)
+            self.SNET = torch.from_numpy(snet).to(dev)
+            self.FILM = torch.empty((n_steps, eng.film_rows), dtype=torch.float32, device=dev)
+            self.GBUF = torch.empty((n_steps, eng.emb_dim), dtype=torch.float32, device=dev)
+            eng.rec_embed(p, self.SNET, n_steps, self.FILM, self.GBUF)
+            win = np.ones((n_steps, B), dtype=np.float32)
+            coefs = []
+            for n in range(n_steps):
+                s_now = f32(sig[n])
+                c = {"s2": f32(s_now * s_now)}
+                if edm is not None:
+                    w = edm_weights(s_now, eng.level_db, edm.get("data_level_db"))
+                    win[n, :] = w["in"]
+                    c.update(w_skip=w["skip"], w_out=w["out"])
+                if n < n_steps - 1:
+                    c.update(c_score=f32(f32(s_now * s_now) * f32(eta)), c_noise=f32(beta),
+                             s_next=f32(sig[n + 1]))
+                else:
+                    c.update(c_score=f32(s_now * s_now))
+                coefs.append(c)
+            self.WIN = torch.from_numpy(win).to(dev)
+            self.sb = eng.alloc_score(B, Tp)
+            # initial sample (universe.py:322-331)
+            if warm_start is None:
+                p.add(L.OP_SCALE, L.ScaleArgs(z=self.NZ.data_ptr(), y=self.X.ptr, n=B * Tp,
+                                              scale=float(sig[0]), add=0))
+            else:
+                p.add(L.OP_SCALE, L.ScaleArgs(z=self.NZ.data_ptr(), y=self.X.ptr, n=B * Tp,
+                                              scale=float(sig[n_start]), add=self.SIG.ptr))
+            film_base = self.FILM.data_ptr()
+            zi = 1
+            for n in steps:
+                in_scale = self.WIN[n].data_ptr() if edm is not None else 0
+                h = eng.rec_score(p, self.sb, self.X, film_base + 4 * n * eng.film_rows, 0,
+                                  in_scale=in_scale, sc_list=self.SC)
+                last = n == n_steps - 1
+                z_ptr = 0 if last else self.NZ[zi].data_ptr()
+                zi += 0 if last else 1
+                p.add(L.OP_HEAD, eng.head_desc(h, self.X.ptr, B, Tp, mode=2 if last else 1,
+                                               x_ptr=self.X.ptr, z_ptr=z_ptr, coef=coefs[n]))
+            x_final = self.X
+        p.add(L.OP_FINISH, L.FinishArgs(x=x_final.ptr, x_bstride=Tp, left=self.pad // 2,
+                                        batch=B, len=mix_len, y=self.OUT.data_ptr(),
+                                        mix_rms=self.MIXRMS.data_ptr() if keep_rms else 0))
+
+    def draw_noise(self, rng):
+        """Noise in the reference's draw order (universe.py:39-41,326,338):
+        x0 first, then one z per intermediate step."""
+        shape = (self.B, 1, self.Tp)
+        for k in range(self.n_noise):
+            if rng is not None and rng.device != self.NZ.device:
+                z = torch.randn(shape, generator=rng, device=rng.device, dtype=torch.float32)
+                self.NZ[k].copy_(z, non_blocking=False)
+            else:
+                torch.randn(shape, generator=rng, out=self.NZ[k])
+
+    def __call__(self, mix, rng=None, use_graph=True):
+        assert mix.shape == (self.B, 1, self.mix_len), mix.shape
+        self.MIX.copy_(mix)
+        self.draw_noise(rng)
+        stream = torch.cuda.current_stream(self.dev).cuda_stream
+        self._launch(stream, use_graph)
+        self.check()
+        return self.OUT
+
+
+class ScorePlan(_PlanBase):
+    """ScoreNetwork.forward(x, sigma, cond) for a fixed (B, T)."""
+
+    def __init__(self, eng, B, T):
+        super().__init__(eng)
+        dev = self.dev
+        self.B, self.T = B, T
+        self.XIN = new_act(B, 1, T, dev)
+        self.SIG = torch.empty(B, dtype=torch.float32, device=dev)
+        self.OUT = new_act(B, 1, T, dev)
+        self.SC = eng.alloc_sc(B, T)
+        self.CIN = [new_act(B, s.C, s.T, dev) for s in self.SC]
+        self.FILM = torch.empty((B, eng.film_rows), dtype=torch.float32, device=dev)
+        self.GBUF = torch.empty((B, eng.emb_dim), dtype=torch.float32, device=dev)
+        self.sb = eng.alloc_score(B, T)
+        p = self.prog
+        eng.rec_embed(p, self.SIG, B, self.FILM, self.GBUF)
+        eng.rec_sc(p, self.CIN, self.SC)
+        h = eng.rec_score(p, self.sb, self.XIN, self.FILM.data_ptr(), eng.film_rows, sc_list=self.SC)
+        p.add(L.OP_HEAD, eng.head_desc(h, self.OUT.ptr, B, T, mode=0))
+
+    def __call__(self, x, sigma, cond, use_graph=False):
+        self.XIN.t.copy_(x)
+        self.SIG.copy_(sigma.reshape(-1).to(torch.float32))
+        for dst, src in zip(self.CIN, cond):
+            dst.t.copy_(src)
+        self._launch(torch.cuda.current_stream(self.dev).cuda_stream, use_graph)
+        self.check()
+        return self.OUT.t
+
+
+class CondPlan(_PlanBase):
+    """ConditionerNetwork.forward(x, train=True) for a fixed (B, T)."""
+
+    def __init__(self, eng, B, T, need_aux=True):
+        super().__init__(eng)
+        self.B, self.T = B, T
+        self.XIN = new_act(B, 1, T, self.dev)
+        self.cb = eng.alloc_cond(B, T, need_aux=need_aux)
+        self.conds, self.y = eng.rec_cond(self.prog, self.cb, self.XIN, need_aux=need_aux)
+
+    def __call__(self, x, use_graph=False):
+        self.XIN.t.copy_(x)
+        self._launch(torch.cuda.current_stream(self.dev).cuda_stream, use_graph)
+        self.check()
+        return [c.t for c in self.conds], self.y.t, self.cb["H"].t

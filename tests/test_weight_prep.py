@@ -1,0 +1,166 @@
+"""CPU checks of the weight folding that feeds the HIP conv kernel.
+
+The kernel computes (include/ouhip.h, ou_conv):
+    xv[c'][t] = prelu(x[c'/R][t*R + c'%R + shift]);  acc[m][u] = sum W[m][c'][k] xv[c'][u+k-pad]
+    then pixel shuffle (m = ph*cout + co -> t = u*rout + ph) and bias.
+Here that formulation is emulated in float64 with the engine's logical
+weights (ConvSpec) and compared with the oracle's restatement of the reference
+op sequence (PReLU -> FIR -> strided conv, PReLU -> ConvTranspose -> FIR, ...).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden_state_dict, load_golden
+from open_universe_amd import engine as E
+from open_universe_amd import dsp
+from oracle import ou_oracle as O
+
+
+def emulate(spec, x, n_frames, out_len, valid_len=None, in_scale=None):
+    x = x.double()
+    B, Cin, T = x.shape
+    R, kt = spec.frame, spec.w.shape[2]
+    ts = torch.arange(-spec.pad, n_frames - spec.pad + kt - 1)
+    xv = torch.zeros(B, Cin * R, len(ts), dtype=torch.float64)
+    for c in range(Cin * R):
+        ci, p = divmod(c, R)
+        pos = ts * R + p + spec.shift
+        ok = (pos >= 0) & (pos < T)
+        xv[:, c, ok] = x[:, ci, pos[ok]]
+    if in_scale is not None:
+        xv = xv * in_scale
+    xv = torch.where(xv >= 0, xv, xv * spec.slope)
+    acc = F.conv1d(xv, torch.from_numpy(np.asarray(spec.w, np.float64)))
+    m = acc.shape[1]
+    cout = m // spec.rout
+    y = acc.reshape(B, spec.rout, cout, n_frames).permute(0, 2, 3, 1).reshape(B, cout, -1)
+    if spec.bias is not None:
+        y = y + torch.from_numpy(np.asarray(spec.bias, np.float64))[None, :, None]
+    if valid_len is not None and valid_len < y.shape[-1]:
+        y[..., valid_len:] = 0
+    if y.shape[-1] < out_len:
+        y = F.pad(y, (0, out_len - y.shape[-1]))
+    return y[..., :out_len]
+
+
+@pytest.fixture(scope="module")
+def sd():
+    d = load_golden("pp16_c4")
+    return {k: v.double() for k, v in golden_state_dict(d).items()}
+
+
+def _x(B, C, T, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(B, C, T, generator=g, dtype=torch.float64)
+
+
+def test_binomial_taps_match_reference_values():
+    # SURVEY.md 8(a) A9 (values from the reference's get_binomial_filter)
+    np.testing.assert_allclose(dsp.binomial_taps(5)[:3], [0.267261, 1.069045, 1.603567], atol=1e-6)
+    np.testing.assert_allclose(dsp.binomial_taps(11)[:4], [0.007716, 0.077161, 0.347224, 0.92593],
+                               atol=1e-6)
+    for k in (5, 7, 9, 11, 17):
+        np.testing.assert_allclose(dsp.binomial_taps(k), O.get_binomial_filter(k).numpy(), rtol=1e-6)
+
+
+@pytest.mark.parametrize("k,name", [(5, "conv1"), (3, "conv2")])
+def test_same_conv(sd, k, name):
+    p = f"_edm_model.encoder.ds_modules.1.{name}"
+    x = _x(2, 8, 37)
+    spec = E.spec_same(sd, p, k)
+    y = emulate(spec, x, 37, 37)
+    ref = O.prelu_conv(sd, p, x, k, padding="same")
+    torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("lvl,r", [(0, 2), (1, 4), (3, 5)])
+@pytest.mark.parametrize("T", [40, 43])
+def test_down_conv_with_fir(sd, lvl, r, T):
+    p = f"_edm_model.encoder.ds_modules.{lvl}.rate_change_conv"
+    C = 4 * 2**lvl
+    x = _x(2, C, T, seed=lvl)
+    spec = E.spec_down(sd, p, r, True)
+    U = -(-T // r)
+    y = emulate(spec, x, U, U)
+    ref = O.prelu_conv(sd, p, x, r, stride=r, antialias=True)
+    torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("lvl,r", [(1, 5), (2, 4), (4, 2)])
+@pytest.mark.parametrize("extra_len", [0, -3])
+def test_up_conv_with_fir(sd, lvl, r, extra_len):
+    p = f"_edm_model.decoder.up_modules.{lvl}.rate_change_conv"
+    Cin = 2 * sd[p + ".conv.weight_v"].shape[1]
+    Tin = 11
+    x = _x(2, sd[p + ".conv.weight_v"].shape[0], Tin, seed=lvl)
+    spec = E.spec_up(sd, p, r, True)
+    length = r * Tin + extra_len
+    y = emulate(spec, x, Tin, length, valid_len=r * Tin)
+    ref = O.prelu_conv(sd, p, x, r, stride=r, transpose=True, antialias=True)
+    ref = F.pad(ref, (0, length - ref.shape[-1]))
+    torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-6)
+
+
+def test_up_conv_plain(sd):
+    p = "condition_model.decoder.up_modules.2.rate_change_conv"
+    x = _x(1, sd[p + ".conv.weight_v"].shape[0], 9)
+    spec = E.spec_up(sd, p, 4, False)
+    y = emulate(spec, x, 9, 36)
+    ref = O.prelu_conv(sd, p, x, 4, stride=4, transpose=True)
+    torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("i,r", [(0, 160), (1, 80), (2, 20)])
+def test_st_convs(sd, i, r):
+    p = f"condition_model.encoder.st_convs.{i}"
+    C = 4 * 2**i
+    T = 3 * r + 7
+    x = _x(1, C, T)
+    spec = E.spec_down(sd, p, r, False)
+    U = -(-T // r)
+    y = emulate(spec, x, U, U)
+    ref = O.prelu_conv(sd, p, x, r, stride=r)
+    torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-6)
+
+
+def test_mel_front_end_as_gemm():
+    """STFT as a framed GEMM (R = hop, 4 frames) + |.|^2 + filterbank GEMM equals
+    the (restated) torchaudio MelSpectrogram on the padded signal
+    (condition.py:85-102)."""
+    hop, nfft, nmels = 160, 640, 80
+    T = 160 * 12
+    x = _x(2, 1, T)
+    pl = (nfft - hop) // 2
+    nfreq = nfft // 2 + 1
+    win = dsp.hann_periodic(nfft).astype(np.float64)
+    n = np.arange(nfft)
+    ang = 2 * math.pi * np.outer(np.arange(nfreq), n) / nfft
+    dft = np.concatenate([win * np.cos(ang), win * np.sin(ang)], 0)
+    wl = dft.reshape(2 * nfreq, nfft // hop, hop).transpose(0, 2, 1)
+    spec = E.ConvSpec(wl, 1, hop, 0, 1, 1.0, None, shift=-pl)
+    U = T // hop
+    s = emulate(spec, x, U, U)
+    power = s[:, :nfreq] ** 2 + s[:, nfreq:] ** 2
+    fb = torch.from_numpy(dsp.melscale_fbanks(nfreq, 0.0, 12000.0, nmels, 24000).astype(np.float64))
+    mel = torch.einsum("bft,fm->bmt", power, fb)
+    xp = F.pad(x, (pl, nfft - hop - pl))
+    ref = O.mel_spectrogram(xp, nfft, hop, nmels).squeeze(1)
+    torch.testing.assert_close(mel, ref, rtol=5e-5, atol=1e-6)
+
+
+def test_mel_fbank_matches_oracle():
+    np.testing.assert_allclose(dsp.melscale_fbanks(321, 0.0, 12000.0, 80, 24000),
+                               O.melscale_fbanks(321, 0.0, 12000.0, 80, 24000).numpy(),
+                               rtol=1e-5, atol=1e-7)
+
+
+def test_resample_kernels_match_oracle():
+    for o, n in ((1, 2), (2, 1)):
+        k, w = dsp.sinc_resample_kernel(o, n)
+        k2, w2, _, _ = O._sinc_resample_kernel(o, n)
+        assert w == w2
+        np.testing.assert_allclose(k, k2.reshape(k.shape).numpy(), rtol=1e-6, atol=1e-7)
