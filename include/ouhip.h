@@ -310,6 +310,12 @@ int ou_program_run(ou_program* p, void* stream);
 int ou_program_capture(ou_program* p);
 /* Launch the instantiated graph on ``stream``. */
 int ou_program_launch(ou_program* p, void* stream);
+/* Kind (OU_OP_*) of op i. */
+int ou_program_op_kind(const ou_program* p, int i);
+/* Eager replay with a hipEvent pair around every op on ``stream``; writes the
+ * per-op device time in milliseconds to ms[0..size) (synchronises).  Used by
+ * bench.py to attribute time to kernels inside the same workload. */
+int ou_program_profile(ou_program* p, void* stream, float* ms);
 
 #ifdef __cplusplus
 }

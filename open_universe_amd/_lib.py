@@ -154,6 +154,8 @@ EXPORTS = {
     "ou_program_run": (c_int, [c_void_p, c_void_p]),
     "ou_program_capture": (c_int, [c_void_p]),
     "ou_program_launch": (c_int, [c_void_p, c_void_p]),
+    "ou_program_op_kind": (c_int, [c_void_p, c_int]),
+    "ou_program_profile": (c_int, [c_void_p, c_void_p, POINTER(c_float)]),
 }
 
 _lib = None
@@ -214,11 +216,13 @@ class Program:
         self.h = self.lib.ou_program_create()
         self.keep = []          # tensors whose memory the program references
         self.captured = False
+        self.flops = []         # algorithmic FLOPs of the reference ops each op replaces
 
     def add(self, op, desc):
         assert isinstance(desc, OP_STRUCT[op])
         check(self.lib.ou_program_add(self.h, op, ctypes.byref(desc), ctypes.sizeof(desc)),
               f"program_add(op={op})")
+        self.flops.append(float(getattr(desc, "_flops", 0.0)))
 
     def __len__(self):
         return self.lib.ou_program_size(self.h)
@@ -232,6 +236,16 @@ class Program:
 
     def launch(self, stream):
         check(self.lib.ou_program_launch(self.h, c_void_p(stream)), "program_launch")
+
+    def op_kinds(self):
+        return [self.lib.ou_program_op_kind(self.h, i) for i in range(len(self))]
+
+    def profile(self, stream):
+        """Eager replay with an event pair around each op -> per-op ms."""
+        n = len(self)
+        buf = (c_float * n)()
+        check(self.lib.ou_program_profile(self.h, c_void_p(stream), buf), "program_profile")
+        return list(buf)
 
     def __del__(self):
         try:

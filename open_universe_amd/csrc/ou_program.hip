@@ -182,4 +182,36 @@ int ou_program_launch(ou_program* p, void* stream)
     return 0;
 }
 
+int ou_program_op_kind(const ou_program* p, int i)
+{
+    if (!p || i < 0 || i >= (int)p->ops.size()) return -1;
+    return p->ops[i].kind;
+}
+
+int ou_program_profile(ou_program* p, void* stream, float* ms)
+{
+    if (!p || !ms) return ou_fail(-1, "program_profile: null");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t n = p->ops.size();
+    std::vector<hipEvent_t> ev(n + 1);
+    for (auto& e : ev) OU_HIP_CHECK(hipEventCreate(&e), "event create");
+    int rc = 0;
+    (void)hipEventRecord(ev[0], s);
+    for (size_t i = 0; i < n && rc == 0; ++i) {
+        rc = run_op(p->ops[i].kind, p->ops[i].desc.data(), s);
+        (void)hipEventRecord(ev[i + 1], s);
+    }
+    if (rc == 0) {
+        hipError_t e = hipEventSynchronize(ev[n]);
+        if (e != hipSuccess) rc = ou_fail(-100, "profile sync: %s", hipGetErrorString(e));
+    }
+    for (size_t i = 0; i < n && rc == 0; ++i) {
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, ev[i], ev[i + 1]);
+        ms[i] = t;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    return rc;
+}
+
 }  // extern "C"

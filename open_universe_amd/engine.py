@@ -57,6 +57,7 @@ class ConvW:
     w: torch.Tensor
     bias: Optional[torch.Tensor]
     shift: int = 0
+    ref_macs: float = 0.0
 
     @property
     def cout(self):
@@ -75,6 +76,7 @@ class ConvSpec:
     slope: float
     bias: Optional[np.ndarray]
     shift: int = 0
+    ref_macs: float = 0.0   # MACs of the replaced reference ops per output frame
 
 
 def make_conv(spec, device):
@@ -85,7 +87,7 @@ def make_conv(spec, device):
     packed = torch.from_numpy(L.conv_pack(w_logical, cc)).to(device)
     b = None if spec.bias is None else torch.from_numpy(np.ascontiguousarray(spec.bias, np.float32)).to(device)
     return ConvW(m, spec.cin, kt, spec.frame, spec.pad, spec.rout, float(spec.slope), cc, packed, b,
-                 spec.shift)
+                 spec.shift, spec.ref_macs)
 
 
 def _slope(sd, p):
@@ -100,13 +102,15 @@ def _bias(sd, key):
 def spec_same(sd, p, k):
     """PReLU_Conv(C, C, k, padding='same') (blocks.py:293-316)."""
     w = fold_weight(sd, p + ".conv")
-    return ConvSpec(w, w.shape[1], 1, (k - 1) // 2, 1, _slope(sd, p), _bias(sd, p + ".conv.bias"))
+    return ConvSpec(w, w.shape[1], 1, (k - 1) // 2, 1, _slope(sd, p), _bias(sd, p + ".conv.bias"),
+                    ref_macs=float(w.size))
 
 
 def spec_plain(sd, p, k, slope=1.0):
     """Plain Conv1d (no activation): input_conv, 1x1 signal_cond_proj, mel conv."""
     w = fold_weight(sd, p)
-    return ConvSpec(w, w.shape[1], 1, (k - 1) // 2, 1, slope, _bias(sd, p + ".bias"))
+    return ConvSpec(w, w.shape[1], 1, (k - 1) // 2, 1, slope, _bias(sd, p + ".bias"),
+                    ref_macs=float(w.size))
 
 
 def spec_down(sd, p, r, antialias):
@@ -122,9 +126,10 @@ def spec_down(sd, p, r, antialias):
         for kk in range(r):
             wf[:, :, kk:kk + 2 * r + 1] += w[:, :, kk:kk + 1].astype(np.float64) * fir[None, None, :]
         wl = wf.reshape(cout, cin, 3, r).transpose(0, 1, 3, 2).reshape(cout, cin * r, 3)
-        return ConvSpec(wl, cin, r, 1, 1, _slope(sd, p), _bias(sd, p + ".bias"))
+        return ConvSpec(wl, cin, r, 1, 1, _slope(sd, p), _bias(sd, p + ".bias"),
+                        ref_macs=float(cout * cin * r + cin * (2 * r + 1) * r))
     return ConvSpec(w.reshape(cout, cin * r, 1), cin, r, 0, 1, _slope(sd, p),
-                    _bias(sd, p + ".conv.bias"))
+                    _bias(sd, p + ".conv.bias"), ref_macs=float(cout * cin * r))
 
 
 def spec_up(sd, p, r, antialias):
@@ -143,9 +148,11 @@ def spec_up(sd, p, r, antialias):
                 d = s_ // r
                 e = s_ - d * r
                 wl[ph, :, :, d + 1] += fir[j] * w[:, :, e].T
-        return ConvSpec(wl.reshape(r * cout, cin, 3), cin, 1, 1, r, _slope(sd, p), _bias(sd, p + ".bias"))
+        return ConvSpec(wl.reshape(r * cout, cin, 3), cin, 1, 1, r, _slope(sd, p), _bias(sd, p + ".bias"),
+                        ref_macs=float(cin * cout * r + cout * (2 * r + 1) * r))
     wl = w.transpose(2, 1, 0).reshape(r * cout, cin, 1)
-    return ConvSpec(wl, cin, 1, 0, r, _slope(sd, p), _bias(sd, p + ".conv.bias"))
+    return ConvSpec(wl, cin, 1, 0, r, _slope(sd, p), _bias(sd, p + ".conv.bias"),
+                    ref_macs=float(cin * cout * r))
 
 
 def prep_same(sd, p, k, device):
@@ -205,7 +212,8 @@ def prep_gru(sd, p, num_layers, device):
         s, sr = f"_l{l}", f"_l{l}_reverse"
         w_ih = np.concatenate([_np(sd[p + ".weight_ih" + s]), _np(sd[p + ".weight_ih" + sr])], 0)
         b_ih = np.concatenate([_np(sd[p + ".bias_ih" + s]), _np(sd[p + ".bias_ih" + sr])], 0)
-        proj = make_conv(ConvSpec(w_ih[:, :, None], w_ih.shape[1], 1, 0, 1, 1.0, b_ih), device)
+        proj = make_conv(ConvSpec(w_ih[:, :, None], w_ih.shape[1], 1, 0, 1, 1.0, b_ih,
+                                  ref_macs=float(w_ih.size)), device)
         w_hh = torch.stack([sd[p + ".weight_hh" + s], sd[p + ".weight_hh" + sr]]).float().contiguous().to(device)
         b_hh = torch.stack([sd[p + ".bias_hh" + s], sd[p + ".bias_hh" + sr]]).float().contiguous().to(device)
         layers.append((proj, w_hh, b_hh))
@@ -255,6 +263,7 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
     if res2 is not None:
         d.res2, d.r2_bstride, d.r2_cstride, d.s2 = res2.ptr, res2.bs, res2.cs, s2
     d.tile = -1
+    d._flops = 2.0 * cw.ref_macs * n_frames * d.batch
     # shape guards: the kernel trusts these (an out-of-bounds store faults the GPU)
     assert x.C == cw.cin, ("conv input channels", x.C, cw.cin)
     assert y.C == cw.cout, ("conv output channels", y.C, cw.cout)
@@ -297,6 +306,7 @@ def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, re
         d.res, d.res_bstride, d.res_cstride, d.res_scale = res.ptr, res.bs, res.cs, res_scale
     d.hidden, d.steps, d.batch = gw.hidden, x.T, x.B
     d.granules, d.status = granules.data_ptr(), status.data_ptr()
+    d._flops = 2.0 * 2 * 3 * H * H * x.T * x.B
     prog.add(L.OP_GRU, d)
 
 
@@ -546,6 +556,7 @@ class Engine:
                 d.mlp_w[k], d.mlp_b[k], d.mlp_slope[k] = w.data_ptr(), b.data_ptr(), s
         d.rows = self.film_rows
         d.w, d.bias, d.out, d.gbuf = self.emb_w.data_ptr(), self.emb_b.data_ptr(), film_out.data_ptr(), gbuf.data_ptr()
+        d._flops = 2.0 * self.film_rows * self.emb_dim * n
         prog.add(L.OP_EMBED, d)
 
     def head_desc(self, h: Act, out_ptr, B, T, mode=0, x_ptr=0, z_ptr=0, coef=None):
@@ -559,6 +570,7 @@ class Engine:
             for k, v in coef.items():
                 setattr(d, k, float(v))
         d.x, d.z, d.out = x_ptr, z_ptr, out_ptr
+        d._flops = 2.0 * h.C * 3 * T * B
         return d
 
     # -------------------------------------------------------------- conditioner
