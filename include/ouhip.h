@@ -86,17 +86,25 @@ typedef struct ou_conv_desc {
     int32_t _reserved;
 } ou_conv_desc;
 
-/* Pick the channel chunk for a layer: multiple of lcm(frame, 8). */
+/* Default channel chunk of the kernel for a tap count (informational: the
+ * packed weight layout does not depend on it). */
 int ou_conv_chunk(int kt, int frame);
 /* Number of floats of the packed weight buffer. */
 int64_t ou_conv_packed_size(int m, int cin_eff, int kt, int cc);
 /* Host-side packing: w_logical[m][cin_eff][kt] (row-major, host memory)
- * -> packed[] in the per-lane MFMA fragment order the kernel streams. */
+ * -> packed[] in the per-lane MFMA fragment order the kernel streams:
+ * [m-tile of 32][channel pair][tap][lane], lane l holding row l & 31 and
+ * channel 2*pair + (l >> 5); channels padded with zeros to a multiple of 64. */
 int ou_conv_pack(const float* w_logical, int m, int cin_eff, int kt, int cc,
                  float* packed);
 int ou_conv(const ou_conv_desc* d, void* stream);
-/* The tile configuration ou_conv would use for this descriptor (0..5). */
+/* The tile configuration ou_conv would use for this descriptor when
+ * d->tile < 0; ou_conv_num_tiles() configurations exist, ou_conv_tile_ok()
+ * says whether one fits the LDS budget for a tap count (host autotuning
+ * times the valid ones per layer and stores the winner in d->tile). */
 int ou_conv_pick_tile(const ou_conv_desc* d);
+int ou_conv_num_tiles(void);
+int ou_conv_tile_ok(int kt, int tile);
 
 /* ------------------------------------------------------------------------
  * Bidirectional GRU recurrence (kernel K6).  Replaces the recurrent part of

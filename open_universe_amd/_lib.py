@@ -134,6 +134,8 @@ EXPORTS = {
     "ou_conv_pack": (c_int, [POINTER(c_float), c_int, c_int, c_int, c_int, POINTER(c_float)]),
     "ou_conv": (c_int, [POINTER(ConvDesc), c_void_p]),
     "ou_conv_pick_tile": (c_int, [POINTER(ConvDesc)]),
+    "ou_conv_num_tiles": (c_int, []),
+    "ou_conv_tile_ok": (c_int, [c_int, c_int]),
     "ou_gru_workspace_bytes": (c_int64, [c_int, c_int]),
     "ou_gru": (c_int, [POINTER(GruDesc), c_void_p]),
     "ou_embed": (c_int, [POINTER(EmbedDesc), c_void_p]),
@@ -208,6 +210,11 @@ def conv_pack(w_logical, cc):
     return out
 
 
+# Optional per-layer tile autotuner for ou_conv (set by the engine on a GPU):
+# called with a ConvDesc whose tile is -1, returns the tile id to record.
+TUNER = None
+
+
 class Program:
     """A recorded launch list (ou_program) with optional hipGraph replay."""
 
@@ -220,6 +227,8 @@ class Program:
 
     def add(self, op, desc):
         assert isinstance(desc, OP_STRUCT[op])
+        if op == OP_CONV and desc.tile < 0 and TUNER is not None:
+            desc.tile = TUNER(desc)
         check(self.lib.ou_program_add(self.h, op, ctypes.byref(desc), ctypes.sizeof(desc)),
               f"program_add(op={op})")
         self.flops.append(float(getattr(desc, "_flops", 0.0)))

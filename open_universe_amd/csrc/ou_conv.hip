@@ -14,27 +14,32 @@
 // so strided convs and the STFT become plain convolutions over frames.
 //
 // MI355X mapping
-//   * fp32 inputs => v_mfma_f32_32x32x2_f32 (exact f32 FMA chain, 157 TF peak).
-//   * workgroup = 4 waves; each wave owns a 32 x (32*NR) output tile.
-//   * K is walked in chunks of cc frame-view channels.  The chunk's input
-//     window (cc x (BN + KT - 1) frames) is staged into LDS once, with the
-//     PReLU (and the optional per-item input scale) applied on the way in, so
-//     the k-tap re-reads of the same sample hit LDS, not HBM.
-//   * A (weights) streams straight from global/L2 into VGPRs in per-lane
-//     fragment order (packed once on the host by ou_conv_pack), 256 B per wave
-//     per MFMA step, coalesced.
-//   * Lane halves (lane>>5) take channel c and c+cc/2 of the chunk at the same
+//   * fp32 operands => v_mfma_f32_32x32x2_f32 (exact f32 FMA chain; 157 TF/s
+//     dense peak, 64 cycles per instruction per SIMD).
+//   * workgroup = 4 waves arranged WM x WN x WK: WM x WN output sub-tiles of
+//     32 x (32*NR), and WK waves splitting the K range of the same sub-tile
+//     (intra-workgroup split-K, reduced through LDS).  Small-N deep levels
+//     (512 channels x 801 frames at batch 1) need WK > 1 to put >= 1 wave on
+//     every SIMD; the high-rate levels use WK = 1 and wide N tiles.
+//   * K is walked in chunks of CC frame-view channels x KT taps.  Both
+//     operands of a chunk are staged through LDS, double-buffered: the global
+//     loads of chunk q+1 are issued into registers before the MFMAs of chunk q
+//     and written to the other LDS buffer after them, so one barrier per chunk
+//     separates staging from compute and HBM/L2 latency hides under MFMA.
+//   * The PReLU (and the optional per-item input scale) is applied while
+//     staging the input window, so the KT-tap re-reads of a sample hit LDS.
+//   * Lane half h = lane>>5 owns channel 2*cp + h of the chunk at the same
 //     tap, so every B-fragment read is 32 consecutive floats of one LDS row
-//     (conflict-free ds_read_b32) and no per-step index decode is needed.
-//   * Epilogue (bias, zero-fill, residual, FiLM, residual) runs on the
-//     accumulator registers; each 32-lane half stores one contiguous 128-B
-//     row segment.
+//     (conflict-free ds_read_b32) and no per-step index decode is needed.  The
+//     weights are packed once on the host in exactly that per-lane order
+//     (ou_conv_pack), so A-fragment reads are lane-linear too.
+//   * Epilogue (bias, zero-fill, residual, FiLM, residual) on the accumulator
+//     registers; each 32-lane half stores one contiguous 128-B row segment.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
-#include <vector>
 
 #include "../../include/ouhip.h"
 #include "ou_common.h"
@@ -43,34 +48,121 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-template <int KT, int WM, int WN, int NR>
-struct ConvCfg {
+constexpr int kCinAlign = 64;   // packed weights pad the channel axis to this
+
+template <int KT, int CC, int WM, int WN, int WK, int NR>
+struct Cfg {
     static constexpr int BM = 32 * WM;
     static constexpr int BN = 32 * NR * WN;
-    static constexpr int W = BN + KT - 1;   // staged frames per chunk
-    static constexpr int WS = W;            // LDS row stride (floats)
+    static constexpr int W = BN + KT - 1;           // staged frames per chunk
+    static constexpr int WS = W | 1;                 // odd LDS row stride
+    static constexpr int HALF = CC / 2;              // channel pairs per chunk
+    static constexpr int S = HALF * KT;              // k-steps per chunk
+    static constexpr int HPW = HALF / WK;            // channel pairs per wave
+    static constexpr int XN = CC * W;                // staged input floats
+    static constexpr int XE = (XN + 255) / 256;      // per thread
+    static constexpr int AN = WM * S * 64;           // staged weight floats
+    static constexpr int AE4 = (AN / 4 + 255) / 256; // float4 per thread
+    static constexpr int XBUF = CC * WS;
+    static constexpr int ABUF = AN;
+    static constexpr int STAGE = XBUF + ABUF;
+    static constexpr int RED = (WK - 1) * WM * WN * NR * 16 * 64;
+    static constexpr int LDS = (2 * STAGE > RED ? 2 * STAGE : RED);
+    static_assert(HALF % WK == 0, "channel pairs must split evenly over WK");
+    static_assert(WM * WN * WK == 4, "4 waves per workgroup");
 };
 
-template <int KT, int WM, int WN, int NR>
-__global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, int mtiles)
+template <int KT, int CC, int WM, int WN, int WK, int NR>
+__global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, int mtiles,
+                                                   int64_t a_mt_stride)
 {
-    using C = ConvCfg<KT, WM, WN, NR>;
-    extern __shared__ __attribute__((aligned(16))) float xs[];
+    using C = Cfg<KT, CC, WM, WN, WK, NR>;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int wm = wave / WN;
     const int wn = wave % WN;
+    const int wm = (wave / WN) % WM;
+    const int wk = wave / (WN * WM);
     const int b = blockIdx.z;
     const int n0 = blockIdx.x * C::BN;
-    const int mt = blockIdx.y * WM + wm;
+    const int mt0 = blockIdx.y * WM;           // first m-tile of the workgroup
+    const int mt = mt0 + wm;
     const bool active = mt < mtiles;          // wave-uniform
     const int h = lane >> 5;
     const int l32 = lane & 31;
-    const int cc = d.cc;
-    const int half = cc >> 1;
     const int R = d.frame;
+
+    const float* __restrict__ x = d.x + (int64_t)b * d.x_bstride;
+    const float scale = d.in_scale ? d.in_scale[b] : 1.0f;
+    const float slope = d.slope;
+    const int t0 = n0 - d.pad;
+    const int64_t xc = d.x_cstride;
+    const int in_len = d.in_len;
+    const int cin = d.cin;
+
+    // ---- staging helpers -------------------------------------------------
+    float xr[C::XE];
+    float4 ar[C::AE4 > 0 ? C::AE4 : 1];
+    auto load_chunk = [&](int q) {
+#pragma unroll
+        for (int e = 0; e < C::XE; ++e) {
+            const int idx = tid + e * 256;
+            float v = 0.f;
+            if (idx < C::XN) {
+                int c, w, ci, pos;
+                if (R == 1) {
+                    c = idx / C::W;
+                    w = idx - c * C::W;
+                    ci = q * CC + c;
+                    pos = t0 + w + d.shift;
+                } else {
+                    w = idx / CC;
+                    c = idx - w * CC;
+                    const int cq = q * CC + c;
+                    ci = cq / R;
+                    pos = (t0 + w) * R + (cq - ci * R) + d.shift;
+                }
+                if (ci < cin && pos >= 0 && pos < in_len) v = x[(int64_t)ci * xc + pos];
+            }
+            xr[e] = v;
+        }
+#pragma unroll
+        for (int e = 0; e < C::AE4; ++e) {
+            const int f = min(tid + e * 256, C::AN / 4 - 1);  // float4 index in the chunk
+            const int ml = f / (C::S * 16);              // m-tile within the workgroup
+            const int r = f - ml * (C::S * 16);
+            const int mtg = min(mt0 + ml, mtiles - 1);   // clamp: rows past M are unused
+            const float4* src = (const float4*)(d.w + (int64_t)mtg * a_mt_stride +
+                                                (int64_t)q * C::S * 64) + r;
+            ar[e] = *src;
+        }
+    };
+    auto store_chunk = [&](int buf) {
+        float* xs = lds + buf * C::STAGE;
+        float* as = xs + C::XBUF;
+#pragma unroll
+        for (int e = 0; e < C::XE; ++e) {
+            const int idx = tid + e * 256;
+            if (idx < C::XN) {
+                int c, w;
+                if (R == 1) {
+                    c = idx / C::W;
+                    w = idx - c * C::W;
+                } else {
+                    w = idx / CC;
+                    c = idx - w * CC;
+                }
+                float v = xr[e] * scale;
+                v = v >= 0.f ? v : v * slope;
+                xs[c * C::WS + w] = v;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < C::AE4; ++e)
+            if (tid + e * 256 < C::AN / 4) ((float4*)as)[tid + e * 256] = ar[e];
+    };
 
     floatx16 acc[NR];
 #pragma unroll
@@ -78,82 +170,54 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
 
-    const float* __restrict__ x = d.x + (int64_t)b * d.x_bstride;
-    const float scale = d.in_scale ? d.in_scale[b] : 1.0f;
-    const float slope = d.slope;
-    const int t0 = n0 - d.pad;
-    const int steps = half * KT;              // MFMA k-steps per chunk
-    const int64_t xc = d.x_cstride;
-    const int in_len = d.in_len;
-    const int cin = d.cin;
-
+    load_chunk(0);
+    store_chunk(0);
+    __syncthreads();
     for (int q = 0; q < nchunks; ++q) {
-        __syncthreads();
-        // ---- stage the chunk's input window into LDS (PReLU applied) ----
-        if (R == 1) {
-            const int total = cc * C::W;
-            for (int e = tid; e < total; e += 256) {
-                const int c = e / C::W;
-                const int w = e - c * C::W;
-                const int ci = q * cc + c;
-                const int pos = t0 + w + d.shift;
-                float v = 0.f;
-                if (ci < cin && pos >= 0 && pos < in_len) {
-                    v = x[(int64_t)ci * xc + pos] * scale;
-                    v = v >= 0.f ? v : v * slope;
+        const int cur = q & 1;
+        if (q + 1 < nchunks) load_chunk(q + 1);
+        if (active) {
+            const float* xs = lds + cur * C::STAGE;
+            const float* as = xs + C::XBUF + wm * (C::S * 64) + lane;
+            const float* xrow = xs + h * C::WS + wn * (32 * NR) + l32;
+#pragma unroll
+            for (int cpl = 0; cpl < C::HPW; ++cpl) {
+                const int cp = wk * C::HPW + cpl;
+#pragma unroll
+                for (int k = 0; k < KT; ++k) {
+                    const float a = as[(cp * KT + k) * 64];
+                    const float* xr_ = xrow + (2 * cp) * C::WS + k;
+#pragma unroll
+                    for (int nr = 0; nr < NR; ++nr)
+                        acc[nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xr_[nr * 32], acc[nr],
+                                                                       0, 0, 0);
                 }
-                xs[c * C::WS + w] = v;
-            }
-        } else {
-            // frame view: chunk = cc/R whole channels; walk samples in order so
-            // consecutive lanes read consecutive addresses
-            const int span = C::W * R;
-            const int total = cc * C::W;        // = (cc/R) * span
-            const int ci0 = (q * cc) / R;
-            const int pos0 = t0 * R + d.shift;
-            for (int e = tid; e < total; e += 256) {
-                const int cl = e / span;
-                const int pl = e - cl * span;
-                const int w = pl / R;
-                const int p = pl - w * R;
-                const int ci = ci0 + cl;
-                const int pos = pos0 + pl;
-                float v = 0.f;
-                if (ci < cin && pos >= 0 && pos < in_len) {
-                    v = x[(int64_t)ci * xc + pos] * scale;
-                    v = v >= 0.f ? v : v * slope;
-                }
-                xs[(cl * R + p) * C::WS + w] = v;
             }
         }
+        if (q + 1 < nchunks) store_chunk(cur ^ 1);
         __syncthreads();
-        if (!active) continue;
+    }
 
-        // ---- MFMA over the chunk ----
-        const float* __restrict__ ap =
-            d.w + ((int64_t)(mt * nchunks + q) * steps) * 64 + lane;
-        const float* xrow = xs + h * half * C::WS + wn * (32 * NR) + l32;
-        float a_next[KT];
+    // ---- intra-workgroup split-K reduction (fixed order: deterministic) ----
+    if (WK > 1) {
+        float* red = lds;
+        const int sub = wm * WN + wn;
+        if (wk > 0) {
 #pragma unroll
-        for (int k = 0; k < KT; ++k) a_next[k] = ap[k * 64];
-        for (int cp = 0; cp < half; ++cp) {
-            float a[KT];
+            for (int nr = 0; nr < NR; ++nr)
 #pragma unroll
-            for (int k = 0; k < KT; ++k) a[k] = a_next[k];
-            if (cp + 1 < half) {
-#pragma unroll
-                for (int k = 0; k < KT; ++k) a_next[k] = ap[((cp + 1) * KT + k) * 64];
-            }
-            const float* xr = xrow + cp * C::WS;
-#pragma unroll
-            for (int k = 0; k < KT; ++k) {
-#pragma unroll
-                for (int nr = 0; nr < NR; ++nr) {
-                    acc[nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[k], xr[nr * 32 + k],
-                                                                   acc[nr], 0, 0, 0);
-                }
-            }
+                for (int r = 0; r < 16; ++r)
+                    red[((((wk - 1) * WM * WN + sub) * NR + nr) * 16 + r) * 64 + lane] = acc[nr][r];
         }
+        __syncthreads();
+        if (wk > 0) return;
+#pragma unroll
+        for (int j = 1; j < WK; ++j)
+#pragma unroll
+            for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    acc[nr][r] += red[((((j - 1) * WM * WN + sub) * NR + nr) * 16 + r) * 64 + lane];
     }
     if (!active) return;
 
@@ -192,116 +256,153 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     }
 }
 
-struct TileShape {
-    int wm, wn, nr;
+// ---- tile table ------------------------------------------------------------
+struct Tile {
+    int wm, wn, wk, nr;
 };
-// tile ids: 0 = 32x256, 1 = 64x128, 2 = 64x64, 3 = 128x32, 4 = 32x128, 5 = 32x64
-constexpr TileShape kTiles[] = {{1, 4, 2}, {2, 2, 2}, {2, 2, 1}, {4, 1, 1}, {1, 4, 1}, {2, 1, 1}};
+// id: 0 32x512, 1 32x256, 2 64x128, 3 64x64, 4 32x32/K4, 5 64x32/K2, 6 32x64/K2, 7 128x32
+constexpr Tile kTiles[] = {{1, 4, 1, 4}, {1, 4, 1, 2}, {2, 2, 1, 2}, {2, 2, 1, 1},
+                           {1, 1, 4, 1}, {2, 1, 2, 1}, {1, 2, 2, 1}, {4, 1, 1, 1}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
-template <int KT, int WM, int WN, int NR>
+// channel chunk per (kt, wk): ~1-2k MFMA cycles per wave per chunk
+constexpr int chunk_for(int kt, int wk) { return (kt == 1 ? 32 : 16) * (wk >= 2 ? 2 : 1); }
+
+template <int KT, int WM, int WN, int WK, int NR>
 int launch_t(const ou_conv_desc& d, hipStream_t s)
 {
-    using C = ConvCfg<KT, WM, WN, NR>;
+    constexpr int CC = chunk_for(KT, WK);
+    using C = Cfg<KT, CC, WM, WN, WK, NR>;
     const int mtiles = (d.m + 31) / 32;
     const int cin_eff = d.cin * d.frame;
-    const int nchunks = (cin_eff + d.cc - 1) / d.cc;
+    const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
+    const int nchunks = (cin_eff + CC - 1) / CC;
+    const int64_t a_mt_stride = (int64_t)(cin_pad / 2) * KT * 64;
     dim3 grid((d.n_frames + C::BN - 1) / C::BN, (mtiles + WM - 1) / WM, d.batch);
-    size_t lds = (size_t)d.cc * C::WS * sizeof(float);
-    if (lds > 160 * 1024) return ou_fail(-3, "conv: LDS window too large (cc=%d)", d.cc);
-    hipLaunchKernelGGL((conv_kernel<KT, WM, WN, NR>), grid, dim3(256), lds, s, d, nchunks, mtiles);
+    const size_t lds = (size_t)C::LDS * sizeof(float);
+    hipLaunchKernelGGL((conv_kernel<KT, CC, WM, WN, WK, NR>), grid, dim3(256), lds, s, d, nchunks,
+                       mtiles, a_mt_stride);
     return ou_check_launch("conv");
 }
+
+template <int KT, int WM, int WN, int WK, int NR>
+constexpr int lds_bytes_t()
+{
+    return Cfg<KT, chunk_for(KT, WK), WM, WN, WK, NR>::LDS * 4;
+}
+
+template <int KT>
+int lds_bytes_kt(int tile)
+{
+    switch (tile) {
+    case 0: return lds_bytes_t<KT, 1, 4, 1, 4>();
+    case 1: return lds_bytes_t<KT, 1, 4, 1, 2>();
+    case 2: return lds_bytes_t<KT, 2, 2, 1, 2>();
+    case 3: return lds_bytes_t<KT, 2, 2, 1, 1>();
+    case 4: return lds_bytes_t<KT, 1, 1, 4, 1>();
+    case 5: return lds_bytes_t<KT, 2, 1, 2, 1>();
+    case 6: return lds_bytes_t<KT, 1, 2, 2, 1>();
+    case 7: return lds_bytes_t<KT, 4, 1, 1, 1>();
+    }
+    return -1;
+}
+
+int lds_bytes(int kt, int tile)
+{
+    switch (kt) {
+    case 1: return lds_bytes_kt<1>(tile);
+    case 3: return lds_bytes_kt<3>(tile);
+    case 4: return lds_bytes_kt<4>(tile);
+    case 5: return lds_bytes_kt<5>(tile);
+    }
+    return -1;
+}
+
+constexpr int kMaxLds = 64 * 1024;
 
 template <int KT>
 int launch_kt(const ou_conv_desc& d, int tile, hipStream_t s)
 {
     switch (tile) {
-    case 0: return launch_t<KT, 1, 4, 2>(d, s);
-    case 1: return launch_t<KT, 2, 2, 2>(d, s);
-    case 2: return launch_t<KT, 2, 2, 1>(d, s);
-    case 3: return launch_t<KT, 4, 1, 1>(d, s);
-    case 4: return launch_t<KT, 1, 4, 1>(d, s);
-    case 5: return launch_t<KT, 2, 1, 1>(d, s);
+    case 0: return launch_t<KT, 1, 4, 1, 4>(d, s);
+    case 1: return launch_t<KT, 1, 4, 1, 2>(d, s);
+    case 2: return launch_t<KT, 2, 2, 1, 2>(d, s);
+    case 3: return launch_t<KT, 2, 2, 1, 1>(d, s);
+    case 4: return launch_t<KT, 1, 1, 4, 1>(d, s);
+    case 5: return launch_t<KT, 2, 1, 2, 1>(d, s);
+    case 6: return launch_t<KT, 1, 2, 2, 1>(d, s);
+    case 7: return launch_t<KT, 4, 1, 1, 1>(d, s);
     }
     return ou_fail(-2, "conv: bad tile %d", tile);
 }
 
+// Static choice (used when the host has not autotuned the layer): the
+// largest tile that still gives >= 2 workgroups per CU, split-K when N is short.
 int pick_tile(const ou_conv_desc& d)
 {
-    const int64_t target = 1024;  // workgroups: >= 4 per CU when possible
     auto wgs = [&](int t) {
-        const int bm = 32 * kTiles[t].wm, bn = 32 * kTiles[t].nr * kTiles[t].wn;
+        const Tile& k = kTiles[t];
+        const int bm = 32 * k.wm, bn = 32 * k.nr * k.wn;
         return (int64_t)((d.m + bm - 1) / bm) * ((d.n_frames + bn - 1) / bn) * d.batch;
     };
-    const int order_small_m[] = {0, 4, 5};
-    const int order_big_m[] = {1, 2, 3};
-    const int* order = d.m <= 32 ? order_small_m : order_big_m;
-    for (int i = 0; i < 3; ++i) {
-        const int t = order[i];
-        const int bn = 32 * kTiles[t].nr * kTiles[t].wn;
-        const size_t lds = (size_t)d.cc * (bn + d.kt - 1) * sizeof(float);
-        if (lds > 64 * 1024) continue;
-        if (wgs(t) >= target || i == 2) return t;
+    auto ok = [&](int t) { return lds_bytes(d.kt, t) <= kMaxLds; };
+    if (d.m <= 32) {
+        for (int t : {0, 1}) if (ok(t) && wgs(t) >= 512) return t;
+        return 4;
     }
-    return d.m <= 32 ? 5 : 3;
+    for (int t : {2, 3}) if (ok(t) && wgs(t) >= 512) return t;
+    if (wgs(6) >= 512) return 6;
+    return 4;
 }
 
 }  // namespace
 
 extern "C" int ou_conv_chunk(int kt, int frame)
 {
-    const int base = kt >= 3 ? 16 : 32;
-    int unit = 8;
-    // lcm(frame, 8)
-    int a = frame, bb = 8;
-    while (bb) { int t = a % bb; a = bb; bb = t; }
-    unit = frame / a * 8;
-    int cc = unit;
-    while (cc < base) cc += unit;
-    // (cc/2)*kt must be a multiple of 4 for the packed layout: cc % 8 == 0 ensures it
-    return cc;
+    (void)frame;
+    return chunk_for(kt, 1);
 }
 
 extern "C" int64_t ou_conv_packed_size(int m, int cin_eff, int kt, int cc)
 {
+    (void)cc;
     const int64_t mtiles = (m + 31) / 32;
-    const int64_t nchunks = (cin_eff + cc - 1) / cc;
-    return mtiles * nchunks * (int64_t)(cc / 2) * kt * 64;
+    const int64_t cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
+    return mtiles * (cin_pad / 2) * kt * 64;
 }
 
+// Packed order: [m-tile][channel pair cp][tap k][lane]; lane -> (row mt*32 +
+// (lane & 31), channel 2*cp + (lane >> 5)); zero outside [0, m) x [0, cin_eff).
 extern "C" int ou_conv_pack(const float* w, int m, int cin_eff, int kt, int cc, float* out)
 {
-    if (!w || !out || m <= 0 || cin_eff <= 0 || kt <= 0 || cc <= 0 || (cc & 1))
+    (void)cc;
+    if (!w || !out || m <= 0 || cin_eff <= 0 || kt <= 0)
         return ou_fail(-1, "conv_pack: bad arguments");
     const int mtiles = (m + 31) / 32;
-    const int nchunks = (cin_eff + cc - 1) / cc;
-    const int half = cc / 2;
+    const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
     int64_t o = 0;
     for (int mt = 0; mt < mtiles; ++mt)
-        for (int q = 0; q < nchunks; ++q)
-            for (int cp = 0; cp < half; ++cp)
-                for (int k = 0; k < kt; ++k)
-                    for (int lane = 0; lane < 64; ++lane) {
-                        const int row = mt * 32 + (lane & 31);
-                        const int c = q * cc + cp + (lane >> 5) * half;
-                        out[o++] = (row < m && c < cin_eff)
-                                       ? w[((int64_t)row * cin_eff + c) * kt + k]
-                                       : 0.f;
-                    }
+        for (int cp = 0; cp < cin_pad / 2; ++cp)
+            for (int k = 0; k < kt; ++k)
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int row = mt * 32 + (lane & 31);
+                    const int c = 2 * cp + (lane >> 5);
+                    out[o++] = (row < m && c < cin_eff) ? w[((int64_t)row * cin_eff + c) * kt + k]
+                                                        : 0.f;
+                }
     return 0;
 }
 
 extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
 {
     if (!dp) return ou_fail(-1, "conv: null descriptor");
-    ou_conv_desc d = *dp;
+    const ou_conv_desc& d = *dp;
     if (!d.x || !d.w || !d.y || d.m <= 0 || d.batch <= 0 || d.n_frames <= 0 || d.cin <= 0 ||
-        d.frame <= 0 || d.rout <= 0 || d.m % d.rout != 0 || d.cc <= 0 || (d.cc & 1) ||
-        (d.frame > 1 && d.cc % d.frame != 0))
-        return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d cc=%d frame=%d)", d.m, d.rout,
-                       d.cc, d.frame);
-    int tile = d.tile >= 0 && d.tile < kNumTiles ? d.tile : pick_tile(d);
+        d.frame <= 0 || d.rout <= 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0)
+        return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d frame=%d)", d.m, d.rout, d.frame);
+    const int tile = d.tile >= 0 && d.tile < kNumTiles ? d.tile : pick_tile(d);
+    if (lds_bytes(d.kt, tile) > kMaxLds)
+        return ou_fail(-2, "conv: tile %d needs %d B of LDS for kt=%d", tile, lds_bytes(d.kt, tile), d.kt);
     hipStream_t s = (hipStream_t)stream;
     switch (d.kt) {
     case 1: return launch_kt<1>(d, tile, s);
@@ -313,3 +414,8 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
 }
 
 extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile(*d) : -1; }
+extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
+extern "C" int ou_conv_tile_ok(int kt, int tile)
+{
+    return tile >= 0 && tile < kNumTiles && lds_bytes(kt, tile) > 0 && lds_bytes(kt, tile) <= kMaxLds;
+}

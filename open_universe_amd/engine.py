@@ -318,6 +318,67 @@ def level_lengths(T, rates):
 
 
 # ---------------------------------------------------------------------------
+# per-layer tile autotuning
+# ---------------------------------------------------------------------------
+class ConvTuner:
+    """Times every tile configuration that fits LDS for a conv geometry (on the
+    current stream, with HIP events) and keeps the fastest.  Plans are built
+    once per input shape, so this runs once per distinct layer geometry."""
+
+    def __init__(self, reps=3):
+        self.cache = {}
+        self.reps = reps
+
+    @staticmethod
+    def key(d):
+        return (d.m, d.cin, d.frame, d.kt, d.pad, d.n_frames, d.batch, d.rout, d.in_len,
+                d.out_len, bool(d.res1), bool(d.film), bool(d.res2), bool(d.in_scale))
+
+    def __call__(self, d):
+        import ctypes
+
+        k = self.key(d)
+        if k in self.cache:
+            return self.cache[k]
+        lib = L.load()
+        stream = torch.cuda.current_stream().cuda_stream
+        best, best_ms = -1, float("inf")
+        for t in range(lib.ou_conv_num_tiles()):
+            if not lib.ou_conv_tile_ok(d.kt, t):
+                continue
+            d.tile = t
+            if lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream)) != 0:
+                continue
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(self.reps):
+                lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / self.reps
+            if ms < best_ms:
+                best, best_ms = t, ms
+        d.tile = -1
+        self.cache[k] = best
+        return best
+
+
+_TUNER = None
+
+
+def enable_autotune(flag=True):
+    global _TUNER
+    import os
+
+    if flag and os.environ.get("OUHIP_AUTOTUNE", "1") != "0":
+        if _TUNER is None:
+            _TUNER = ConvTuner()
+        L.TUNER = _TUNER
+    else:
+        L.TUNER = None
+
+
+# ---------------------------------------------------------------------------
 # engine
 # ---------------------------------------------------------------------------
 class Engine:
@@ -349,6 +410,7 @@ class Engine:
             if "sdl" in parts:
                 self._prep_sdl(sd, "signal_decoupling_layer", dev)
         self.status = torch.zeros(4, dtype=torch.int32, device=dev)
+        enable_autotune(self.device.type == "cuda")
 
     # -------------------------------------------------------------- weights
     def _prep_score(self, sd, p, dev):

@@ -60,27 +60,27 @@ def test_struct_layouts_match_c():
 
 
 def test_conv_pack_layout():
-    """Packed order: [mtile][chunk][cp][k][lane], lane -> (row = lane & 31,
-    channel = chunk*cc + cp + (lane >> 5) * cc/2), zero padded."""
+    """Packed order: [mtile][channel pair][tap][lane], lane -> (row = lane & 31,
+    channel = 2 * pair + (lane >> 5)); channels zero-padded to a multiple of 64."""
     rng = np.random.default_rng(0)
     m, cin, kt = 40, 20, 3
     w = rng.standard_normal((m, cin, kt)).astype(np.float32)
-    cc = L.conv_chunk(kt, 1)
-    packed = L.conv_pack(w, cc)
-    mtiles, nch, half = 2, -(-cin // cc), cc // 2
-    ref = np.zeros((mtiles, nch, half, kt, 64), np.float32)
+    packed = L.conv_pack(w, L.conv_chunk(kt, 1))
+    mtiles, pairs = 2, 32
+    ref = np.zeros((mtiles, pairs, kt, 64), np.float32)
     for mt in range(mtiles):
-        for q in range(nch):
-            for cp in range(half):
-                for k in range(kt):
-                    for lane in range(64):
-                        row, c = mt * 32 + (lane & 31), q * cc + cp + (lane >> 5) * half
-                        if row < m and c < cin:
-                            ref[mt, q, cp, k, lane] = w[row, c, k]
+        for cp in range(pairs):
+            for k in range(kt):
+                for lane in range(64):
+                    row, c = mt * 32 + (lane & 31), 2 * cp + (lane >> 5)
+                    if row < m and c < cin:
+                        ref[mt, cp, k, lane] = w[row, c, k]
     np.testing.assert_array_equal(packed, ref.reshape(-1))
 
 
-@pytest.mark.parametrize("kt,frame,cc", [(5, 1, 16), (3, 1, 16), (1, 1, 32), (3, 5, 40),
-                                         (1, 160, 160), (4, 160, 160), (3, 3, 24), (1, 20, 40)])
-def test_conv_chunk(kt, frame, cc):
-    assert L.conv_chunk(kt, frame) == cc
+def test_conv_tiles_fit_lds():
+    lib = L.load()
+    n = lib.ou_conv_num_tiles()
+    assert n >= 6
+    for kt in (1, 3, 4, 5):
+        assert any(lib.ou_conv_tile_ok(kt, t) for t in range(n))
