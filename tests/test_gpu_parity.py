@@ -214,4 +214,5 @@ def test_enhance_full_size_properties(pp16):
         p1.NZ.copy_(nz)
         p1._launch(torch.cuda.current_stream().cuda_stream, True)
         torch.cuda.synchronize()
-        assert rel_rms(p1.OUT[0].cpu(), a[1].cpu()) < 1e-6
+        # different batch sizes may autotune to different tiles (summation order)
+        assert rel_rms(p1.OUT[0].cpu(), a[1].cpu()) < 1e-4
