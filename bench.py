@@ -90,11 +90,18 @@ def cpu_baseline(model, cfg, seconds):
                       f"B=1, 8 steps, fp32, best of 3 after 1 warm-up ({best:.3f} s), {cpu_model()}"}
 
 
-def profile_roofline(plan, stream):
+def profile_roofline(plan, stream, dump=None):
     """Per-op device time of one instrumented eager replay of the plan."""
     from open_universe_amd import _lib as L
 
     ms = plan.prog.profile(stream)
+    if dump:
+        rows = []
+        for i, (t, k, f) in enumerate(zip(ms, plan.prog.op_kinds(), plan.prog.flops)):
+            info = plan.prog.info[i] if i < len(plan.prog.info) else {}
+            rows.append({"i": i, "kind": k, "ms": t, "gflop": f / 1e9, **info})
+        with open(dump, "w") as fh:
+            json.dump(rows, fh)
     kinds = plan.prog.op_kinds()
     flops = plan.prog.flops
     conv_ms = sum(t for t, k in zip(ms, kinds) if k == L.OP_CONV)
@@ -115,6 +122,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=CLIP_S)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--dump-ops", default=None, help="write per-op profile rows (JSON)")
     args = ap.parse_args()
 
     import numpy as np
@@ -162,7 +170,7 @@ def main():
         with torch.no_grad():
             plan.MIX.copy_(clips[0][:, None])
             plan.draw_noise(rng)
-            prof = profile_roofline(plan, torch.cuda.current_stream(dev).cuda_stream)
+            prof = profile_roofline(plan, torch.cuda.current_stream(dev).cuda_stream, args.dump_ops)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -224,6 +224,7 @@ class Program:
         self.keep = []          # tensors whose memory the program references
         self.captured = False
         self.flops = []         # algorithmic FLOPs of the reference ops each op replaces
+        self.info = []          # per-op geometry (profiling / reports)
 
     def add(self, op, desc):
         assert isinstance(desc, OP_STRUCT[op])
@@ -232,6 +233,14 @@ class Program:
         check(self.lib.ou_program_add(self.h, op, ctypes.byref(desc), ctypes.sizeof(desc)),
               f"program_add(op={op})")
         self.flops.append(float(getattr(desc, "_flops", 0.0)))
+        if op == OP_CONV:
+            self.info.append({"m": desc.m, "cin": desc.cin, "frame": desc.frame, "kt": desc.kt,
+                              "n": desc.n_frames, "b": desc.batch, "rout": desc.rout,
+                              "tile": desc.tile})
+        elif op == OP_GRU:
+            self.info.append({"H": desc.hidden, "T": desc.steps, "b": desc.batch})
+        else:
+            self.info.append({})
 
     def __len__(self):
         return self.lib.ou_program_size(self.h)

@@ -63,14 +63,16 @@ struct Cfg {
     static constexpr int XE = (XN + 255) / 256;      // per thread
     static constexpr int AN = WM * S * 64;           // staged weight floats
     static constexpr int AE4 = (AN / 4 + 255) / 256; // float4 per thread
-    static constexpr int XBUF = CC * WS;
-    static constexpr int ABUF = AN;
+    static constexpr int XBUF = (CC * WS + 3) / 4 * 4;
+    static constexpr int ABUF = AE4 * 1024;          // padded: every thread stores AE4 float4
     static constexpr int STAGE = XBUF + ABUF;
     static constexpr int RED = (WK - 1) * WM * WN * NR * 16 * 64;
     static constexpr int LDS = (2 * STAGE > RED ? 2 * STAGE : RED);
     static_assert(HALF % WK == 0, "channel pairs must split evenly over WK");
     static_assert(WM * WN * WK == 4, "4 waves per workgroup");
 };
+
+constexpr int kSentinel = 0x7ffffff0;   // byte offset past any buffer: loads return 0
 
 template <int KT, int CC, int WM, int WN, int WK, int NR>
 __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, int mtiles,
@@ -89,80 +91,102 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const int n0 = blockIdx.x * C::BN;
     const int mt0 = blockIdx.y * WM;           // first m-tile of the workgroup
     const int mt = mt0 + wm;
-    const bool active = mt < mtiles;          // wave-uniform
     const int h = lane >> 5;
     const int l32 = lane & 31;
     const int R = d.frame;
-
-    const float* __restrict__ x = d.x + (int64_t)b * d.x_bstride;
+    const int cin = d.cin;
+    const int in_len = d.in_len;
+    const int xc = (int)d.x_cstride;
+    const float* xb = d.x + (int64_t)b * d.x_bstride;
     const float scale = d.in_scale ? d.in_scale[b] : 1.0f;
     const float slope = d.slope;
     const int t0 = n0 - d.pad;
-    const int64_t xc = d.x_cstride;
-    const int in_len = d.in_len;
-    const int cin = d.cin;
 
-    // ---- staging helpers -------------------------------------------------
+    // ---- per-element staging geometry, fixed for the whole K loop -------
+    // R == 1: element (c, w) reads x[q*CC + c][t0 + w + shift]; the chunk
+    // advances the buffer base by CC channels and shrinks its size, so the
+    // channel bound is the buffer's range check.  R > 1 (frame view): element
+    // (w, c) reads channel c' = q*CC + c -> (c'/R, c'%R), recomputed per chunk.
+    int xoff[C::XE];
+    int loff[C::XE];
+#pragma unroll
+    for (int e = 0; e < C::XE; ++e) {
+        const int idx = tid + e * 256;
+        int c, w;
+        if (R == 1) {
+            c = idx / C::W;
+            w = idx - c * C::W;
+        } else {
+            w = idx / CC;
+            c = idx - w * CC;
+        }
+        loff[e] = idx < C::XN ? c * C::WS + w : -1;
+        if (R == 1) {
+            const int pos = t0 + w + d.shift;
+            xoff[e] = (idx < C::XN && pos >= 0 && pos < in_len) ? (c * xc + pos) * 4 : kSentinel;
+        } else {
+            xoff[e] = (t0 + w) * R + d.shift;   // sample index of phase 0 of frame w
+        }
+    }
+    const float* wbase = d.w;
+    int aoff[C::AE4];
+#pragma unroll
+    for (int e = 0; e < C::AE4; ++e) {
+        const int f = min(tid + e * 256, C::AN / 4 - 1);
+        const int ml = f / (C::S * 16);
+        const int r = f - ml * (C::S * 16);
+        const int mtg = min(mt0 + ml, mtiles - 1);   // rows past M are computed, never stored
+        aoff[e] = (int)(mtg * a_mt_stride) + r * 4;   // float index of the float4
+    }
+
     float xr[C::XE];
-    float4 ar[C::AE4 > 0 ? C::AE4 : 1];
-    auto load_chunk = [&](int q) {
-#pragma unroll
-        for (int e = 0; e < C::XE; ++e) {
-            const int idx = tid + e * 256;
-            float v = 0.f;
-            if (idx < C::XN) {
-                int c, w, ci, pos;
-                if (R == 1) {
-                    c = idx / C::W;
-                    w = idx - c * C::W;
-                    ci = q * CC + c;
-                    pos = t0 + w + d.shift;
-                } else {
-                    w = idx / CC;
-                    c = idx - w * CC;
-                    const int cq = q * CC + c;
-                    ci = cq / R;
-                    pos = (t0 + w) * R + (cq - ci * R) + d.shift;
-                }
-                if (ci < cin && pos >= 0 && pos < in_len) v = x[(int64_t)ci * xc + pos];
-            }
-            xr[e] = v;
-        }
-#pragma unroll
-        for (int e = 0; e < C::AE4; ++e) {
-            const int f = min(tid + e * 256, C::AN / 4 - 1);  // float4 index in the chunk
-            const int ml = f / (C::S * 16);              // m-tile within the workgroup
-            const int r = f - ml * (C::S * 16);
-            const int mtg = min(mt0 + ml, mtiles - 1);   // clamp: rows past M are unused
-            const float4* src = (const float4*)(d.w + (int64_t)mtg * a_mt_stride +
-                                                (int64_t)q * C::S * 64) + r;
-            ar[e] = *src;
-        }
-    };
-    auto store_chunk = [&](int buf) {
-        float* xs = lds + buf * C::STAGE;
-        float* as = xs + C::XBUF;
-#pragma unroll
-        for (int e = 0; e < C::XE; ++e) {
-            const int idx = tid + e * 256;
-            if (idx < C::XN) {
-                int c, w;
-                if (R == 1) {
-                    c = idx / C::W;
-                    w = idx - c * C::W;
-                } else {
-                    w = idx / CC;
-                    c = idx - w * CC;
-                }
-                float v = xr[e] * scale;
-                v = v >= 0.f ? v : v * slope;
-                xs[c * C::WS + w] = v;
-            }
-        }
-#pragma unroll
-        for (int e = 0; e < C::AE4; ++e)
-            if (tid + e * 256 < C::AN / 4) ((float4*)as)[tid + e * 256] = ar[e];
-    };
+    float ar[4 * C::AE4];
+
+#define OU_LOAD_CHUNK(q)                                                                       \
+    {                                                                                          \
+        const int q_ = (q);                                                                    \
+        if (R == 1) {                                                                          \
+            const int nch = cin - q_ * CC;                                                     \
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(               \
+                (void*)(xb + (int64_t)q_ * CC * xc), (short)0, nch > 0 ? nch * xc * 4 : 0,     \
+                0x00020000);                                                                   \
+            _Pragma("unroll") for (int e = 0; e < C::XE; ++e) xr[e] =                          \
+                __builtin_amdgcn_raw_buffer_load_b32(rs, xoff[e], 0, 0);                       \
+        } else {                                                                               \
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(               \
+                (void*)xb, (short)0, cin * xc * 4, 0x00020000);                               \
+            _Pragma("unroll") for (int e = 0; e < C::XE; ++e) {                                \
+                const int idx = tid + e * 256;                                                 \
+                const int cq = q_ * CC + (idx - (idx / CC) * CC);                              \
+                const int ci = cq / R;                                                         \
+                const int pos = xoff[e] + (cq - ci * R);                                       \
+                const int off = (idx < C::XN && ci < cin && pos >= 0 && pos < in_len)          \
+                                    ? (ci * xc + pos) * 4                                      \
+                                    : kSentinel;                                               \
+                xr[e] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);                   \
+            }                                                                                  \
+        }                                                                                      \
+        _Pragma("unroll") for (int e = 0; e < C::AE4; ++e) {                                   \
+            const float4 v4 = *(const float4*)(wbase + aoff[e] + (int64_t)q_ * C::S * 64);     \
+            ar[4 * e] = v4.x;                                                                  \
+            ar[4 * e + 1] = v4.y;                                                              \
+            ar[4 * e + 2] = v4.z;                                                              \
+            ar[4 * e + 3] = v4.w;                                                              \
+        }                                                                                      \
+    }
+
+#define OU_STORE_CHUNK(buf)                                                                    \
+    {                                                                                          \
+        float* xs_ = lds + (buf) * C::STAGE;                                                   \
+        _Pragma("unroll") for (int e = 0; e < C::XE; ++e) {                                    \
+            float v = xr[e] * scale;                                                           \
+            v = v >= 0.f ? v : v * slope;                                                      \
+            if (loff[e] >= 0) xs_[loff[e]] = v;                                                \
+        }                                                                                      \
+        float4* as_ = (float4*)(xs_ + C::XBUF);                                                \
+        _Pragma("unroll") for (int e = 0; e < C::AE4; ++e) as_[tid + e * 256] =                \
+            make_float4(ar[4 * e], ar[4 * e + 1], ar[4 * e + 2], ar[4 * e + 3]);               \
+    }
 
     floatx16 acc[NR];
 #pragma unroll
@@ -170,13 +194,13 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
 
-    load_chunk(0);
-    store_chunk(0);
+    OU_LOAD_CHUNK(0);
+    OU_STORE_CHUNK(0);
     __syncthreads();
     for (int q = 0; q < nchunks; ++q) {
         const int cur = q & 1;
-        if (q + 1 < nchunks) load_chunk(q + 1);
-        if (active) {
+        if (q + 1 < nchunks) OU_LOAD_CHUNK(q + 1);
+        {
             const float* xs = lds + cur * C::STAGE;
             const float* as = xs + C::XBUF + wm * (C::S * 64) + lane;
             const float* xrow = xs + h * C::WS + wn * (32 * NR) + l32;
@@ -194,9 +218,11 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
                 }
             }
         }
-        if (q + 1 < nchunks) store_chunk(cur ^ 1);
+        if (q + 1 < nchunks) OU_STORE_CHUNK(cur ^ 1);
         __syncthreads();
     }
+#undef OU_LOAD_CHUNK
+#undef OU_STORE_CHUNK
 
     // ---- intra-workgroup split-K reduction (fixed order: deterministic) ----
     if (WK > 1) {
@@ -219,7 +245,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
                 for (int r = 0; r < 16; ++r)
                     acc[nr][r] += red[((((j - 1) * WM * WN + sub) * NR + nr) * 16 + r) * 64 + lane];
     }
-    if (!active) return;
+    if (mt >= mtiles) return;
 
     // ---- epilogue ----
     const int M = d.m;
@@ -265,13 +291,21 @@ constexpr Tile kTiles[] = {{1, 4, 1, 4}, {1, 4, 1, 2}, {2, 2, 1, 2}, {2, 2, 1, 1
                            {1, 1, 4, 1}, {2, 1, 2, 1}, {1, 2, 2, 1}, {4, 1, 1, 1}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
-// channel chunk per (kt, wk): ~1-2k MFMA cycles per wave per chunk
-constexpr int chunk_for(int kt, int wk) { return (kt == 1 ? 32 : 16) * (wk >= 2 ? 2 : 1); }
+constexpr int kMaxLds = 64 * 1024;
+
+// channel chunk: the largest of 64/32/16 whose double-buffered stage fits LDS
+template <int KT, int WM, int WN, int WK, int NR>
+constexpr int chunk_for()
+{
+    return Cfg<KT, 64, WM, WN, WK, NR>::LDS * 4 <= kMaxLds   ? 64
+           : Cfg<KT, 32, WM, WN, WK, NR>::LDS * 4 <= kMaxLds ? 32
+                                                              : 16;
+}
 
 template <int KT, int WM, int WN, int WK, int NR>
 int launch_t(const ou_conv_desc& d, hipStream_t s)
 {
-    constexpr int CC = chunk_for(KT, WK);
+    constexpr int CC = chunk_for<KT, WM, WN, WK, NR>();
     using C = Cfg<KT, CC, WM, WN, WK, NR>;
     const int mtiles = (d.m + 31) / 32;
     const int cin_eff = d.cin * d.frame;
@@ -288,7 +322,7 @@ int launch_t(const ou_conv_desc& d, hipStream_t s)
 template <int KT, int WM, int WN, int WK, int NR>
 constexpr int lds_bytes_t()
 {
-    return Cfg<KT, chunk_for(KT, WK), WM, WN, WK, NR>::LDS * 4;
+    return Cfg<KT, chunk_for<KT, WM, WN, WK, NR>(), WM, WN, WK, NR>::LDS * 4;
 }
 
 template <int KT>
@@ -317,8 +351,6 @@ int lds_bytes(int kt, int tile)
     }
     return -1;
 }
-
-constexpr int kMaxLds = 64 * 1024;
 
 template <int KT>
 int launch_kt(const ou_conv_desc& d, int tile, hipStream_t s)
@@ -360,7 +392,7 @@ int pick_tile(const ou_conv_desc& d)
 extern "C" int ou_conv_chunk(int kt, int frame)
 {
     (void)frame;
-    return chunk_for(kt, 1);
+    return kt == 1 ? 32 : 16;
 }
 
 extern "C" int64_t ou_conv_packed_size(int m, int cin_eff, int kt, int cc)
