@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
                 (void*)(xb + (int64_t)q_ * CC * xc), (short)0, nch > 0 ? nch * xc * 4 : 0,     \
                 0x00020000);                                                                   \
             _Pragma("unroll") for (int e = 0; e < C::XE; ++e) xr[e] =                          \
-                __builtin_amdgcn_raw_buffer_load_b32(rs, xoff[e], 0, 0);                       \
+                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, xoff[e], 0, 0));      \
         } else {                                                                               \
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(               \
                 (void*)xb, (short)0, cin * xc * 4, 0x00020000);                               \
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
                 const int off = (idx < C::XN && ci < cin && pos >= 0 && pos < in_len)          \
                                     ? (ci * xc + pos) * 4                                      \
                                     : kSentinel;                                               \
-                xr[e] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);                   \
+                xr[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));  \
             }                                                                                  \
         }                                                                                      \
         _Pragma("unroll") for (int e = 0; e < C::AE4; ++e) {                                   \
