@@ -46,7 +46,7 @@ class GruDesc(ctypes.Structure):
         ("y", fp), ("y_bstride", c_int64), ("y_cstride", c_int64),
         ("res", fp), ("res_bstride", c_int64), ("res_cstride", c_int64),
         ("res_scale", c_float), ("hidden", c_int32), ("steps", c_int32), ("batch", c_int32),
-        ("_pad", c_int32), ("granules", fp), ("status", fp),
+        ("flags", c_int32), ("granules", fp), ("status", fp),
     ]
 
 

@@ -30,29 +30,51 @@
 
 namespace {
 
-constexpr int kUnitsPerWG = 32;
 constexpr int kMaxBatchPerWG = 4;
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-template <int H, int NB>
-__global__ __launch_bounds__(256) void gru_kernel(ou_gru_desc d, int nb)
+// One "chain" = one (batch group, direction): G = H/U workgroups of 8*U
+// threads, each owning U hidden units.  Chains are independent; a workgroup
+// of a chain only talks to the other members of the same chain.
+//
+// Placement (flags & 1): block ids are laid out so that the G members of a
+// chain share blockIdx % 8 -- observed to put them on one XCD (one L2), which
+// shortens every hand-off.  Speed only: correctness never depends on where
+// a block runs (the hand-off is agent-scope sc1 granules).
+template <int H, int NB, int U>
+__global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int nchains, int flags)
 {
+    constexpr int G = H / U;             // workgroups per chain
+    constexpr int NT = 8 * U;            // threads
     constexpr int KPL = H / 8;           // k-slice per lane
     constexpr int SEG = KPL + 4;         // padded LDS segment (bank spread)
     __shared__ __attribute__((aligned(16))) float hs[NB][8 * SEG];
     __shared__ int abort_flag;
+
+    const int bid = blockIdx.x;
+    int chain, member;
+    if (flags & 1) {
+        const int c8 = bid & 7, rest = bid >> 3;
+        member = rest % G;
+        chain = (rest / G) * 8 + c8;
+    } else {
+        chain = bid / G;
+        member = bid % G;
+    }
+    if (chain >= nchains) return;        // padding block of the XCD layout
+    const int dir = chain & 1;
+    const int b0 = (chain >> 1) * nb;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int kg = lane & 7;
     const int u = lane >> 3;
-    const int j = blockIdx.x * kUnitsPerWG + wave * 8 + u;   // hidden unit
-    const int dir = blockIdx.y;
-    const int b0 = blockIdx.z * nb;
+    const int j = member * U + wave * 8 + u;   // hidden unit
     const int nbh = min(nb, d.batch - b0);
     const int T = d.steps;
+    const bool sleep_poll = !(flags & 2);
     if (tid == 0) abort_flag = 0;
 
     // W_hh rows of this unit (gates r, z, n), k-slice of this lane, in VGPRs
@@ -78,7 +100,8 @@ __global__ __launch_bounds__(256) void gru_kernel(ou_gru_desc d, int nb)
 
     for (int t = 0; t < T; ++t) {
         const int time = dir == 0 ? t : T - 1 - t;
-        // prefetch this step's input projections (only the kg==0 lanes use them)
+        // this step's input projections (only the kg==0 lanes use them);
+        // issued before the wait so their latency hides under it
         float gir[NB], giz[NB], gin[NB];
         if (kg == 0) {
 #pragma unroll
@@ -93,21 +116,21 @@ __global__ __launch_bounds__(256) void gru_kernel(ou_gru_desc d, int nb)
         }
         // gather h_{t-1}
         if (t == 0) {
-            for (int i = tid; i < nbh * H; i += 256) {
+            for (int i = tid; i < nbh * H; i += NT) {
                 const int bb = i / H, k = i - bb * H;
                 hs[bb][(k / KPL) * SEG + (k % KPL)] = 0.f;
             }
         } else {
             const uint32_t want = (uint32_t)t;   // tag of h_{t-1}
             const int par = (t - 1) & 1;
-            for (int i = tid; i < nbh * H; i += 256) {
+            for (int i = tid; i < nbh * H; i += NT) {
                 const int bb = i / H, k = i - bb * H;
                 uint64_t* p = gran + gidx(b0 + bb, par, k);
                 uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 uint32_t spins = 0;
                 while ((uint32_t)(v >> 32) != want) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 22)) {   // ~seconds: the chain is dead
+                    if (sleep_poll) __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 23)) {   // ~seconds: the chain is dead
                         atomicExch(d.status, 1);
                         abort_flag = 1;
                         break;
@@ -163,6 +186,31 @@ __global__ __launch_bounds__(256) void gru_kernel(ou_gru_desc d, int nb)
     }
 }
 
+template <int H, int NB, int U>
+void launch_u(const ou_gru_desc& d, int nb, int nchains, int flags, hipStream_t s)
+{
+    constexpr int G = H / U;
+    const int grid = (flags & 1) ? 8 * G * ((nchains + 7) / 8) : nchains * G;
+    hipLaunchKernelGGL((gru_kernel<H, NB, U>), dim3(grid), dim3(8 * U), 0, s, d, nb, nchains, flags);
+}
+
+template <int H, int NB>
+void launch_nb(const ou_gru_desc& d, int nb, int nchains, int flags, hipStream_t s)
+{
+    if ((flags & 4) && H >= 64 && H % 64 == 0)
+        launch_u<H, NB, (H >= 64 ? 64 : 32)>(d, nb, nchains, flags, s);
+    else
+        launch_u<H, NB, 32>(d, nb, nchains, flags, s);
+}
+
+template <int H>
+void launch_h(const ou_gru_desc& d, int nb, int nchains, int flags, hipStream_t s)
+{
+    if (nb == 1) launch_nb<H, 1>(d, nb, nchains, flags, s);
+    else if (nb == 2) launch_nb<H, 2>(d, nb, nchains, flags, s);
+    else launch_nb<H, 4>(d, nb, nchains, flags, s);
+}
+
 }  // namespace
 
 extern "C" int64_t ou_gru_workspace_bytes(int hidden, int batch)
@@ -181,24 +229,18 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
     OU_HIP_CHECK(hipMemsetAsync(d.granules, 0, ou_gru_workspace_bytes(d.hidden, d.batch), s),
                  "gru: memset");
     const int nb = d.batch >= kMaxBatchPerWG ? kMaxBatchPerWG : (d.batch >= 2 ? 2 : 1);
-    dim3 grid(d.hidden / kUnitsPerWG, 2, (d.batch + nb - 1) / nb);
-    // every workgroup of a chain must be resident at once: at most a few
-    // hundred 256-thread workgroups, far below 256 CUs x 4.
-    if (grid.x * grid.y * grid.z > 512) return ou_fail(-2, "gru: grid too large for residency");
-#define OU_GRU_CASE(HH)                                                                \
-    case HH:                                                                           \
-        if (nb == 1) hipLaunchKernelGGL((gru_kernel<HH, 1>), grid, dim3(256), 0, s, d, nb); \
-        else if (nb == 2) hipLaunchKernelGGL((gru_kernel<HH, 2>), grid, dim3(256), 0, s, d, nb); \
-        else hipLaunchKernelGGL((gru_kernel<HH, 4>), grid, dim3(256), 0, s, d, nb);      \
-        break;
+    const int nchains = 2 * ((d.batch + nb - 1) / nb);
+    const int flags = d.flags < 0 ? 1 : d.flags;   // default: XCD-local chains
+    // every workgroup of a chain must be resident at once: a few hundred
+    // workgroups at most, far below 256 CUs x 4
+    if (nchains * (d.hidden / 32) > 512) return ou_fail(-2, "gru: grid too large for residency");
     switch (d.hidden) {
-        OU_GRU_CASE(32)
-        OU_GRU_CASE(64)
-        OU_GRU_CASE(128)
-        OU_GRU_CASE(256)
-        OU_GRU_CASE(384)
+    case 32: launch_h<32>(d, nb, nchains, flags, s); break;
+    case 64: launch_h<64>(d, nb, nchains, flags, s); break;
+    case 128: launch_h<128>(d, nb, nchains, flags, s); break;
+    case 256: launch_h<256>(d, nb, nchains, flags, s); break;
+    case 384: launch_h<384>(d, nb, nchains, flags, s); break;
     default: return ou_fail(-1, "gru: unsupported hidden size %d", d.hidden);
     }
-#undef OU_GRU_CASE
     return ou_check_launch("gru");
 }

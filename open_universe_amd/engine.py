@@ -289,6 +289,9 @@ def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film
     prog.add(L.OP_CONV, conv_desc(bw.conv3, tB, out, res1=h, s1=NF2, res2=res2, s2=s2))
 
 
+GRU_FLAGS = -1   # kernel default (XCD-local chains); see ou_gru_desc.flags
+
+
 def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, res: Act = None,
             res_scale=1.0):
     proj, w_hh, b_hh = gw.layers[layer]
@@ -306,6 +309,7 @@ def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, re
         d.res, d.res_bstride, d.res_cstride, d.res_scale = res.ptr, res.bs, res.cs, res_scale
     d.hidden, d.steps, d.batch = gw.hidden, x.T, x.B
     d.granules, d.status = granules.data_ptr(), status.data_ptr()
+    d.flags = GRU_FLAGS
     d._flops = 2.0 * 2 * 3 * H * H * x.T * x.B
     prog.add(L.OP_GRU, d)
 

@@ -1,0 +1,49 @@
+"""Time the GRU recurrence variants (ou_gru_desc.flags) at score-network
+shape (H = 256, T = 801) for a few batch sizes; prints us per time step."""
+import sys
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from open_universe_amd import _lib as L
+from open_universe_amd import engine as E
+from open_universe_amd.configs import get_config
+from open_universe_amd.networks.universe import UniverseGAN
+from open_universe_amd.utils.synthetic import synth_state_dict
+
+
+def main():
+    dev = "cuda:0"
+    cfg = get_config("pp16")
+    m = UniverseGAN(**{k: v for k, v in cfg.items() if k != "_target_"})
+    m.load_state_dict(synth_state_dict([(k, v.shape) for k, v in m.state_dict().items()]), strict=False)
+    m = m.to(dev).eval()
+    eng = m._get_engine()
+    T = 801
+    stream = torch.cuda.current_stream().cuda_stream
+    for B in (1, 4, 8):
+        x = E.Act(torch.randn(B, 512, T, device=dev) * 0.5)
+        gi, y = E.new_act(B, 1536, T, dev), E.new_act(B, 512, T, dev)
+        gran = torch.zeros(L.load().ou_gru_workspace_bytes(256, B) // 8, dtype=torch.int64, device=dev)
+        ref = None
+        for flags in (0, 1, 2, 3, 4, 5, 7):
+            E.GRU_FLAGS = flags
+            prog = L.Program()
+            E.rec_gru(prog, eng.s_gru, 0, x, gi, y, gran, eng.status)
+            prog.run(stream)
+            torch.cuda.synchronize()
+            ms = []
+            for _ in range(5):
+                t = prog.profile(stream)
+                ms.append(t[1])
+            out = y.t.clone()
+            if ref is None:
+                ref = out
+            ok = torch.equal(out, ref) and int(eng.status.max()) == 0
+            print(f"B={B} flags={flags}: {1000 * min(ms) / T:.3f} us/step "
+                  f"(median {1000 * sorted(ms)[2] / T:.3f}) identical={ok}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
