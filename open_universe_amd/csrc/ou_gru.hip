@@ -98,22 +98,30 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
         return (((int64_t)b * 2 + dir) * 2 + par) * H + k;
     };
 
-    for (int t = 0; t < T; ++t) {
-        const int time = dir == 0 ? t : T - 1 - t;
-        // this step's input projections (only the kg==0 lanes use them);
-        // issued before the wait so their latency hides under it
-        float gir[NB], giz[NB], gin[NB];
-        if (kg == 0) {
+    // per-step operands of this lane's unit: gi (3 gates) and the optional
+    // output residual, prefetched one step ahead (issued right after the
+    // gather barrier, so they are never queued in front of the next poll)
+    float gir[NB], giz[NB], gin[NB], rsd[NB];
+    auto prefetch = [&](int step, float* pr, float* pz, float* pn, float* pres) {
+        const int tm = dir == 0 ? step : T - 1 - step;
 #pragma unroll
-            for (int bb = 0; bb < NB; ++bb) {
-                if (bb >= nbh) break;
+        for (int bb = 0; bb < NB; ++bb) {
+            if (bb < nbh && kg == 0) {
                 const float* g = d.gi + (int64_t)(b0 + bb) * d.gi_bstride +
-                                 (int64_t)(dir * 3 * H) * T + time;
-                gir[bb] = g[(int64_t)(0 * H + j) * T];
-                giz[bb] = g[(int64_t)(1 * H + j) * T];
-                gin[bb] = g[(int64_t)(2 * H + j) * T];
+                                 (int64_t)(dir * 3 * H) * T + tm;
+                pr[bb] = g[(int64_t)(0 * H + j) * T];
+                pz[bb] = g[(int64_t)(1 * H + j) * T];
+                pn[bb] = g[(int64_t)(2 * H + j) * T];
+                pres[bb] = d.res ? d.res[(int64_t)(b0 + bb) * d.res_bstride +
+                                         (int64_t)(dir * H + j) * d.res_cstride + tm]
+                                 : 0.f;
             }
         }
+    };
+    prefetch(0, gir, giz, gin, rsd);
+
+    for (int t = 0; t < T; ++t) {
+        const int time = dir == 0 ? t : T - 1 - t;
         // gather h_{t-1}
         if (t == 0) {
             for (int i = tid; i < nbh * H; i += NT) {
@@ -143,6 +151,13 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
         __syncthreads();
         if (abort_flag) return;   // uniform across the workgroup
 
+        float cr[NB], cz[NB], cn[NB], cres[NB];
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) {
+            cr[bb] = gir[bb]; cz[bb] = giz[bb]; cn[bb] = gin[bb]; cres[bb] = rsd[bb];
+        }
+        if (t + 1 < T) prefetch(t + 1, gir, giz, gin, rsd);
+
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb) {
             if (bb >= nbh) break;
@@ -164,9 +179,9 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
             }
             if (kg == 0) {
                 const float hprev = hs[bb][(j / KPL) * SEG + (j % KPL)];
-                const float r = sigmoidf_(gir[bb] + (sr + bhr));
-                const float z = sigmoidf_(giz[bb] + (sz + bhz));
-                const float n = tanhf(gin[bb] + r * (sn + bhn));
+                const float r = sigmoidf_(cr[bb] + (sr + bhr));
+                const float z = sigmoidf_(cz[bb] + (sz + bhz));
+                const float n = tanhf(cn[bb] + r * (sn + bhn));
                 const float hn = (1.0f - z) * n + z * hprev;
                 const int b = b0 + bb;
                 if (t + 1 < T) {
@@ -174,11 +189,8 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
                     __hip_atomic_store(gran + gidx(b, t & 1, j), g, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 }
-                float out = hn;
                 const int64_t c = (int64_t)(dir * H + j);
-                if (d.res)
-                    out = (hn + d.res[(int64_t)b * d.res_bstride + c * d.res_cstride + time]) *
-                          d.res_scale;
+                const float out = d.res ? (hn + cres[bb]) * d.res_scale : hn;
                 d.y[(int64_t)b * d.y_bstride + c * d.y_cstride + time] = out;
             }
         }
