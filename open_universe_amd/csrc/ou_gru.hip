@@ -129,23 +129,45 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
                 hs[bb][(k / KPL) * SEG + (k % KPL)] = 0.f;
             }
         } else {
+            // all of this thread's granules are requested at once; only the
+            // stale ones are re-polled (one L2 round trip per pass, not per granule)
             const uint32_t want = (uint32_t)t;   // tag of h_{t-1}
             const int par = (t - 1) & 1;
-            for (int i = tid; i < nbh * H; i += NT) {
+            constexpr int NPER = (NB * H + NT - 1) / NT;
+            uint64_t v[NPER];
+            uint64_t* pp[NPER];
+#pragma unroll
+            for (int e = 0; e < NPER; ++e) {
+                const int i = tid + e * NT;
                 const int bb = i / H, k = i - bb * H;
-                uint64_t* p = gran + gidx(b0 + bb, par, k);
-                uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                uint32_t spins = 0;
-                while ((uint32_t)(v >> 32) != want) {
-                    if (sleep_poll) __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 23)) {   // ~seconds: the chain is dead
-                        atomicExch(d.status, 1);
-                        abort_flag = 1;
-                        break;
-                    }
-                    v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                pp[e] = gran + gidx(b0 + min(bb, nbh - 1), par, k);
+                v[e] = (i < nbh * H) ? __hip_atomic_load(pp[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : ((uint64_t)want << 32);
+            }
+            uint32_t spins = 0;
+            while (true) {
+                bool ok = true;
+#pragma unroll
+                for (int e = 0; e < NPER; ++e) ok &= (uint32_t)(v[e] >> 32) == want;
+                if (ok) break;
+                if (sleep_poll) __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 23)) {   // ~seconds: the chain is dead
+                    atomicExch(d.status, 1);
+                    abort_flag = 1;
+                    break;
                 }
-                hs[bb][(k / KPL) * SEG + (k % KPL)] = __uint_as_float((uint32_t)v);
+#pragma unroll
+                for (int e = 0; e < NPER; ++e)
+                    if ((uint32_t)(v[e] >> 32) != want)
+                        v[e] = __hip_atomic_load(pp[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int e = 0; e < NPER; ++e) {
+                const int i = tid + e * NT;
+                if (i < nbh * H) {
+                    const int bb = i / H, k = i - bb * H;
+                    hs[bb][(k / KPL) * SEG + (k % KPL)] = __uint_as_float((uint32_t)v[e]);
+                }
             }
         }
         __syncthreads();
@@ -242,7 +264,8 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
                  "gru: memset");
     const int nb = d.batch >= kMaxBatchPerWG ? kMaxBatchPerWG : (d.batch >= 2 ? 2 : 1);
     const int nchains = 2 * ((d.batch + nb - 1) / nb);
-    const int flags = d.flags < 0 ? 1 : d.flags;   // default: XCD-local chains
+    // default: XCD-local chains, 64-unit workgroups (fewer producers per hand-off)
+    const int flags = d.flags < 0 ? 5 : d.flags;
     // every workgroup of a chain must be resident at once: a few hundred
     // workgroups at most, far below 256 CUs x 4
     if (nchains * (d.hidden / 32) > 512) return ou_fail(-2, "gru: grid too large for residency");
