@@ -34,6 +34,18 @@ constexpr int kMaxBatchPerWG = 4;
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Sum over the 8 consecutive lanes of a group with DPP (no LDS round trip):
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], then row_half_mirror (i <-> 7-i)
+// adds the other quad.  Every lane of the group ends with the total.
+#define OU_DPP(v, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (v)), (ctrl), 0xF, 0xF, true))
+__device__ __forceinline__ float sum8(float v)
+{
+    v += OU_DPP(v, 0xB1);
+    v += OU_DPP(v, 0x4E);
+    v += OU_DPP(v, 0x141);
+    return v;
+}
+
 // One "chain" = one (batch group, direction): G = H/U workgroups of 8*U
 // threads, each owning U hidden units.  Chains are independent; a workgroup
 // of a chain only talks to the other members of the same chain.
@@ -193,12 +205,9 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
                 sr = fmaf(wr[k + 2], hq.z, sr); sz = fmaf(wz[k + 2], hq.z, sz); sn = fmaf(wn[k + 2], hq.z, sn);
                 sr = fmaf(wr[k + 3], hq.w, sr); sz = fmaf(wz[k + 3], hq.w, sz); sn = fmaf(wn[k + 3], hq.w, sn);
             }
-#pragma unroll
-            for (int off = 1; off < 8; off <<= 1) {
-                sr += __shfl_xor(sr, off);
-                sz += __shfl_xor(sz, off);
-                sn += __shfl_xor(sn, off);
-            }
+            sr = sum8(sr);
+            sz = sum8(sz);
+            sn = sum8(sn);
             if (kg == 0) {
                 const float hprev = hs[bb][(j / KPL) * SEG + (j % KPL)];
                 const float r = sigmoidf_(cr[bb] + (sr + bhr));
