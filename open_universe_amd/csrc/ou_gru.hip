@@ -273,8 +273,10 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
                  "gru: memset");
     const int nb = d.batch >= kMaxBatchPerWG ? kMaxBatchPerWG : (d.batch >= 2 ? 2 : 1);
     const int nchains = 2 * ((d.batch + nb - 1) / nb);
-    // default: XCD-local chains, 64-unit workgroups (fewer producers per hand-off)
-    const int flags = d.flags < 0 ? 5 : d.flags;
+    // default: XCD-local chains; 64-unit workgroups (fewer producers per
+    // hand-off) for one item per chain, 32-unit ones when a workgroup carries
+    // several items (measured: tools/gru_bench.py)
+    const int flags = d.flags >= 0 ? d.flags : (nb == 1 ? 5 : 1);
     // every workgroup of a chain must be resident at once: a few hundred
     // workgroups at most, far below 256 CUs x 4
     if (nchains * (d.hidden / 32) > 512) return ou_fail(-2, "gru: grid too large for residency");
