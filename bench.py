@@ -131,9 +131,9 @@ def main():
 
     from open_universe_amd.utils.synthetic import synth_audio
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from open_universe_amd.sharding import dist_env, max_over_ranks
+
+    rank, local, world = dist_env()
     if world > 1:
         dist.init_process_group("gloo")
     torch.cuda.set_device(local)
@@ -159,10 +159,7 @@ def main():
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed)
 
     prof = None
     if not args.no_profile:

@@ -193,16 +193,20 @@ class Universe(nn.Module):
             mix = mix.to(torch.float32).contiguous()
             eng = self._get_engine()
             B, _, T = mix.shape
+            # mean / median reduce on the device inside the plan; signal_median
+            # needs the whole ensemble (tensor ops below)
+            ens_mode = {"mean": 0, "median": 1}.get(ensemble_stat) if ensemble is not None else None
             key = (B, T, int(n_steps), float(epsilon), bool(keep_rms), bool(use_aux_signal),
-                   warm_start)
+                   warm_start, ensemble, ens_mode)
             plan = self._plans.get(key)
             if plan is None:
                 plan = EnhancePlan(eng, B, T, int(n_steps), float(epsilon), keep_rms=bool(keep_rms),
                                    use_aux_signal=bool(use_aux_signal), warm_start=warm_start,
-                                   diff=dict(self.diff_kwargs))
+                                   diff=dict(self.diff_kwargs), ensemble=ensemble,
+                                   ensemble_mode=ens_mode)
                 self._plans[key] = plan
             x = plan(mix, rng).clone()[:, None, :]
-            if ensemble is not None:
+            if ensemble is not None and ens_mode is None:
                 x = self._ensemble_reduce(x.view((-1,) + tuple(mix_shape)), ensemble_stat)
         if x_ndim == 1:
             x = x[0, 0]

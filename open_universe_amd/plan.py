@@ -71,7 +71,8 @@ class EnhancePlan(_PlanBase):
     """The whole enhance() for a fixed (batch, length, n_steps, options)."""
 
     def __init__(self, eng, batch, mix_len, n_steps, epsilon, keep_rms=False,
-                 use_aux_signal=False, warm_start=None, diff=None):
+                 use_aux_signal=False, warm_start=None, diff=None, ensemble=None,
+                 ensemble_mode=None):
         super().__init__(eng)
         dev, B = self.dev, batch
         self.B, self.mix_len, self.n_steps = B, mix_len, n_steps
@@ -175,6 +176,14 @@ class EnhancePlan(_PlanBase):
         p.add(L.OP_FINISH, L.FinishArgs(x=x_final.ptr, x_bstride=Tp, left=self.pad // 2,
                                         batch=B, len=mix_len, y=self.OUT.data_ptr(),
                                         mix_rms=self.MIXRMS.data_ptr() if keep_rms else 0))
+        # ensemble reduction (universe.py:359-366): B = E x B0 results -> B0
+        self.RED = None
+        if ensemble is not None and ensemble_mode is not None:
+            assert B % ensemble == 0
+            self.RED = torch.empty((B // ensemble, mix_len), dtype=torch.float32, device=dev)
+            p.add(L.OP_ENSEMBLE, L.EnsembleArgs(x=self.OUT.data_ptr(), y=self.RED.data_ptr(),
+                                                ensemble=ensemble, mode=ensemble_mode,
+                                                n=(B // ensemble) * mix_len))
 
     def draw_noise(self, rng):
         """Noise in the reference's draw order (universe.py:39-41,326,338):
@@ -194,7 +203,7 @@ class EnhancePlan(_PlanBase):
         stream = torch.cuda.current_stream(self.dev).cuda_stream
         self._launch(stream, use_graph)
         self.check()
-        return self.OUT
+        return self.OUT if self.RED is None else self.RED
 
 
 class ScorePlan(_PlanBase):
