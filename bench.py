@@ -123,6 +123,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--dump-ops", default=None, help="write per-op profile rows (JSON)")
+    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "pmc_latest.json"),
+                    help="per-kernel HBM traffic from tools/pmc_summary.py (rocprofv3 PMC passes)")
     args = ap.parse_args()
 
     import numpy as np
@@ -198,9 +200,19 @@ def main():
         }
         if prof is not None:
             achieved = prof["conv_flops"] / (prof["conv_ms"] * 1e-3) / 1e12
+            traffic, tsrc = None, None
+            if args.traffic_json and os.path.exists(args.traffic_json):
+                with open(args.traffic_json) as fh:
+                    pmc = json.load(fh)
+                row = pmc.get("kernels", {}).get("conv_kernel")
+                if row:
+                    traffic = row["traffic_bytes_per_launch"]
+                    tsrc = (f"{os.path.relpath(args.traffic_json, HERE)} ({pmc.get('tag', '')}): "
+                            "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes per ou_conv launch")
             out["roofline"] = {
                 "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TF,
-                "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TF, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TF, 4), "traffic": traffic,
+                "traffic_source": tsrc,
                 "kernel": "ou_conv (conv_kernel, all launches of one enhance)",
                 "launches": prof["n_conv"],
                 "avg_launch_ms": round(prof["conv_ms"] / prof["n_conv"], 5),

@@ -327,11 +327,27 @@ def level_lengths(T, rates):
 class ConvTuner:
     """Times every tile configuration that fits LDS for a conv geometry (on the
     current stream, with HIP events) and keeps the fastest.  Plans are built
-    once per input shape, so this runs once per distinct layer geometry."""
+    once per input shape, so this runs once per distinct layer geometry.
+    With ``path`` (env OUHIP_TUNE_CACHE) the choices persist across processes
+    as JSON; a cached geometry launches nothing at plan build."""
 
-    def __init__(self, reps=3):
+    def __init__(self, reps=3, path=None):
+        import json
+        import os
+
         self.cache = {}
         self.reps = reps
+        self.path = path
+        if path and os.path.exists(path):
+            with open(path) as fh:
+                self.cache = {tuple(json.loads(k)): v for k, v in json.load(fh).items()}
+
+    def _save(self):
+        import json
+
+        if self.path:
+            with open(self.path, "w") as fh:
+                json.dump({json.dumps(list(k)): v for k, v in self.cache.items()}, fh)
 
     @staticmethod
     def key(d):
@@ -364,6 +380,7 @@ class ConvTuner:
                 best, best_ms = t, ms
         d.tile = -1
         self.cache[k] = best
+        self._save()
         return best
 
 
@@ -376,7 +393,7 @@ def enable_autotune(flag=True):
 
     if flag and os.environ.get("OUHIP_AUTOTUNE", "1") != "0":
         if _TUNER is None:
-            _TUNER = ConvTuner()
+            _TUNER = ConvTuner(path=os.environ.get("OUHIP_TUNE_CACHE") or None)
         L.TUNER = _TUNER
     else:
         L.TUNER = None

@@ -1,0 +1,63 @@
+#!/usr/bin/env python
+"""Per-kernel HBM traffic from rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+    python tools/pmc_summary.py FETCH_CSV WRITE_CSV [--out JSON]
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 correction
+(MI355X_MICROARCH.md, HBM/rocprofv3 section): FETCH_SIZE reports half the bytes
+of wide coalesced reads, so it is doubled; WRITE_SIZE is taken as is.  The
+Infinity Cache (256 MiB) hits are counted as fetches too, so this is an upper
+bound on HBM reads.
+"""
+import argparse
+import collections
+import csv
+import json
+import re
+
+
+def short(name):
+    name = re.sub(r"\(.*", "", name.strip())
+    name = re.sub(r"<.*", "", name)
+    return name.split("::")[-1].replace("void ", "").strip()
+
+
+def read(path, counter):
+    per = collections.defaultdict(float)  # (dispatch, kernel) -> value
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            if row.get("Counter_Name") != counter:
+                continue
+            per[(row["Dispatch_Id"], short(row["Kernel_Name"]))] += float(row["Counter_Value"])
+    agg = collections.defaultdict(lambda: [0, 0.0])
+    for (_, k), v in per.items():
+        agg[k][0] += 1
+        agg[k][1] += v
+    return agg
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--out")
+    ap.add_argument("--tag", default="")
+    a = ap.parse_args()
+    f, w = read(a.fetch, "FETCH_SIZE"), read(a.write, "WRITE_SIZE")
+    rows = {}
+    for k in sorted(set(f) | set(w)):
+        n = max(f[k][0], w[k][0])
+        fb = 2.0 * 1024.0 * f[k][1] / max(f[k][0], 1)
+        wb = 1024.0 * w[k][1] / max(w[k][0], 1)
+        rows[k] = {"dispatches": n, "fetch_bytes_per_launch": round(fb),
+                   "write_bytes_per_launch": round(wb),
+                   "traffic_bytes_per_launch": round(fb + wb)}
+    out = {"tag": a.tag, "correction": "FETCH_SIZE x2 (gfx950), KiB->bytes", "kernels": rows}
+    txt = json.dumps(out, indent=1)
+    print(txt)
+    if a.out:
+        open(a.out, "w").write(txt + "\n")
+
+
+if __name__ == "__main__":
+    main()
