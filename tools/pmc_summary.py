@@ -17,7 +17,8 @@ import re
 
 
 def short(name):
-    name = re.sub(r"\(.*", "", name.strip())
+    name = name.strip().replace("(anonymous namespace)::", "")
+    name = re.sub(r"\(.*", "", name)
     name = re.sub(r"<.*", "", name)
     return name.split("::")[-1].replace("void ", "").strip()
 
