@@ -130,7 +130,9 @@ typedef struct ou_gru_desc {
     int32_t steps;             /* T                                               */
     int32_t batch;
     int32_t flags;             /* -1 default; bit0 XCD-local chains, bit1 spin    */
-                               /* without s_sleep, bit2 64-unit workgroups        */
+                               /* without s_sleep, bit2 64-unit workgroups, bit3  */
+                               /* 128-unit workgroups, bit4 timing diagnostic     */
+                               /* (skips the hand-off wait: wrong results)        */
     uint64_t* granules;        /* workspace: ou_gru_workspace_bytes()             */
     int32_t* status;           /* device int, set nonzero on spin timeout         */
 } ou_gru_desc;

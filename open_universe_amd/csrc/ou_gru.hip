@@ -32,6 +32,23 @@ namespace {
 
 constexpr int kMaxBatchPerWG = 4;
 
+// workspace after the granules: one XCC-id slot per (item, direction, member)
+__host__ __device__ constexpr int64_t xcc_slot_base(int batch, int hidden) { return (int64_t)batch * 4 * hidden; }
+__host__ __device__ constexpr int64_t xcc_slot_count(int batch, int hidden) { return (int64_t)batch * hidden / 4; }
+
+// Diagnostic build only (-DOU_GRU_STAMPS, tools/gru_bench.py): thread 0 of
+// every workgroup sums s_memtime deltas per phase of the step loop and writes
+// them after the granules (5 phases + step count per workgroup).
+#ifdef OU_GRU_STAMPS
+constexpr int kStampSlots = 8;
+#define OU_STAMP_INIT uint64_t st_[5] = {0, 0, 0, 0, 0}; uint64_t tp_ = __builtin_amdgcn_s_memtime();
+#define OU_STAMP(i) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); st_[i] += n_ - tp_; tp_ = n_; } while (0)
+#else
+constexpr int kStampSlots = 0;
+#define OU_STAMP_INIT
+#define OU_STAMP(i) do { } while (0)
+#endif
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // Sum over the 8 consecutive lanes of a group with DPP (no LDS round trip):
@@ -87,6 +104,7 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
     const int nbh = min(nb, d.batch - b0);
     const int T = d.steps;
     const bool sleep_poll = !(flags & 2);
+    const bool nowait = flags & 16;      // timing diagnostic only: results are wrong
     if (tid == 0) abort_flag = 0;
 
     // W_hh rows of this unit (gates r, z, n), k-slice of this lane, in VGPRs
@@ -131,6 +149,7 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
         }
     };
     prefetch(0, gir, giz, gin, rsd);
+    OU_STAMP_INIT
 
     for (int t = 0; t < T; ++t) {
         const int time = dir == 0 ? t : T - 1 - t;
@@ -159,6 +178,7 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
             uint32_t spins = 0;
             while (true) {
                 bool ok = true;
+                if (nowait) break;
 #pragma unroll
                 for (int e = 0; e < NPER; ++e) ok &= (uint32_t)(v[e] >> 32) == want;
                 if (ok) break;
@@ -173,6 +193,7 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
                     if ((uint32_t)(v[e] >> 32) != want)
                         v[e] = __hip_atomic_load(pp[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            OU_STAMP(0);
 #pragma unroll
             for (int e = 0; e < NPER; ++e) {
                 const int i = tid + e * NT;
@@ -184,6 +205,7 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
         }
         __syncthreads();
         if (abort_flag) return;   // uniform across the workgroup
+        OU_STAMP(1);
 
         float cr[NB], cz[NB], cn[NB], cres[NB];
 #pragma unroll
@@ -208,6 +230,7 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
             sr = sum8(sr);
             sz = sum8(sz);
             sn = sum8(sn);
+            OU_STAMP(2);
             if (kg == 0) {
                 const float hprev = hs[bb][(j / KPL) * SEG + (j % KPL)];
                 const float r = sigmoidf_(cr[bb] + (sr + bhr));
@@ -225,8 +248,338 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
                 d.y[(int64_t)b * d.y_bstride + c * d.y_cstride + time] = out;
             }
         }
+        OU_STAMP(3);
         __syncthreads();
+        OU_STAMP(4);
     }
+#ifdef OU_GRU_STAMPS
+    if (tid == 0) {
+        uint64_t* o = gran + xcc_slot_base(d.batch, H) + xcc_slot_count(d.batch, H) + (int64_t)bid * kStampSlots;
+        for (int i = 0; i < 5; ++i) o[i] = st_[i];
+        o[5] = T;
+    }
+#endif
+}
+
+
+// ---------------------------------------------------------------------------
+// k-split recurrence (default for H % 64 == 0).
+//
+// Lane L of a wave owns the k-slice [L*KPL, (L+1)*KPL) of h (KPL = H/64) for
+// ALL 8 hidden units of its wave: W_hh[g*H + j][k-slice] for 8 units x 3
+// gates sits in 24*KPL VGPRs.  Every wave is self-contained: it polls the
+// granules of its own k-slice (16-byte sc1 loads, two granules each), so
+// there is no LDS staging and no workgroup barrier in the step loop.  The 24
+// per-lane partial sums are reduced with a reduce-scatter -- permlane32_swap,
+// permlane16_swap, DPP row_ror:8 (each halves the values a lane carries),
+// then an 8-lane DPP sum -- which leaves lane L with the r/z/n sums of unit
+// L >> 3 (replicated on 8 lanes).  Each lane keeps its unit's h_{t-1} in a
+// register; one lane per unit publishes h_t.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float fast_sigmoid(float x)
+{
+    // 1 / (1 + 2^(-x log2 e)): v_exp_f32 + v_rcp_f32 (~1 ulp each)
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
+}
+__device__ __forceinline__ float fast_tanh(float x)
+{
+    // 2 sigmoid(2x) - 1: absolute error ~1e-7 around 0, relative ~1e-7 elsewhere
+    return fmaf(2.0f, fast_sigmoid(2.0f * x), -1.0f);
+}
+
+__device__ __forceinline__ void swap32(float& x, float& y)
+{
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    x = __uint_as_float(r[0]);
+    y = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap16(float& x, float& y)
+{
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    x = __uint_as_float(r[0]);
+    y = __uint_as_float(r[1]);
+}
+
+constexpr int kKsWaves = 4;   // waves per workgroup
+
+
+template <int H, int NB, int UW>
+__global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, int nb, int nchains, int flags,
+                                                               int bofs)
+{
+    constexpr int KPL = H / 64;
+    constexpr int G = H / (UW * kKsWaves);   // workgroups per chain
+    constexpr int NV = UW * 3 * NB;          // partial sums per lane
+    constexpr int NG = 3 * NB;               // sums left per lane after the scatter
+    constexpr int USH = UW == 8 ? 3 : 4;     // unit of lane L = L >> USH
+    static_assert(H % 64 == 0 && G >= 1 && (UW == 4 || UW == 8), "k-split GRU: H % 64 == 0, UW 4 or 8");
+
+    const int bid = blockIdx.x;
+    int chain, member;
+    if (flags & 1) {
+        const int c8 = bid & 7, rest = bid >> 3;
+        member = rest % G;
+        chain = (rest / G) * 8 + c8;
+    } else {
+        chain = bid / G;
+        member = bid % G;
+    }
+    if (chain >= nchains) return;            // padding block of the XCD layout
+    const int dir = chain & 1;
+    const int b0 = bofs + (chain >> 1) * nb;
+    const int nbh = min(nb, d.batch - b0);
+    const int T = d.steps;
+    const bool sleep_poll = !(flags & 2);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int ubase = (member * kKsWaves + wave) * UW;
+    const int j = ubase + (lane >> USH);     // unit whose gates this lane computes
+    const bool writer = (lane & ((1 << USH) - 1)) == 0;
+
+    float w[UW][3][KPL];
+    const float* wbase = d.w_hh + (int64_t)dir * 3 * H * H + lane * KPL;
+#pragma unroll
+    for (int u = 0; u < UW; ++u)
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+#pragma unroll
+            for (int k = 0; k < KPL; ++k) w[u][g][k] = wbase[(int64_t)(g * H + ubase + u) * H + k];
+    const float bhr = d.b_hh[dir * 3 * H + 0 * H + j];
+    const float bhz = d.b_hh[dir * 3 * H + 1 * H + j];
+    const float bhn = d.b_hh[dir * 3 * H + 2 * H + j];
+
+    // granules [B][2 dir][2 parity][H]; this lane reads KPL consecutive ones
+    uint64_t* gran = d.granules;
+
+    // Same-XCD fast path.  Consumers always load granules sc1 (served by the
+    // L2, never by a stale L1).  A producer normally stores sc1 (write-
+    // through, which drops the line from its L2, so every consumer load goes
+    // out to the Infinity Cache).  When every workgroup of this chain runs on
+    // one XCD -- checked here at run time, never assumed -- the chain shares
+    // one L2 and a plain store (kept in that L2) is visible to the sc1 loads.
+    // Either way every granule is tag-checked.
+    bool local_l2 = false;
+    if (!(flags & 64)) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        uint64_t* xs = gran + xcc_slot_base(d.batch, H) + ((int64_t)b0 * 2 + dir) * G;
+        if (threadIdx.x == 0)
+            __hip_atomic_store(xs + member, (1ull << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t v = 0;
+        for (uint32_t spins = 0;; ++spins) {
+            v = lane < G ? __hip_atomic_load(xs + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : ((1ull << 32) | xcc);
+            if (__all((uint32_t)(v >> 32) == 1u)) break;
+            if (spins > (1u << 23)) {
+                if (lane == 0) atomicExch(d.status, 1);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        local_l2 = __all((uint32_t)v == xcc);
+    }
+    const int64_t gran_bytes = (int64_t)d.batch * 2 * 2 * H * 8;
+    const __amdgpu_buffer_rsrc_t grsrc =
+        __builtin_amdgcn_make_buffer_rsrc(gran, 0, (int)gran_bytes, 0x00020000);
+    auto goff = [&](int b, int par) -> int {   // byte offset of this lane's slice
+        return (int)(((((int64_t)b * 2 + dir) * 2 + par) * H + lane * KPL) * 8);
+    };
+
+    float hp[NB];                            // h_{t-1} of unit j
+    float gir[NB], giz[NB], gin[NB], rsd[NB];
+    auto prefetch = [&](int step) {
+        const int tm = dir == 0 ? step : T - 1 - step;
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) {
+            if (bb < nbh) {
+                const float* g = d.gi + (int64_t)(b0 + bb) * d.gi_bstride + (int64_t)(dir * 3 * H) * T + tm;
+                gir[bb] = g[(int64_t)(0 * H + j) * T];
+                giz[bb] = g[(int64_t)(1 * H + j) * T];
+                gin[bb] = g[(int64_t)(2 * H + j) * T];
+                rsd[bb] = d.res ? d.res[(int64_t)(b0 + bb) * d.res_bstride +
+                                        (int64_t)(dir * H + j) * d.res_cstride + tm]
+                                : 0.f;
+            }
+        }
+    };
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) hp[bb] = 0.f;
+    prefetch(0);
+    OU_STAMP_INIT
+
+    for (int t = 0; t < T; ++t) {
+        const int time = dir == 0 ? t : T - 1 - t;
+        float h[NB][KPL];
+        if (t == 0) {
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+                for (int k = 0; k < KPL; ++k) h[bb][k] = 0.f;
+        } else {
+            const uint32_t want = (uint32_t)t;   // tag of h_{t-1}
+            const int par = (t - 1) & 1;
+            for (uint32_t spins = 0;; ++spins) {
+                bool ok = true;
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) {
+                    const int b = b0 + min(bb, nbh - 1);
+                    if constexpr (KPL % 2 == 0) {
+#pragma unroll
+                        for (int q = 0; q < KPL / 2; ++q) {
+                            // aux 16 = sc1: served by L2, never by this CU's L1
+                            const auto v = __builtin_amdgcn_raw_buffer_load_b128(grsrc, goff(b, par) + 16 * q, 0, 16);
+                            h[bb][2 * q] = __uint_as_float(v[0]);
+                            h[bb][2 * q + 1] = __uint_as_float(v[2]);
+                            ok &= bb >= nbh || (v[1] == want && v[3] == want);
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < KPL; ++k) {
+                            const uint64_t v = __hip_atomic_load(
+                                gran + ((((int64_t)b * 2 + dir) * 2 + par) * H + lane * KPL + k),
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            h[bb][k] = __uint_as_float((uint32_t)v);
+                            ok &= bb >= nbh || (uint32_t)(v >> 32) == want;
+                        }
+                    }
+                }
+                if (__all(ok)) break;
+                if (sleep_poll) __builtin_amdgcn_s_sleep(1);
+                if (spins > (1u << 23)) {        // ~seconds: the chain is dead
+                    if (lane == 0) atomicExch(d.status, 1);
+                    return;
+                }
+                asm volatile("" ::: "memory");   // re-load every pass
+            }
+        }
+        OU_STAMP(0);
+
+        float cr[NB], cz[NB], cn[NB], cres[NB];
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) {
+            cr[bb] = gir[bb]; cz[bb] = giz[bb]; cn[bb] = gin[bb]; cres[bb] = rsd[bb];
+        }
+        if (t + 1 < T) prefetch(t + 1);
+
+        // partial dot products, value index (u * NB + b) * 3 + g
+        float acc[NV];
+#pragma unroll
+        for (int u = 0; u < UW; ++u)
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb)
+#pragma unroll
+                for (int g = 0; g < 3; ++g) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int k = 0; k < KPL; ++k) a = fmaf(w[u][g][k], h[bb][k], a);
+                    acc[(u * NB + bb) * 3 + g] = a;
+                }
+        OU_STAMP(1);
+
+        // reduce-scatter over the 64 lanes: the top unit bit <-> lane bit 5,
+        // the next <-> lane bit 4 (and for UW = 8 the last <-> lane bit 3);
+        // then sum over the 2^USH lanes left
+#pragma unroll
+        for (int i = 0; i < NV / 2; ++i) {
+            swap32(acc[i], acc[i + NV / 2]);
+            acc[i] += acc[i + NV / 2];
+        }
+#pragma unroll
+        for (int i = 0; i < NV / 4; ++i) {
+            swap16(acc[i], acc[i + NV / 4]);
+            acc[i] += acc[i + NV / 4];
+        }
+        if constexpr (UW == 8) {
+            const bool hi8 = lane & 8;
+#pragma unroll
+            for (int i = 0; i < NG; ++i) {
+                const float send = hi8 ? acc[i] : acc[i + NG];
+                const float keep = hi8 ? acc[i + NG] : acc[i];
+                acc[i] = keep + OU_DPP(send, 0x128);   // row_ror:8 == lane ^ 8
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NG; ++i) acc[i] += OU_DPP(acc[i], 0x128);
+        }
+#pragma unroll
+        for (int i = 0; i < NG; ++i) acc[i] = sum8(acc[i]);
+        OU_STAMP(2);
+
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb) {
+            if (bb >= nbh) break;
+            const float r = fast_sigmoid(cr[bb] + (acc[bb * 3 + 0] + bhr));
+            const float z = fast_sigmoid(cz[bb] + (acc[bb * 3 + 1] + bhz));
+            const float n = fast_tanh(cn[bb] + r * (acc[bb * 3 + 2] + bhn));
+            const float hn = (1.0f - z) * n + z * hp[bb];
+            hp[bb] = hn;
+            if (writer) {
+                const int b = b0 + bb;
+                if (t + 1 < T) {
+                    const uint64_t gv = ((uint64_t)(uint32_t)(t + 1) << 32) | __float_as_uint(hn);
+                    uint64_t* gp = gran + ((((int64_t)b * 2 + dir) * 2 + (t & 1)) * H + j);
+                    if (local_l2)   // plain 8-byte store: stays in the shared L2
+                        __hip_atomic_store(gp, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    else            // sc1 write-through
+                        __hip_atomic_store(gp, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                const float out = d.res ? (hn + cres[bb]) * d.res_scale : hn;
+                d.y[(int64_t)b * d.y_bstride + (int64_t)(dir * H + j) * d.y_cstride + time] = out;
+            }
+        }
+        OU_STAMP(3);
+    }
+#ifdef OU_GRU_STAMPS
+    if (lane == 0 && wave == 0) {
+        uint64_t* o = gran + xcc_slot_base(d.batch, H) + xcc_slot_count(d.batch, H) + (int64_t)bid * kStampSlots;
+        for (int i = 0; i < 4; ++i) o[i] = st_[i];
+        o[4] = local_l2;
+        o[5] = T;
+    }
+#endif
+}
+
+template <int H, int NB, int UW>
+void launch_ks(const ou_gru_desc& d, int nb, int nchains, int flags, int bofs, hipStream_t s)
+{
+    constexpr int G = H / (UW * kKsWaves);
+    const int grid = (flags & 1) ? 8 * G * ((nchains + 7) / 8) : nchains * G;
+    hipLaunchKernelGGL((gru_ks_kernel<H, NB, UW>), dim3(grid), dim3(64 * kKsWaves), 0, s, d, nb, nchains, flags,
+                       bofs);
+}
+
+// items per launch of the k-split kernel: every workgroup of every chain must
+// be resident at once (one 256-thread workgroup per CU is always possible)
+constexpr int kKsMaxWGs = 256;
+
+template <int H, int UW>
+int launch_ks_uw(const ou_gru_desc& d, int flags, hipStream_t s)
+{
+    constexpr int G = H / (UW * kKsWaves);
+    constexpr int kMaxNb = H >= 512 ? 2 : 4;   // 4 items at H = 512 would spill
+    // one item per chain while the chip has room, else 2 or 4
+    int nb = 1;
+    while (nb < kMaxNb && 2 * ((d.batch + nb - 1) / nb) * G > kKsMaxWGs) nb *= 2;
+    const int per_launch = (kKsMaxWGs / (2 * G)) * nb;
+    for (int b = 0; b < d.batch; b += per_launch) {
+        const int items = min(per_launch, d.batch - b);
+        const int nchains = 2 * ((items + nb - 1) / nb);
+        if (nb == 1) launch_ks<H, 1, UW>(d, nb, nchains, flags, b, s);
+        else if (nb == 2 || kMaxNb == 2) launch_ks<H, 2, UW>(d, nb, nchains, flags, b, s);
+        else launch_ks<H, kMaxNb, UW>(d, nb, nchains, flags, b, s);
+    }
+    return 0;
+}
+
+template <int H>
+int launch_ks_all(const ou_gru_desc& d, int flags, hipStream_t s)
+{
+    // 4 units per wave (half the per-wave dot product, twice the CUs) while
+    // one item per chain fits; 8 units per wave otherwise (or flags bit7)
+    constexpr int G4 = H / (4 * kKsWaves);
+    if (!(flags & 128) && 2 * d.batch * G4 <= kKsMaxWGs) return launch_ks_uw<H, 4>(d, flags, s);
+    return launch_ks_uw<H, 8>(d, flags, s);
 }
 
 template <int H, int NB, int U>
@@ -240,7 +593,9 @@ void launch_u(const ou_gru_desc& d, int nb, int nchains, int flags, hipStream_t 
 template <int H, int NB>
 void launch_nb(const ou_gru_desc& d, int nb, int nchains, int flags, hipStream_t s)
 {
-    if ((flags & 4) && H >= 64 && H % 64 == 0)
+    if ((flags & 8) && H >= 128 && H % 128 == 0)
+        launch_u<H, NB, (H >= 128 ? 128 : 32)>(d, nb, nchains, flags, s);
+    else if ((flags & 4) && H >= 64 && H % 64 == 0)
         launch_u<H, NB, (H >= 64 ? 64 : 32)>(d, nb, nchains, flags, s);
     else
         launch_u<H, NB, 32>(d, nb, nchains, flags, s);
@@ -258,7 +613,8 @@ void launch_h(const ou_gru_desc& d, int nb, int nchains, int flags, hipStream_t 
 
 extern "C" int64_t ou_gru_workspace_bytes(int hidden, int batch)
 {
-    return (int64_t)batch * 2 * 2 * hidden * sizeof(uint64_t);
+    return (xcc_slot_base(batch, hidden) + xcc_slot_count(batch, hidden) + (int64_t)kStampSlots * 1024) *
+           (int64_t)sizeof(uint64_t);
 }
 
 extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
@@ -271,6 +627,20 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
     hipStream_t s = (hipStream_t)stream;
     OU_HIP_CHECK(hipMemsetAsync(d.granules, 0, ou_gru_workspace_bytes(d.hidden, d.batch), s),
                  "gru: memset");
+    // k-split kernel (default for H % 64 == 0; flags bit5 selects the
+    // workgroup-gather kernel below)
+    if (d.hidden % 64 == 0 && !(d.flags >= 0 && (d.flags & 32))) {
+        const int kflags = d.flags >= 0 ? d.flags : 1;
+        switch (d.hidden) {
+        case 64: launch_ks_all<64>(d, kflags, s); break;
+        case 128: launch_ks_all<128>(d, kflags, s); break;
+        case 256: launch_ks_all<256>(d, kflags, s); break;
+        case 384: launch_ks_all<384>(d, kflags, s); break;
+        case 512: launch_ks_all<512>(d, kflags, s); break;
+        default: return ou_fail(-1, "gru: unsupported hidden size %d", d.hidden);
+        }
+        return ou_check_launch("gru");
+    }
     const int nb = d.batch >= kMaxBatchPerWG ? kMaxBatchPerWG : (d.batch >= 2 ? 2 : 1);
     const int nchains = 2 * ((d.batch + nb - 1) / nb);
     // default: XCD-local chains; 64-unit workgroups (fewer producers per

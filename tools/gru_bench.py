@@ -27,7 +27,7 @@ def main():
         gi, y = E.new_act(B, 1536, T, dev), E.new_act(B, 512, T, dev)
         gran = torch.zeros(L.load().ou_gru_workspace_bytes(256, B) // 8, dtype=torch.int64, device=dev)
         ref = None
-        for flags in (0, 1, 2, 3, 4, 5, 7):
+        for flags in [int(f) for f in os.environ.get("GRU_FLAGS", "5,7,9,11,21,25").split(",")]:
             E.GRU_FLAGS = flags
             prog = L.Program()
             E.rec_gru(prog, eng.s_gru, 0, x, gi, y, gran, eng.status)
@@ -41,8 +41,18 @@ def main():
             if ref is None:
                 ref = out
             ok = torch.equal(out, ref) and int(eng.status.max()) == 0
+            eng.status.zero_()
             print(f"B={B} flags={flags}: {1000 * min(ms) / T:.3f} us/step "
                   f"(median {1000 * sorted(ms)[2] / T:.3f}) identical={ok}", flush=True)
+            if os.environ.get("OUHIP_LIB", "").endswith("_diag.so"):
+                # phase stamps (OU_GRU_STAMPS build): cycles per step per workgroup
+                st = gran[B * 4 * 256 + B * 256 // 4:].view(-1, 8).cpu()
+                rows = [r for r in st.tolist() if r[5] > 0]
+                names = (("poll", "lds+bar1", "dot", "gate+store", "bar2") if flags & 32 else
+                         ("poll", "fma", "reduce", "gate+store", "local_l2x"))
+                for w, r in enumerate(rows[:4]):
+                    print("   wg%d " % w + " ".join(f"{n}={r[i] / r[5]:.0f}" for i, n in enumerate(names[:4])) + f" {names[4]}={r[4]}",
+                          f"total={sum(r[:5]) / r[5]:.0f} cyc/step", flush=True)
 
 
 if __name__ == "__main__":
