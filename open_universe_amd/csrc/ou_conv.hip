@@ -50,36 +50,69 @@ namespace {
 
 constexpr int kCinAlign = 64;   // packed weights pad the channel axis to this
 
-template <int KT, int CC, int WM, int WN, int WK, int NR>
+// Tile: 4 waves as WM x WN x WK; each wave owns MR x NR MFMA tiles of 32 x 32
+// (register blocking) over its share (1/WK) of every K chunk.
+template <int KT, int CC, int WM, int WN, int WK, int MR, int NR>
 struct Cfg {
-    static constexpr int BM = 32 * WM;
+    static constexpr int BM = 32 * WM * MR;
     static constexpr int BN = 32 * NR * WN;
-    static constexpr int W = BN + KT - 1;           // staged frames per chunk
-    static constexpr int WS = W | 1;                 // odd LDS row stride
+    static constexpr int W = BN + KT - 1;            // staged frames per chunk
     static constexpr int HALF = CC / 2;              // channel pairs per chunk
-    static constexpr int S = HALF * KT;              // k-steps per chunk
-    static constexpr int HPW = HALF / WK;            // channel pairs per wave
-    static constexpr int XN = CC * W;                // staged input floats
-    static constexpr int XE = (XN + 255) / 256;      // per thread
-    static constexpr int AN = WM * S * 64;           // staged weight floats
-    static constexpr int AE4 = (AN / 4 + 255) / 256; // float4 per thread
-    static constexpr int XBUF = (CC * WS + 3) / 4 * 4;
-    static constexpr int ABUF = AE4 * 1024;          // padded: every thread stores AE4 float4
-    static constexpr int STAGE = XBUF + ABUF;
-    static constexpr int RED = (WK - 1) * WM * WN * NR * 16 * 64;
-    static constexpr int LDS = (2 * STAGE > RED ? 2 * STAGE : RED);
-    static_assert(HALF % WK == 0, "channel pairs must split evenly over WK");
-    static_assert(WM * WN * WK == 4, "4 waves per workgroup");
+    static constexpr int HQ = HALF / 4;              // 4-pair groups per chunk
+    static constexpr int CPW = HQ / WK;              // 4-pair groups per wave
+    static constexpr int SX = CC + 4;                // X row stride (floats): SX/4 odd
+    static constexpr int XG = W * CC / 4;            // float4 groups of X per chunk
+    static constexpr int XE = (XG + 255) / 256;      // per thread
+    static constexpr int AG = WM * MR * HQ * KT * 64;  // float4 of A per chunk
+    static constexpr int AE = (AG + 255) / 256;
+    static constexpr int XBUF = W * SX;
+    static constexpr int STAGE = XBUF + AG * 4;
+    static constexpr int RED = (WK - 1) * WM * WN * MR * NR * 16 * 64;
+    static constexpr int LDS1 = STAGE > RED ? STAGE : RED;            // one chunk
+    static constexpr int LDS2 = 2 * STAGE > RED ? 2 * STAGE : RED;    // double-buffered
 };
 
 constexpr int kSentinel = 0x7ffffff0;   // byte offset past any buffer: loads return 0
 
-template <int KT, int CC, int WM, int WN, int WK, int NR>
+// Diagnostic build only (-DOU_CONV_STAMPS, tools/conv_bench.py --stamps):
+// thread 0 of each of the first kStampWGs workgroups sums s_memtime deltas
+// per phase: prologue, load issue, MFMA, staging stores, barrier, split-K
+// reduce + epilogue.
+#ifdef OU_CONV_STAMPS
+constexpr int kStampWGs = 4096;
+constexpr int kStampPhases = 8;
+__device__ uint64_t g_conv_stamps[kStampWGs * kStampPhases];
+#define OU_CSTAMP_INIT uint64_t cst_[kStampPhases] = {}; uint64_t ctp_ = __builtin_amdgcn_s_memtime(); \
+    cst_[6] = __builtin_amdgcn_s_memrealtime();
+#define OU_CSTAMP(i) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); cst_[i] += n_ - ctp_; ctp_ = n_; } while (0)
+#define OU_CSTAMP_SAVE                                                                         \
+    do {                                                                                       \
+        const int wg_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);        \
+        cst_[7] = __builtin_amdgcn_s_memrealtime();                                            \
+        if (threadIdx.x == 0 && wg_ < kStampWGs)                                               \
+            for (int i_ = 0; i_ < kStampPhases; ++i_) g_conv_stamps[wg_ * kStampPhases + i_] = cst_[i_]; \
+    } while (0)
+#else
+#define OU_CSTAMP_INIT
+#define OU_CSTAMP(i) do { } while (0)
+#define OU_CSTAMP_SAVE do { } while (0)
+#endif
+
+// LDS images of one K chunk (CC frame-view channels x KT taps):
+//   X  [frame w][h * HALF + p]  = PReLU(x'[2 p + h][t0 + w])     row stride SX
+//   A  [m-tile][p / 4][tap][lane][p % 4]  (the packed global order, copied)
+// so one ds_read_b128 gives a lane the operands of 4 consecutive k-steps
+// (channel pairs p .. p+3 at one tap) for both A and B, conflict-free.
+template <int KT, int CC, int WM, int WN, int WK, int MR, int NR>
 __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, int mtiles,
                                                    int64_t a_mt_stride)
 {
-    using C = Cfg<KT, CC, WM, WN, WK, NR>;
-    extern __shared__ __attribute__((aligned(16))) float lds[];
+    using C = Cfg<KT, CC, WM, WN, WK, MR, NR>;
+    static_assert(CC % 8 == 0 && C::HQ % WK == 0, "chunk must split into 4-pair groups per wave");
+    static_assert(WM * WN * WK == 4, "4 waves per workgroup");
+    static_assert((C::SX / 4) % 2 == 1, "X row stride must be an odd number of 16-B slots");
+    extern __shared__ float4 lds4[];
+    float* lds = (float*)lds4;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -89,8 +122,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const int wk = wave / (WN * WM);
     const int b = blockIdx.z;
     const int n0 = blockIdx.x * C::BN;
-    const int mt0 = blockIdx.y * WM;           // first m-tile of the workgroup
-    const int mt = mt0 + wm;
+    const int mt0 = blockIdx.y * (WM * MR);       // first m-tile of the workgroup
     const int h = lane >> 5;
     const int l32 = lane & 31;
     const int R = d.frame;
@@ -102,45 +134,43 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const float slope = d.slope;
     const int t0 = n0 - d.pad;
 
-    // ---- per-element staging geometry, fixed for the whole K loop -------
-    // R == 1: element (c, w) reads x[q*CC + c][t0 + w + shift]; the chunk
-    // advances the buffer base by CC channels and shrinks its size, so the
-    // channel bound is the buffer's range check.  R > 1 (frame view): element
-    // (w, c) reads channel c' = q*CC + c -> (c'/R, c'%R), recomputed per chunk.
-    int xoff[C::XE];
-    int loff[C::XE];
+    // ---- staging geometry, fixed for the whole K loop ----------------------
+    // X group g -> frame w = g % W, lane half hh, 4-pair group cq; its four
+    // elements are chunk channels 8 cq + 2 j + hh (j = 0..3) at frame w.
+    int xdst[C::XE];
+    int xsrc[C::XE];   // R == 1: byte offset of element j = 0 (or kSentinel); R > 1: sample of phase 0
+    int xcl[C::XE];    // chunk channel of element j = 0
 #pragma unroll
     for (int e = 0; e < C::XE; ++e) {
-        const int idx = tid + e * 256;
-        int c, w;
-        if (R == 1) {
-            c = idx / C::W;
-            w = idx - c * C::W;
-        } else {
-            w = idx / CC;
-            c = idx - w * CC;
-        }
-        loff[e] = idx < C::XN ? c * C::WS + w : -1;
+        const int g = tid + e * 256;
+        const int w = g % C::W;
+        const int r = g / C::W;
+        const int hh = r & 1, cq = r >> 1;
+        const bool valid = g < C::XG;
+        xdst[e] = valid ? w * C::SX + hh * C::HALF + 4 * cq : -1;
+        xcl[e] = 8 * cq + hh;
         if (R == 1) {
             const int pos = t0 + w + d.shift;
-            xoff[e] = (idx < C::XN && pos >= 0 && pos < in_len) ? (c * xc + pos) * 4 : kSentinel;
+            xsrc[e] = (valid && pos >= 0 && pos < in_len) ? (xcl[e] * xc + pos) * 4 : kSentinel;
         } else {
-            xoff[e] = (t0 + w) * R + d.shift;   // sample index of phase 0 of frame w
+            xsrc[e] = (t0 + w) * R + d.shift;
         }
     }
-    const float* wbase = d.w;
-    int aoff[C::AE4];
+    // packed weights: (mtiles * a_mt_stride) floats; one buffer resource
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)d.w, (short)0, (int)min<int64_t>((int64_t)mtiles * a_mt_stride * 4, 0x7fffffff), 0x00020000);
+    int aoff[C::AE];
 #pragma unroll
-    for (int e = 0; e < C::AE4; ++e) {
-        const int f = min(tid + e * 256, C::AN / 4 - 1);
-        const int ml = f / (C::S * 16);
-        const int r = f - ml * (C::S * 16);
+    for (int e = 0; e < C::AE; ++e) {
+        const int f = min(tid + e * 256, C::AG - 1);
+        const int ml = f / (C::HQ * KT * 64);
+        const int r = f - ml * (C::HQ * KT * 64);
         const int mtg = min(mt0 + ml, mtiles - 1);   // rows past M are computed, never stored
-        aoff[e] = (int)(mtg * a_mt_stride) + r * 4;   // float index of the float4
+        aoff[e] = (int)(mtg * a_mt_stride) + r * 4;
     }
 
-    float xr[C::XE];
-    float ar[4 * C::AE4];
+    float xr[4 * C::XE];   // plain float arrays: float4 arrays end up in scratch
+    float ar[4 * C::AE];
 
 #define OU_LOAD_CHUNK(q)                                                                       \
     {                                                                                          \
@@ -150,79 +180,109 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(               \
                 (void*)(xb + (int64_t)q_ * CC * xc), (short)0, nch > 0 ? nch * xc * 4 : 0,     \
                 0x00020000);                                                                   \
-            _Pragma("unroll") for (int e = 0; e < C::XE; ++e) xr[e] =                          \
-                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, xoff[e], 0, 0));      \
+            _Pragma("unroll") for (int e = 0; e < C::XE; ++e) {                                \
+                const unsigned o = (unsigned)xsrc[e];                                          \
+                const unsigned st = 8u * (unsigned)xc;                                         \
+                _Pragma("unroll") for (int j = 0; j < 4; ++j) xr[4 * e + j] =                  \
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + j * st, 0, 0));   \
+            }                                                                                  \
         } else {                                                                               \
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(               \
                 (void*)xb, (short)0, cin * xc * 4, 0x00020000);                               \
             _Pragma("unroll") for (int e = 0; e < C::XE; ++e) {                                \
-                const int idx = tid + e * 256;                                                 \
-                const int cq = q_ * CC + (idx - (idx / CC) * CC);                              \
-                const int ci = cq / R;                                                         \
-                const int pos = xoff[e] + (cq - ci * R);                                       \
-                const int off = (idx < C::XN && ci < cin && pos >= 0 && pos < in_len)          \
-                                    ? (ci * xc + pos) * 4                                      \
-                                    : kSentinel;                                               \
-                xr[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));  \
+                _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                \
+                    const int cq = q_ * CC + xcl[e] + 2 * j;                                   \
+                    const int ci = cq / R;                                                     \
+                    const int pos = xsrc[e] + (cq - ci * R);                                   \
+                    const int off = (xdst[e] >= 0 && ci < cin && pos >= 0 && pos < in_len)     \
+                                        ? (ci * xc + pos) * 4                                  \
+                                        : kSentinel;                                           \
+                    xr[4 * e + j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0)); \
+                }                                                                              \
             }                                                                                  \
         }                                                                                      \
-        _Pragma("unroll") for (int e = 0; e < C::AE4; ++e) {                                   \
-            const float4 v4 = *(const float4*)(wbase + aoff[e] + (int64_t)q_ * C::S * 64);     \
-            ar[4 * e] = v4.x;                                                                  \
-            ar[4 * e + 1] = v4.y;                                                              \
-            ar[4 * e + 2] = v4.z;                                                              \
-            ar[4 * e + 3] = v4.w;                                                              \
+        _Pragma("unroll") for (int e = 0; e < C::AE; ++e) {                                    \
+            /* voffset fixed per lane, chunk offset in the scalar soffset: no */                \
+            /* per-chunk VGPR address math (which made the compiler drain vmcnt) */            \
+            const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(                             \
+                wrs, aoff[e] * 4, q_ * (C::HQ * KT * 256 * 4), 0);                            \
+            ar[4 * e] = __uint_as_float(v4[0]);                                                \
+            ar[4 * e + 1] = __uint_as_float(v4[1]);                                            \
+            ar[4 * e + 2] = __uint_as_float(v4[2]);                                            \
+            ar[4 * e + 3] = __uint_as_float(v4[3]);                                            \
         }                                                                                      \
     }
+
+#define OU_PRELU(v) ((v) * scale >= 0.f ? (v) * scale : (v) * scale * slope)
 
 #define OU_STORE_CHUNK(buf)                                                                    \
     {                                                                                          \
         float* xs_ = lds + (buf) * C::STAGE;                                                   \
-        _Pragma("unroll") for (int e = 0; e < C::XE; ++e) {                                    \
-            float v = xr[e] * scale;                                                           \
-            v = v >= 0.f ? v : v * slope;                                                      \
-            if (loff[e] >= 0) xs_[loff[e]] = v;                                                \
-        }                                                                                      \
+        _Pragma("unroll") for (int e = 0; e < C::XE; ++e) if (xdst[e] >= 0)                    \
+            *(float4*)(xs_ + xdst[e]) = make_float4(OU_PRELU(xr[4 * e]), OU_PRELU(xr[4 * e + 1]), \
+                                                    OU_PRELU(xr[4 * e + 2]), OU_PRELU(xr[4 * e + 3])); \
         float4* as_ = (float4*)(xs_ + C::XBUF);                                                \
-        _Pragma("unroll") for (int e = 0; e < C::AE4; ++e) as_[tid + e * 256] =                \
-            make_float4(ar[4 * e], ar[4 * e + 1], ar[4 * e + 2], ar[4 * e + 3]);               \
+        _Pragma("unroll") for (int e = 0; e < C::AE; ++e) if (C::AG % 256 == 0 || tid + e * 256 < C::AG) \
+            as_[tid + e * 256] = make_float4(ar[4 * e], ar[4 * e + 1], ar[4 * e + 2], ar[4 * e + 3]); \
     }
 
-    floatx16 acc[NR];
+    floatx16 acc[MR][NR];
 #pragma unroll
-    for (int i = 0; i < NR; ++i)
+    for (int i = 0; i < MR; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+        for (int j = 0; j < NR; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+    OU_CSTAMP_INIT
     OU_LOAD_CHUNK(0);
     OU_STORE_CHUNK(0);
     __syncthreads();
+    OU_CSTAMP(0);
     for (int q = 0; q < nchunks; ++q) {
         const int cur = q & 1;
         if (q + 1 < nchunks) OU_LOAD_CHUNK(q + 1);
+        OU_CSTAMP(1);
         {
             const float* xs = lds + cur * C::STAGE;
-            const float* as = xs + C::XBUF + wm * (C::S * 64) + lane;
-            const float* xrow = xs + h * C::WS + wn * (32 * NR) + l32;
+            const float4* ap = (const float4*)(xs + C::XBUF) +
+                               ((wm * MR) * C::HQ + wk * C::CPW) * KT * 64 + lane;
+            const float* xp = xs + (wn * 32 * NR + l32) * C::SX + h * C::HALF + 4 * wk * C::CPW;
+            // software-pipelined: the fragments of step s + 1 are read while
+            // the MFMAs of step s run (step = 4 channel pairs at one tap)
+            constexpr int NS = C::CPW * KT;
+            float4 fa[2][MR], fb[2][NR];
+            auto frag = [&](int st, float4* a, float4* bq) {
+                const int cpq = st / KT, k = st - (st / KT) * KT;
 #pragma unroll
-            for (int cpl = 0; cpl < C::HPW; ++cpl) {
-                const int cp = wk * C::HPW + cpl;
+                for (int mr = 0; mr < MR; ++mr) a[mr] = ap[((mr * C::HQ + cpq) * KT + k) * 64];
 #pragma unroll
-                for (int k = 0; k < KT; ++k) {
-                    const float a = as[(cp * KT + k) * 64];
-                    const float* xr_ = xrow + (2 * cp) * C::WS + k;
+                for (int nr = 0; nr < NR; ++nr)
+                    bq[nr] = *(const float4*)(xp + (nr * 32 + k) * C::SX + 4 * cpq);
+            };
+            frag(0, fa[0], fb[0]);
 #pragma unroll
-                    for (int nr = 0; nr < NR; ++nr)
-                        acc[nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xr_[nr * 32], acc[nr],
-                                                                       0, 0, 0);
-                }
+            for (int st = 0; st < NS; ++st) {
+                if (st + 1 < NS) frag(st + 1, fa[(st + 1) & 1], fb[(st + 1) & 1]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                        for (int nr = 0; nr < NR; ++nr)
+                            acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                                fa[st & 1][mr][j], fb[st & 1][nr][j], acc[mr][nr], 0, 0, 0);
             }
         }
+        OU_CSTAMP(2);
         if (q + 1 < nchunks) OU_STORE_CHUNK(cur ^ 1);
+        OU_CSTAMP(3);
         __syncthreads();
+        OU_CSTAMP(4);
     }
 #undef OU_LOAD_CHUNK
 #undef OU_STORE_CHUNK
+#undef OU_PRELU
 
     // ---- intra-workgroup split-K reduction (fixed order: deterministic) ----
     if (WK > 1) {
@@ -230,113 +290,173 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
         const int sub = wm * WN + wn;
         if (wk > 0) {
 #pragma unroll
-            for (int nr = 0; nr < NR; ++nr)
+            for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    red[((((wk - 1) * WM * WN + sub) * NR + nr) * 16 + r) * 64 + lane] = acc[nr][r];
+                for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        red[(((((wk - 1) * WM * WN + sub) * MR + mr) * NR + nr) * 16 + r) * 64 + lane] =
+                            acc[mr][nr][r];
         }
         __syncthreads();
         if (wk > 0) return;
 #pragma unroll
         for (int j = 1; j < WK; ++j)
 #pragma unroll
-            for (int nr = 0; nr < NR; ++nr)
+            for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    acc[nr][r] += red[((((j - 1) * WM * WN + sub) * NR + nr) * 16 + r) * 64 + lane];
+                for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        acc[mr][nr][r] +=
+                            red[(((((j - 1) * WM * WN + sub) * MR + mr) * NR + nr) * 16 + r) * 64 + lane];
     }
-    if (mt >= mtiles) return;
 
     // ---- epilogue ----
+    // Branch-free: every out-of-range element gets a sentinel offset, so its
+    // buffer load returns 0 and its buffer store is dropped.  All residual
+    // loads of the tile are issued before any arithmetic, so their latency is
+    // paid once, not once per row.
     const int M = d.m;
     const int rout = d.rout;
     const int cout = M / rout;
-    float* __restrict__ y = d.y + (int64_t)b * d.y_bstride;
-    const float* r1 = d.res1 ? d.res1 + (int64_t)b * d.r1_bstride : nullptr;
-    const float* r2 = d.res2 ? d.res2 + (int64_t)b * d.r2_bstride : nullptr;
+    const int yrows = cout;
+    const int ylen = d.out_len;
+    const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
+        d.y + (int64_t)b * d.y_bstride, (short)0, (int)min<int64_t>((int64_t)yrows * d.y_cstride * 4, 0x7fffffff),
+        0x00020000);
+    const __amdgpu_buffer_rsrc_t r1s = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(d.res1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y), (short)0,
+        d.res1 ? (int)min<int64_t>((int64_t)yrows * d.r1_cstride * 4, 0x7fffffff) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r2s = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(d.res2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y), (short)0,
+        d.res2 ? (int)min<int64_t>((int64_t)yrows * d.r2_cstride * 4, 0x7fffffff) : 0, 0x00020000);
     const float* fm = d.film ? d.film + (int64_t)b * d.film_bstride : nullptr;
+    const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr;
 #pragma unroll
-    for (int nr = 0; nr < NR; ++nr) {
-        const int u = n0 + wn * (32 * NR) + nr * 32 + l32;
-        if (u >= d.n_frames) continue;
+    for (int mr = 0; mr < MR; ++mr) {
+        const int mt = mt0 + wm * MR + mr;
+        int co[16], ph[16];
+        float bias[16], fa[16], fb[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int m = mt * 32 + row;
-            if (m >= M) continue;
-            int co = m, ph = 0;
-            if (rout > 1) {
-                ph = m / cout;
-                co = m - ph * cout;
+            const int m = min(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
+            ph[r] = rout > 1 ? m / cout : 0;
+            co[r] = m - ph[r] * cout;
+            bias[r] = d.bias ? d.bias[co[r]] : 0.f;
+            fa[r] = fm ? fm[co[r]] : 1.f;
+            fb[r] = fm ? fm[cout + co[r]] : 0.f;
+        }
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+            const int u = n0 + wn * (32 * NR) + nr * 32 + l32;
+            int off[16];
+            float v1[16], v2[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int t = u * rout + ph[r];
+                const bool ok = m < M && u < d.n_frames && t < ylen;
+                off[r] = ok ? t : -1;   // column; row offsets differ per tensor
+                v1[r] = has_r1 ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                     r1s, ok ? (co[r] * (int)d.r1_cstride + t) * 4 : kSentinel, 0, 0))
+                               : 0.f;
+                v2[r] = has_r2 ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                     r2s, ok ? (co[r] * (int)d.r2_cstride + t) * 4 : kSentinel, 0, 0))
+                               : 0.f;
             }
-            const int t = u * rout + ph;
-            if (t >= d.out_len) continue;
-            float v = acc[nr][r];
-            if (d.bias) v += d.bias[co];
-            if (t >= d.valid_len) v = 0.f;
-            if (r1) v = (v + r1[(int64_t)co * d.r1_cstride + t]) * d.s1;
-            if (fm) v = fm[co] * v + fm[cout + co];
-            if (r2) v = (v + r2[(int64_t)co * d.r2_cstride + t]) * d.s2;
-            y[(int64_t)co * d.y_cstride + t] = v;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float v = acc[mr][nr][r] + bias[r];
+                if (off[r] >= d.valid_len) v = 0.f;
+                if (has_r1) v = (v + v1[r]) * d.s1;
+                v = fa[r] * v + fb[r];
+                if (has_r2) v = (v + v2[r]) * d.s2;
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    __float_as_uint(v), ys, off[r] >= 0 ? (co[r] * (int)d.y_cstride + off[r]) * 4 : kSentinel, 0, 0);
+            }
         }
     }
+    OU_CSTAMP(5);
+    OU_CSTAMP_SAVE;
 }
 
 // ---- tile table ------------------------------------------------------------
 struct Tile {
-    int wm, wn, wk, nr;
+    int wm, wn, wk, mr, nr;
 };
-// id: 0 32x512, 1 32x256, 2 64x128, 3 64x64, 4 32x32/K4, 5 64x32/K2, 6 32x64/K2, 7 128x32
-constexpr Tile kTiles[] = {{1, 4, 1, 4}, {1, 4, 1, 2}, {2, 2, 1, 2}, {2, 2, 1, 1},
-                           {1, 1, 4, 1}, {2, 1, 2, 1}, {1, 2, 2, 1}, {4, 1, 1, 1}};
+// BM x BN (split-K): 0 32x256, 1 32x128, 2 32x128/K2, 3 64x128, 4 64x128 (MR2),
+// 5 128x128, 6 128x64, 7 256x32, 8 128x32/K2, 9 64x32/K4, 10 64x64/K2, 11 64x64, 12 32x64/K4
+#define OU_TILES(X)                                                                            \
+    X(0, 1, 4, 1, 1, 2) X(1, 1, 4, 1, 1, 1) X(2, 1, 2, 2, 1, 2) X(3, 2, 2, 1, 1, 2)            \
+    X(4, 1, 4, 1, 2, 1) X(5, 2, 2, 1, 2, 2) X(6, 2, 2, 1, 2, 1) X(7, 4, 1, 1, 2, 1)            \
+    X(8, 2, 1, 2, 2, 1) X(9, 1, 1, 4, 2, 1) X(10, 1, 2, 2, 2, 1) X(11, 2, 2, 1, 1, 1)          \
+    X(12, 1, 1, 4, 1, 2)
+#define OU_TILE_ENTRY(id, wm, wn, wk, mr, nr) {wm, wn, wk, mr, nr},
+constexpr Tile kTiles[] = {OU_TILES(OU_TILE_ENTRY)};
+#undef OU_TILE_ENTRY
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
-constexpr int kMaxLds = 64 * 1024;
+constexpr int kMaxLds = 160 * 1024;     // gfx950: 160 KiB per CU
+constexpr int kLdsTwoPerCu = 80 * 1024; // fits two workgroups per CU
 
-// channel chunk: the largest of 64/32/16 whose double-buffered stage fits LDS
-template <int KT, int WM, int WN, int WK, int NR>
+// channel chunk: the largest of 64/32/16/8 that splits over the K waves and
+// whose double-buffered stage fits two workgroups per CU, else one per CU
+template <int KT, int WM, int WN, int WK, int MR, int NR, int CC>
+constexpr bool chunk_ok(int budget)
+{
+    return CC / 8 % WK == 0 && Cfg<KT, CC, WM, WN, WK, MR, NR>::LDS2 * 4 <= budget;
+}
+template <int KT, int WM, int WN, int WK, int MR, int NR>
 constexpr int chunk_for()
 {
-    return Cfg<KT, 64, WM, WN, WK, NR>::LDS * 4 <= kMaxLds   ? 64
-           : Cfg<KT, 32, WM, WN, WK, NR>::LDS * 4 <= kMaxLds ? 32
-                                                              : 16;
+    return chunk_ok<KT, WM, WN, WK, MR, NR, 64>(kLdsTwoPerCu)   ? 64
+           : chunk_ok<KT, WM, WN, WK, MR, NR, 32>(kLdsTwoPerCu) ? 32
+           : chunk_ok<KT, WM, WN, WK, MR, NR, 16>(kLdsTwoPerCu) ? 16
+           : chunk_ok<KT, WM, WN, WK, MR, NR, 8>(kLdsTwoPerCu)  ? 8
+           : chunk_ok<KT, WM, WN, WK, MR, NR, 32>(kMaxLds)      ? 32
+           : chunk_ok<KT, WM, WN, WK, MR, NR, 16>(kMaxLds)      ? 16
+                                                                : 8 * WK;
 }
 
-template <int KT, int WM, int WN, int WK, int NR>
+template <int KT, int WM, int WN, int WK, int MR, int NR>
+constexpr int lds_bytes_t()
+{
+    constexpr int CC = chunk_for<KT, WM, WN, WK, MR, NR>();
+    return Cfg<KT, CC, WM, WN, WK, MR, NR>::LDS2 * 4;
+}
+
+template <int KT, int WM, int WN, int WK, int MR, int NR>
 int launch_t(const ou_conv_desc& d, hipStream_t s)
 {
-    constexpr int CC = chunk_for<KT, WM, WN, WK, NR>();
-    using C = Cfg<KT, CC, WM, WN, WK, NR>;
+    constexpr int CC = chunk_for<KT, WM, WN, WK, MR, NR>();
+    using C = Cfg<KT, CC, WM, WN, WK, MR, NR>;
     const int mtiles = (d.m + 31) / 32;
     const int cin_eff = d.cin * d.frame;
     const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
     const int nchunks = (cin_eff + CC - 1) / CC;
-    const int64_t a_mt_stride = (int64_t)(cin_pad / 2) * KT * 64;
-    dim3 grid((d.n_frames + C::BN - 1) / C::BN, (mtiles + WM - 1) / WM, d.batch);
-    const size_t lds = (size_t)C::LDS * sizeof(float);
-    hipLaunchKernelGGL((conv_kernel<KT, CC, WM, WN, WK, NR>), grid, dim3(256), lds, s, d, nchunks,
-                       mtiles, a_mt_stride);
+    const int64_t a_mt_stride = (int64_t)cin_pad * KT * 32;
+    dim3 grid((d.n_frames + C::BN - 1) / C::BN, (mtiles + WM * MR - 1) / (WM * MR), d.batch);
+    const int lds = (nchunks > 1 ? C::LDS2 : C::LDS1) * (int)sizeof(float);
+    auto kern = conv_kernel<KT, CC, WM, WN, WK, MR, NR>;
+    static bool attr = false;   // opt in to more than 64 KiB of dynamic LDS, once
+    if (!attr && C::LDS2 * 4 > 64 * 1024) {
+        OU_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         C::LDS2 * 4),
+                     "conv: LDS attribute");
+        attr = true;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, d, nchunks, mtiles, a_mt_stride);
     return ou_check_launch("conv");
-}
-
-template <int KT, int WM, int WN, int WK, int NR>
-constexpr int lds_bytes_t()
-{
-    return Cfg<KT, chunk_for<KT, WM, WN, WK, NR>(), WM, WN, WK, NR>::LDS * 4;
 }
 
 template <int KT>
 int lds_bytes_kt(int tile)
 {
     switch (tile) {
-    case 0: return lds_bytes_t<KT, 1, 4, 1, 4>();
-    case 1: return lds_bytes_t<KT, 1, 4, 1, 2>();
-    case 2: return lds_bytes_t<KT, 2, 2, 1, 2>();
-    case 3: return lds_bytes_t<KT, 2, 2, 1, 1>();
-    case 4: return lds_bytes_t<KT, 1, 1, 4, 1>();
-    case 5: return lds_bytes_t<KT, 2, 1, 2, 1>();
-    case 6: return lds_bytes_t<KT, 1, 2, 2, 1>();
-    case 7: return lds_bytes_t<KT, 4, 1, 1, 1>();
+#define OU_TILE_CASE(id, wm, wn, wk, mr, nr) case id: return lds_bytes_t<KT, wm, wn, wk, mr, nr>();
+        OU_TILES(OU_TILE_CASE)
+#undef OU_TILE_CASE
     }
     return -1;
 }
@@ -356,35 +476,33 @@ template <int KT>
 int launch_kt(const ou_conv_desc& d, int tile, hipStream_t s)
 {
     switch (tile) {
-    case 0: return launch_t<KT, 1, 4, 1, 4>(d, s);
-    case 1: return launch_t<KT, 1, 4, 1, 2>(d, s);
-    case 2: return launch_t<KT, 2, 2, 1, 2>(d, s);
-    case 3: return launch_t<KT, 2, 2, 1, 1>(d, s);
-    case 4: return launch_t<KT, 1, 1, 4, 1>(d, s);
-    case 5: return launch_t<KT, 2, 1, 2, 1>(d, s);
-    case 6: return launch_t<KT, 1, 2, 2, 1>(d, s);
-    case 7: return launch_t<KT, 4, 1, 1, 1>(d, s);
+#define OU_TILE_CASE(id, wm, wn, wk, mr, nr) case id: return launch_t<KT, wm, wn, wk, mr, nr>(d, s);
+        OU_TILES(OU_TILE_CASE)
+#undef OU_TILE_CASE
     }
     return ou_fail(-2, "conv: bad tile %d", tile);
 }
 
 // Static choice (used when the host has not autotuned the layer): the
-// largest tile that still gives >= 2 workgroups per CU, split-K when N is short.
+// largest tile that still gives >= 1 workgroup per CU, split-K when N is short.
 int pick_tile(const ou_conv_desc& d)
 {
     auto wgs = [&](int t) {
         const Tile& k = kTiles[t];
-        const int bm = 32 * k.wm, bn = 32 * k.nr * k.wn;
+        const int bm = 32 * k.wm * k.mr, bn = 32 * k.nr * k.wn;
         return (int64_t)((d.m + bm - 1) / bm) * ((d.n_frames + bn - 1) / bn) * d.batch;
     };
-    auto ok = [&](int t) { return lds_bytes(d.kt, t) <= kMaxLds; };
     if (d.m <= 32) {
-        for (int t : {0, 1}) if (ok(t) && wgs(t) >= 512) return t;
-        return 4;
+        for (int t : {0, 1}) if (wgs(t) >= 256) return t;
+        return 12;
     }
-    for (int t : {2, 3}) if (ok(t) && wgs(t) >= 512) return t;
-    if (wgs(6) >= 512) return 6;
-    return 4;
+    if (d.m <= 64) {
+        for (int t : {3, 11}) if (wgs(t) >= 256) return t;
+        return 9;
+    }
+    for (int t : {5, 6}) if (wgs(t) >= 256) return t;
+    if (wgs(10) >= 256) return 10;
+    return 9;
 }
 
 }  // namespace
@@ -403,8 +521,10 @@ extern "C" int64_t ou_conv_packed_size(int m, int cin_eff, int kt, int cc)
     return mtiles * (cin_pad / 2) * kt * 64;
 }
 
-// Packed order: [m-tile][channel pair cp][tap k][lane]; lane -> (row mt*32 +
-// (lane & 31), channel 2*cp + (lane >> 5)); zero outside [0, m) x [0, cin_eff).
+// Packed order: [m-tile][p / 4][tap k][lane][p % 4] over channel pairs p;
+// lane -> row mt*32 + (lane & 31), channel 2 p + (lane >> 5); zero outside
+// [0, m) x [0, cin_eff).  A K chunk of CC channels is then one contiguous run
+// per m-tile, and one float4 per lane holds 4 consecutive k-steps.
 extern "C" int ou_conv_pack(const float* w, int m, int cin_eff, int kt, int cc, float* out)
 {
     (void)cc;
@@ -414,14 +534,14 @@ extern "C" int ou_conv_pack(const float* w, int m, int cin_eff, int kt, int cc, 
     const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
     int64_t o = 0;
     for (int mt = 0; mt < mtiles; ++mt)
-        for (int cp = 0; cp < cin_pad / 2; ++cp)
+        for (int pq = 0; pq < cin_pad / 8; ++pq)
             for (int k = 0; k < kt; ++k)
-                for (int lane = 0; lane < 64; ++lane) {
-                    const int row = mt * 32 + (lane & 31);
-                    const int c = 2 * cp + (lane >> 5);
-                    out[o++] = (row < m && c < cin_eff) ? w[((int64_t)row * cin_eff + c) * kt + k]
-                                                        : 0.f;
-                }
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 4; ++j) {
+                        const int row = mt * 32 + (lane & 31);
+                        const int c = 2 * (4 * pq + j) + (lane >> 5);
+                        out[o++] = (row < m && c < cin_eff) ? w[((int64_t)row * cin_eff + c) * kt + k] : 0.f;
+                    }
     return 0;
 }
 
@@ -444,6 +564,13 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     }
     return ou_fail(-1, "conv: unsupported kt %d", d.kt);
 }
+
+#ifdef OU_CONV_STAMPS
+extern "C" int ou_conv_read_stamps(uint64_t* host, int n)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_conv_stamps), sizeof(uint64_t) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile(*d) : -1; }
 extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }

@@ -60,21 +60,22 @@ def test_struct_layouts_match_c():
 
 
 def test_conv_pack_layout():
-    """Packed order: [mtile][channel pair][tap][lane], lane -> (row = lane & 31,
-    channel = 2 * pair + (lane >> 5)); channels zero-padded to a multiple of 64."""
+    """Packed order: [mtile][pair // 4][tap][lane][pair % 4], lane -> (row =
+    lane & 31, channel = 2 * pair + (lane >> 5)); channels zero-padded to a
+    multiple of 64 (one float4 per lane = 4 consecutive k-steps)."""
     rng = np.random.default_rng(0)
     m, cin, kt = 40, 20, 3
     w = rng.standard_normal((m, cin, kt)).astype(np.float32)
     packed = L.conv_pack(w, L.conv_chunk(kt, 1))
     mtiles, pairs = 2, 32
-    ref = np.zeros((mtiles, pairs, kt, 64), np.float32)
+    ref = np.zeros((mtiles, pairs // 4, kt, 64, 4), np.float32)
     for mt in range(mtiles):
         for cp in range(pairs):
             for k in range(kt):
                 for lane in range(64):
                     row, c = mt * 32 + (lane & 31), 2 * cp + (lane >> 5)
                     if row < m and c < cin:
-                        ref[mt, cp, k, lane] = w[row, c, k]
+                        ref[mt, cp // 4, k, lane, cp % 4] = w[row, c, k]
     np.testing.assert_array_equal(packed, ref.reshape(-1))
 
 

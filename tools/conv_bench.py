@@ -1,0 +1,120 @@
+#!/usr/bin/env python
+"""Time ou_conv tiles on representative UNIVERSE++ 16 kHz layer shapes.
+
+    python tools/conv_bench.py                       # every layer, every valid tile
+    python tools/conv_bench.py --layer L2k3 --tile 11 --reps 50   # one config (for rocprofv3 --pmc)
+
+Random weights/inputs (timing does not depend on values).  Prints ms per
+launch and algorithmic TFLOP/s per (layer, tile).
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from open_universe_amd import _lib as L
+from open_universe_amd import engine as E
+
+# name: (m, cin, frame, kt, n_frames, rout, residual)
+LAYERS = {
+    "L0k3": (32, 32, 1, 3, 128000, 1, True),
+    "L0k5": (32, 32, 1, 5, 128000, 1, False),
+    "L1k3": (64, 64, 1, 3, 64000, 1, True),
+    "L1k5": (64, 64, 1, 5, 64000, 1, False),
+    "L2k3": (128, 128, 1, 3, 16000, 1, True),
+    "L2k5": (128, 128, 1, 5, 16000, 1, False),
+    "L3k3": (256, 256, 1, 3, 4000, 1, True),
+    "L3k5": (256, 256, 1, 5, 4000, 1, False),
+    "L4k3": (512, 512, 1, 3, 800, 1, True),
+    "L4k5": (512, 512, 1, 5, 800, 1, False),
+    "D3": (512, 256, 5, 3, 800, 1, False),     # down-sampling conv, rate 5 (polyphase)
+    "U3": (1280, 512, 1, 3, 800, 5, True),     # up-sampling conv, rate 5
+    "GI": (1536, 512, 1, 1, 800, 1, False),    # GRU input projection
+}
+
+
+def make(name, dev, seed=0):
+    m, cin, frame, kt, n, rout, res = LAYERS[name]
+    g = torch.Generator().manual_seed(seed)
+    w = (torch.randn(m, cin * frame, kt, generator=g) * 0.05).numpy()
+    spec = E.ConvSpec(w, cin, frame, (kt - 1) // 2, rout, 0.25, np.zeros(m // rout, np.float32),
+                      ref_macs=float(w.size))
+    cw = E.make_conv(spec, dev)
+    x = E.Act(torch.randn(1, cin, n * frame, device=dev))
+    y = E.new_act(1, m // rout, n * rout, dev)
+    r = E.Act(torch.randn(1, m // rout, n * rout, device=dev)) if res else None
+    d = E.conv_desc(cw, x, y, res1=r, s1=0.7, n_frames=n)
+    return d, (cw, x, y, r)
+
+
+def time_tile(d, tile, reps, stream):
+    import ctypes
+
+    lib = L.load()
+    d.tile = tile
+    if lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream)) != 0:
+        return None
+    for _ in range(2):
+        lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layer", default=None)
+    ap.add_argument("--tile", type=int, default=None)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--stamps", action="store_true", help="diag library: per-phase cycles")
+    a = ap.parse_args()
+    dev = "cuda:0"
+    stream = torch.cuda.current_stream().cuda_stream
+    lib = L.load()
+    names = [a.layer] if a.layer else list(LAYERS)
+    for name in names:
+        d, keep = make(name, dev)
+        tiles = [a.tile] if a.tile is not None else [t for t in range(lib.ou_conv_num_tiles())
+                                                      if lib.ou_conv_tile_ok(d.kt, t)]
+        res = []
+        for t in tiles:
+            ms = time_tile(d, t, a.reps, stream)
+            if ms is not None:
+                res.append((ms, t))
+        res.sort()
+        fl = d._flops
+        line = "  ".join(f"t{t}:{ms * 1e3:.1f}us/{fl / ms / 1e9:.0f}TF" for ms, t in res)
+        print(f"{name:5s} {fl / 1e9:6.2f} GFLOP  best t{res[0][1]} {res[0][0] * 1e3:.1f} us "
+              f"{fl / res[0][0] / 1e9:.1f} TF/s | {line}", flush=True)
+        if a.stamps:
+            import ctypes
+
+            n = 4096 * 8
+            buf = (ctypes.c_uint64 * n)()
+            lib.ou_conv_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            assert lib.ou_conv_read_stamps(ctypes.cast(buf, ctypes.c_void_p), n) == 0
+            st = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8).astype(np.float64)
+            st = st[st.sum(1) > 0]
+            names = ("prologue", "load_issue", "mfma", "store", "barrier", "epilogue")
+            mean = st.mean(0)
+            print(f"      stamps over {len(st)} WGs (cycles): " +
+                  " ".join(f"{nm}={mean[i]:.0f}" for i, nm in enumerate(names)) +
+                  f" total={mean[:6].sum():.0f} (min {st[:, :6].sum(1).min():.0f} max {st[:, :6].sum(1).max():.0f})",
+                  flush=True)
+            t0 = st[:, 6].min()
+            s0, s1 = (st[:, 6] - t0) / 100.0, (st[:, 7] - t0) / 100.0   # s_memrealtime: 100 MHz -> us
+            dur = s1 - s0
+            print(f"      realtime: starts 0..{s0.max():.2f} us, ends {s1.min():.2f}..{s1.max():.2f} us, "
+                  f"WG lifetime mean {dur.mean():.2f} max {dur.max():.2f} us; span {s1.max():.2f} us; "
+                  f"start quantiles {np.quantile(s0, [0.25, 0.5, 0.75, 0.95]).round(2).tolist()}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
