@@ -44,7 +44,9 @@ const char* ou_last_error(void);
  * (condition.py:33-65), the GRU input projection and the STFT-as-GEMM of the
  * mel front end (condition.py:85-108).
  *
- *   xv[c'][t] = prelu(in_scale[b] * x[b][c'/R][t*R + c'%R + shift])   (0 outside [0,in_len))
+ *   xv[c'][t] = prelu(in_scale[b] * x[b][c'%cin][t*R + c'/cin + shift])  (0 outside [0,in_len))
+ *   (phase-major frame view: channel c' = ph*cin + ci; W's channel axis, as
+ *   packed by ou_conv_pack, follows the same order)
  *   acc[m][u] = sum_{c',k} W[m][c'][k] * xv[c'][u + k - pad]          u in [0, n_frames)
  *   m = ph*cout + co, t = u*rout + ph  (pixel shuffle; rout = 1 for plain convs)
  *   v = acc + bias[co];  v = t < valid_len ? v : 0
@@ -82,7 +84,8 @@ typedef struct ou_conv_desc {
     const float* res2;         /* residual 2 or NULL                             */
     int64_t r2_bstride, r2_cstride;
     float s2;
-    int32_t tile;              /* tile config (ou_conv_pick_tile), -1 = auto     */
+    int32_t tile;              /* -1 = auto; bits 0-7 tile shape (< ou_conv_     */
+                               /* num_tiles()); bits 8-9 reserved (0)            */
     int32_t _reserved;
 } ou_conv_desc;
 
@@ -93,8 +96,9 @@ int ou_conv_chunk(int kt, int frame);
 int64_t ou_conv_packed_size(int m, int cin_eff, int kt, int cc);
 /* Host-side packing: w_logical[m][cin_eff][kt] (row-major, host memory)
  * -> packed[] in the per-lane MFMA fragment order the kernel streams:
- * [m-tile of 32][channel pair][tap][lane], lane l holding row l & 31 and
- * channel 2*pair + (l >> 5); channels padded with zeros to a multiple of 64. */
+ * [m-tile of 32][pair / 4][tap][lane][pair % 4], lane l holding row l & 31
+ * and channel 2*pair + (l >> 5); channels padded with zeros to a multiple of
+ * 64 (one float4 per lane = 4 consecutive k-steps of the MFMA stream). */
 int ou_conv_pack(const float* w_logical, int m, int cin_eff, int kt, int cc,
                  float* packed);
 int ou_conv(const ou_conv_desc* d, void* stream);
@@ -105,6 +109,9 @@ int ou_conv(const ou_conv_desc* d, void* stream);
 int ou_conv_pick_tile(const ou_conv_desc* d);
 int ou_conv_num_tiles(void);
 int ou_conv_tile_ok(int kt, int tile);
+/* Diagnostics: LDS bytes a tile shape requests at tap count kt, and the
+ * device's opt-in per-workgroup LDS limit. */
+int ou_conv_lds_info(int kt, int tile, int* lds_request, int* device_optin_max);
 
 /* ------------------------------------------------------------------------
  * Bidirectional GRU recurrence (kernel K6).  Replaces the recurrent part of

@@ -136,6 +136,7 @@ EXPORTS = {
     "ou_conv_pick_tile": (c_int, [POINTER(ConvDesc)]),
     "ou_conv_num_tiles": (c_int, []),
     "ou_conv_tile_ok": (c_int, [c_int, c_int]),
+    "ou_conv_lds_info": (c_int, [c_int, c_int, POINTER(c_int), POINTER(c_int)]),
     "ou_gru_workspace_bytes": (c_int64, [c_int, c_int]),
     "ou_gru": (c_int, [POINTER(GruDesc), c_void_p]),
     "ou_embed": (c_int, [POINTER(EmbedDesc), c_void_p]),

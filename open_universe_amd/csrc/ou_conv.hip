@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     static_assert(CC % 8 == 0 && C::HQ % WK == 0, "chunk must split into 4-pair groups per wave");
     static_assert(WM * WN * WK == 4, "4 waves per workgroup");
     static_assert((C::SX / 4) % 2 == 1, "X row stride must be an odd number of 16-B slots");
-    extern __shared__ float4 lds4[];
+    OU_DYNAMIC_LDS(float4, lds4);
     float* lds = (float*)lds4;
 
     const int tid = threadIdx.x;
@@ -157,8 +157,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
         }
     }
     // packed weights: (mtiles * a_mt_stride) floats; one buffer resource
-    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)d.w, (short)0, (int)min<int64_t>((int64_t)mtiles * a_mt_stride * 4, 0x7fffffff), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrs = ou_rsrc(d.w, (int64_t)mtiles * a_mt_stride * 4);
     int aoff[C::AE];
 #pragma unroll
     for (int e = 0; e < C::AE; ++e) {
@@ -177,24 +176,38 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
         const int q_ = (q);                                                                    \
         if (R == 1) {                                                                          \
             const int nch = cin - q_ * CC;                                                     \
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(               \
-                (void*)(xb + (int64_t)q_ * CC * xc), (short)0, nch > 0 ? nch * xc * 4 : 0,     \
-                0x00020000);                                                                   \
+            const __amdgpu_buffer_rsrc_t rs =                                                  \
+                ou_rsrc(xb + (int64_t)q_ * CC * xc, nch > 0 ? (int64_t)nch * xc * 4 : 0);      \
             _Pragma("unroll") for (int e = 0; e < C::XE; ++e) {                                \
                 const unsigned o = (unsigned)xsrc[e];                                          \
                 const unsigned st = 8u * (unsigned)xc;                                         \
                 _Pragma("unroll") for (int j = 0; j < 4; ++j) xr[4 * e + j] =                  \
                     __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + j * st, 0, 0));   \
             }                                                                                  \
+        } else if (cin % CC == 0) {                                                            \
+            /* phase-major frame view: the chunk is one phase ph of channels */                \
+            /* ci0 .. ci0+CC-1: x'[ci0 + cl][t] = x[ci0 + cl][t*R + ph + shift] */              \
+            const int ph = (q_ * CC) / cin;                                                    \
+            const int ci0 = q_ * CC - ph * cin;                                                \
+            const __amdgpu_buffer_rsrc_t rs =                                                  \
+                ou_rsrc(xb + (int64_t)ci0 * xc, (int64_t)(cin - ci0) * xc * 4);                \
+            _Pragma("unroll") for (int e = 0; e < C::XE; ++e) {                                \
+                const int pos = xsrc[e] + ph;                                                  \
+                const bool ok = xdst[e] >= 0 && pos >= 0 && pos < in_len;                      \
+                _Pragma("unroll") for (int j = 0; j < 4; ++j) xr[4 * e + j] =                  \
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(                      \
+                        rs, ok ? ((xcl[e] + 2 * j) * xc + pos) * 4 : kSentinel, 0, 0));        \
+            }                                                                                  \
         } else {                                                                               \
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(               \
-                (void*)xb, (short)0, cin * xc * 4, 0x00020000);                               \
+            const __amdgpu_buffer_rsrc_t rs =                                                  \
+                ou_rsrc(xb, (int64_t)cin * xc * 4);                                            \
             _Pragma("unroll") for (int e = 0; e < C::XE; ++e) {                                \
                 _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                \
                     const int cq = q_ * CC + xcl[e] + 2 * j;                                   \
-                    const int ci = cq / R;                                                     \
-                    const int pos = xsrc[e] + (cq - ci * R);                                   \
-                    const int off = (xdst[e] >= 0 && ci < cin && pos >= 0 && pos < in_len)     \
+                    const int ph = cq / cin;                                                   \
+                    const int ci = cq - ph * cin;                                              \
+                    const int pos = xsrc[e] + ph;                                              \
+                    const int off = (xdst[e] >= 0 && ph < R && pos >= 0 && pos < in_len)       \
                                         ? (ci * xc + pos) * 4                                  \
                                         : kSentinel;                                           \
                     xr[4 * e + j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0)); \
@@ -322,15 +335,9 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const int cout = M / rout;
     const int yrows = cout;
     const int ylen = d.out_len;
-    const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
-        d.y + (int64_t)b * d.y_bstride, (short)0, (int)min<int64_t>((int64_t)yrows * d.y_cstride * 4, 0x7fffffff),
-        0x00020000);
-    const __amdgpu_buffer_rsrc_t r1s = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(d.res1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y), (short)0,
-        d.res1 ? (int)min<int64_t>((int64_t)yrows * d.r1_cstride * 4, 0x7fffffff) : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t r2s = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(d.res2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y), (short)0,
-        d.res2 ? (int)min<int64_t>((int64_t)yrows * d.r2_cstride * 4, 0x7fffffff) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)yrows * d.y_cstride * 4);
+    const __amdgpu_buffer_rsrc_t r1s = ou_rsrc(d.res1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y, d.res1 ? (int64_t)yrows * d.r1_cstride * 4 : 0);
+    const __amdgpu_buffer_rsrc_t r2s = ou_rsrc(d.res2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y, d.res2 ? (int64_t)yrows * d.r2_cstride * 4 : 0);
     const float* fm = d.film ? d.film + (int64_t)b * d.film_bstride : nullptr;
     const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr;
 #pragma unroll
@@ -383,16 +390,19 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 
 // ---- tile table ------------------------------------------------------------
 struct Tile {
-    int wm, wn, wk, mr, nr;
+    int wm, wn, wk, mr, nr, big;
 };
 // BM x BN (split-K): 0 32x256, 1 32x128, 2 32x128/K2, 3 64x128, 4 64x128 (MR2),
-// 5 128x128, 6 128x64, 7 256x32, 8 128x32/K2, 9 64x32/K4, 10 64x64/K2, 11 64x64, 12 32x64/K4
+// 5 128x128, 6 128x64, 7 256x32, 8 128x32/K2, 9 64x32/K4, 10 64x64/K2, 11 64x64,
+// 12 32x64/K4; 13.. the same shapes with chunks sized for one workgroup per CU
+// (up to 160 KiB of LDS: twice the MFMA work per chunk, for grids <= 256 WGs)
 #define OU_TILES(X)                                                                            \
-    X(0, 1, 4, 1, 1, 2) X(1, 1, 4, 1, 1, 1) X(2, 1, 2, 2, 1, 2) X(3, 2, 2, 1, 1, 2)            \
-    X(4, 1, 4, 1, 2, 1) X(5, 2, 2, 1, 2, 2) X(6, 2, 2, 1, 2, 1) X(7, 4, 1, 1, 2, 1)            \
-    X(8, 2, 1, 2, 2, 1) X(9, 1, 1, 4, 2, 1) X(10, 1, 2, 2, 2, 1) X(11, 2, 2, 1, 1, 1)          \
-    X(12, 1, 1, 4, 1, 2)
-#define OU_TILE_ENTRY(id, wm, wn, wk, mr, nr) {wm, wn, wk, mr, nr},
+    X(0, 1, 4, 1, 1, 2, 0) X(1, 1, 4, 1, 1, 1, 0) X(2, 1, 2, 2, 1, 2, 0) X(3, 2, 2, 1, 1, 2, 0) \
+    X(4, 1, 4, 1, 2, 1, 0) X(5, 2, 2, 1, 2, 2, 0) X(6, 2, 2, 1, 2, 1, 0) X(7, 4, 1, 1, 2, 1, 0) \
+    X(8, 2, 1, 2, 2, 1, 0) X(9, 1, 1, 4, 2, 1, 0) X(10, 1, 2, 2, 2, 1, 0) X(11, 2, 2, 1, 1, 1, 0) \
+    X(12, 1, 1, 4, 1, 2, 0) X(13, 1, 1, 4, 1, 2, 1) X(14, 1, 1, 4, 2, 1, 1) X(15, 2, 2, 1, 1, 1, 1) \
+    X(16, 2, 1, 2, 2, 1, 1) X(17, 1, 2, 2, 2, 1, 1) X(18, 1, 4, 1, 1, 1, 1)
+#define OU_TILE_ENTRY(id, wm, wn, wk, mr, nr, big) {wm, wn, wk, mr, nr, big},
 constexpr Tile kTiles[] = {OU_TILES(OU_TILE_ENTRY)};
 #undef OU_TILE_ENTRY
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
@@ -407,9 +417,13 @@ constexpr bool chunk_ok(int budget)
 {
     return CC / 8 % WK == 0 && Cfg<KT, CC, WM, WN, WK, MR, NR>::LDS2 * 4 <= budget;
 }
-template <int KT, int WM, int WN, int WK, int MR, int NR>
+template <int KT, int WM, int WN, int WK, int MR, int NR, int BIG>
 constexpr int chunk_for()
 {
+    if constexpr (BIG)
+        return chunk_ok<KT, WM, WN, WK, MR, NR, 64>(kMaxLds)   ? 64
+               : chunk_ok<KT, WM, WN, WK, MR, NR, 32>(kMaxLds) ? 32
+                                                               : 16 * (WK > 2 ? 2 : 1);
     return chunk_ok<KT, WM, WN, WK, MR, NR, 64>(kLdsTwoPerCu)   ? 64
            : chunk_ok<KT, WM, WN, WK, MR, NR, 32>(kLdsTwoPerCu) ? 32
            : chunk_ok<KT, WM, WN, WK, MR, NR, 16>(kLdsTwoPerCu) ? 16
@@ -419,23 +433,24 @@ constexpr int chunk_for()
                                                                 : 8 * WK;
 }
 
-template <int KT, int WM, int WN, int WK, int MR, int NR>
+template <int KT, int WM, int WN, int WK, int MR, int NR, int BIG>
 constexpr int lds_bytes_t()
 {
-    constexpr int CC = chunk_for<KT, WM, WN, WK, MR, NR>();
+    constexpr int CC = chunk_for<KT, WM, WN, WK, MR, NR, BIG>();
     return Cfg<KT, CC, WM, WN, WK, MR, NR>::LDS2 * 4;
 }
 
-template <int KT, int WM, int WN, int WK, int MR, int NR>
-int launch_t(const ou_conv_desc& d, hipStream_t s)
+template <int KT, int WM, int WN, int WK, int MR, int NR, int BIG>
+int launch_t(const ou_conv_desc& d, int tpw, hipStream_t s)
 {
-    constexpr int CC = chunk_for<KT, WM, WN, WK, MR, NR>();
+    constexpr int CC = chunk_for<KT, WM, WN, WK, MR, NR, BIG>();
     using C = Cfg<KT, CC, WM, WN, WK, MR, NR>;
     const int mtiles = (d.m + 31) / 32;
     const int cin_eff = d.cin * d.frame;
     const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
     const int nchunks = (cin_eff + CC - 1) / CC;
     const int64_t a_mt_stride = (int64_t)cin_pad * KT * 32;
+    (void)tpw;   // one output tile per workgroup
     dim3 grid((d.n_frames + C::BN - 1) / C::BN, (mtiles + WM * MR - 1) / (WM * MR), d.batch);
     const int lds = (nchunks > 1 ? C::LDS2 : C::LDS1) * (int)sizeof(float);
     auto kern = conv_kernel<KT, CC, WM, WN, WK, MR, NR>;
@@ -454,7 +469,7 @@ template <int KT>
 int lds_bytes_kt(int tile)
 {
     switch (tile) {
-#define OU_TILE_CASE(id, wm, wn, wk, mr, nr) case id: return lds_bytes_t<KT, wm, wn, wk, mr, nr>();
+#define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) case id: return lds_bytes_t<KT, wm, wn, wk, mr, nr, big>();
         OU_TILES(OU_TILE_CASE)
 #undef OU_TILE_CASE
     }
@@ -473,10 +488,10 @@ int lds_bytes(int kt, int tile)
 }
 
 template <int KT>
-int launch_kt(const ou_conv_desc& d, int tile, hipStream_t s)
+int launch_kt(const ou_conv_desc& d, int tile, int tpw, hipStream_t s)
 {
     switch (tile) {
-#define OU_TILE_CASE(id, wm, wn, wk, mr, nr) case id: return launch_t<KT, wm, wn, wk, mr, nr>(d, s);
+#define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) case id: return launch_t<KT, wm, wn, wk, mr, nr, big>(d, tpw, s);
         OU_TILES(OU_TILE_CASE)
 #undef OU_TILE_CASE
     }
@@ -552,15 +567,17 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     if (!d.x || !d.w || !d.y || d.m <= 0 || d.batch <= 0 || d.n_frames <= 0 || d.cin <= 0 ||
         d.frame <= 0 || d.rout <= 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0)
         return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d frame=%d)", d.m, d.rout, d.frame);
-    const int tile = d.tile >= 0 && d.tile < kNumTiles ? d.tile : pick_tile(d);
+    // d.tile: bits 0-7 tile shape (kTiles), bits 8-9 log2(output tiles per workgroup)
+    const int tile = d.tile >= 0 && (d.tile & 0xff) < kNumTiles ? (d.tile & 0xff) : pick_tile(d);
+    const int tpw = d.tile >= 0 ? 1 << ((d.tile >> 8) & 3) : 1;
     if (lds_bytes(d.kt, tile) > kMaxLds)
         return ou_fail(-2, "conv: tile %d needs %d B of LDS for kt=%d", tile, lds_bytes(d.kt, tile), d.kt);
     hipStream_t s = (hipStream_t)stream;
     switch (d.kt) {
-    case 1: return launch_kt<1>(d, tile, s);
-    case 3: return launch_kt<3>(d, tile, s);
-    case 4: return launch_kt<4>(d, tile, s);
-    case 5: return launch_kt<5>(d, tile, s);
+    case 1: return launch_kt<1>(d, tile, tpw, s);
+    case 3: return launch_kt<3>(d, tile, tpw, s);
+    case 4: return launch_kt<4>(d, tile, tpw, s);
+    case 5: return launch_kt<5>(d, tile, tpw, s);
     }
     return ou_fail(-1, "conv: unsupported kt %d", d.kt);
 }
@@ -572,9 +589,22 @@ extern "C" int ou_conv_read_stamps(uint64_t* host, int n)
 }
 #endif
 
+// LDS bytes a tile shape requests at a tap count, and the device's opt-in
+// per-workgroup LDS limit (diagnostics: tools/conv_bench.py --info)
+extern "C" int ou_conv_lds_info(int kt, int tile, int* lds_request, int* device_optin_max)
+{
+    if (lds_request) *lds_request = lds_bytes(kt, tile & 0xff);
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess) return -1;
+    if (device_optin_max) *device_optin_max = v;
+    return 0;
+}
+
 extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile(*d) : -1; }
 extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int ou_conv_tile_ok(int kt, int tile)
 {
+    tile &= 0xff;
     return tile >= 0 && tile < kNumTiles && lds_bytes(kt, tile) > 0 && lds_bytes(kt, tile) <= kMaxLds;
 }

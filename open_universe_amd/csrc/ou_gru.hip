@@ -381,7 +381,7 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
     }
     const int64_t gran_bytes = (int64_t)d.batch * 2 * 2 * H * 8;
     const __amdgpu_buffer_rsrc_t grsrc =
-        __builtin_amdgcn_make_buffer_rsrc(gran, 0, (int)gran_bytes, 0x00020000);
+        ou_rsrc(gran, gran_bytes);
     auto goff = [&](int b, int par) -> int {   // byte offset of this lane's slice
         return (int)(((((int64_t)b * 2 + dir) * 2 + par) * H + lane * KPL) * 8);
     };

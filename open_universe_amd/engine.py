@@ -83,6 +83,10 @@ def make_conv(spec, device):
     w_logical = np.ascontiguousarray(spec.w, dtype=np.float32)
     m, cin_eff, kt = w_logical.shape
     assert cin_eff == spec.cin * spec.frame, (cin_eff, spec.cin, spec.frame)
+    if spec.frame > 1:
+        # logical frame-view channel ci*R + ph -> the kernel's phase-major ph*cin + ci
+        w_logical = np.ascontiguousarray(
+            w_logical.reshape(m, spec.cin, spec.frame, kt).transpose(0, 2, 1, 3).reshape(m, cin_eff, kt))
     cc = L.conv_chunk(kt, spec.frame)
     packed = torch.from_numpy(L.conv_pack(w_logical, cc)).to(device)
     b = None if spec.bias is None else torch.from_numpy(np.ascontiguousarray(spec.bias, np.float32)).to(device)
@@ -356,6 +360,7 @@ class ConvTuner:
 
     def __call__(self, d):
         import ctypes
+        import os
 
         k = self.key(d)
         if k in self.cache:
@@ -363,12 +368,21 @@ class ConvTuner:
         lib = L.load()
         stream = torch.cuda.current_stream().cuda_stream
         best, best_ms = -1, float("inf")
-        for t in range(lib.ou_conv_num_tiles()):
-            if not lib.ou_conv_tile_ok(d.kt, t):
-                continue
+        cands = [t | (tpw << 8) for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t)
+                 for tpw in (0,)]   # tile shape (bits 8-9, tiles per workgroup: reserved)
+        log = os.environ.get("OUHIP_TUNE_LOG")
+        for t in cands:
             d.tile = t
+            if log:   # diagnostics: name every candidate before it runs
+                with open(log, "a") as fh:
+                    fh.write(f"m={d.m} cin={d.cin} frame={d.frame} kt={d.kt} n={d.n_frames} b={d.batch} "
+                             f"rout={d.rout} res1={bool(d.res1)} tile={t & 0xff} tpw={1 << (t >> 8)}\n")
+                    fh.flush()
+                    os.fsync(fh.fileno())
             if lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream)) != 0:
                 continue
+            if log:
+                torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(self.reps):

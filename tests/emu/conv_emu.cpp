@@ -1,0 +1,89 @@
+// Bounds check of every ou_conv tile configuration on the CPU: the HIP
+// source compiled for the host against tests/emu/hip/hip_runtime.h, under
+// AddressSanitizer.  Exits nonzero (ASan report / EMU message) on the first
+// out-of-bounds global, buffer or LDS access.  See tests/test_emu_bounds.py.
+#include "../../open_universe_amd/csrc/ou_conv.hip"
+
+#include <memory>
+
+struct Geom {
+    int cout, cin, frame, kt, T, B, rout;
+    bool res1, res2, film, scale;
+};
+
+static float* alloc(size_t n)
+{
+    float* p = (float*)std::malloc(n * sizeof(float));   // exact size: ASan guards both ends
+    for (size_t i = 0; i < n; ++i) p[i] = 0.25f;
+    return p;
+}
+
+static int run(const Geom& g, int tile)
+{
+    const int cin_eff = g.cin * g.frame;
+    const int m = g.cout * g.rout;
+    const int U = g.rout > 1 ? g.T : (g.T + g.frame - 1) / g.frame;   // frames
+    const int out_len = U * g.rout;
+    std::vector<float> wl((size_t)m * cin_eff * g.kt, 0.1f);
+    const int64_t np = ou_conv_packed_size(m, cin_eff, g.kt, 0);
+    float* w = alloc(np);
+    ou_conv_pack(wl.data(), m, cin_eff, g.kt, 0, w);
+    float* x = alloc((size_t)g.B * g.cin * g.T);
+    float* y = alloc((size_t)g.B * g.cout * out_len);
+    float* bias = alloc(g.cout);
+    float* r1 = g.res1 ? alloc((size_t)g.B * g.cout * out_len) : nullptr;
+    float* r2 = g.res2 ? alloc((size_t)g.B * g.cout * out_len) : nullptr;
+    float* fm = g.film ? alloc((size_t)g.B * 2 * g.cout) : nullptr;
+    float* sc = g.scale ? alloc(g.B) : nullptr;
+    ou_conv_desc d{};
+    d.x = x; d.x_bstride = (int64_t)g.cin * g.T; d.x_cstride = g.T;
+    d.cin = g.cin; d.in_len = g.T; d.frame = g.frame; d.shift = 0; d.in_scale = sc; d.slope = 0.25f;
+    d.w = w; d.m = m; d.kt = g.kt; d.pad = (g.kt - 1) / 2; d.cc = 0;
+    d.n_frames = U; d.batch = g.B;
+    d.y = y; d.y_bstride = (int64_t)g.cout * out_len; d.y_cstride = out_len;
+    d.rout = g.rout; d.out_len = out_len; d.valid_len = out_len - 3;
+    d.bias = bias;
+    d.res1 = r1; d.r1_bstride = d.y_bstride; d.r1_cstride = d.y_cstride; d.s1 = 0.7f;
+    d.film = fm; d.film_bstride = 2 * g.cout;
+    d.res2 = r2; d.r2_bstride = d.y_bstride; d.r2_cstride = d.y_cstride; d.s2 = 0.5f;
+    d.tile = tile;
+    const int rc = ou_conv(&d, nullptr);
+    for (float* p : {w, x, y, bias, r1, r2, fm, sc}) std::free(p);
+    return rc;
+}
+
+int main(int argc, char** argv)
+{
+    const Geom geoms[] = {
+        {64, 64, 1, 3, 517, 2, 1, false, false, false, false},
+        {64, 64, 1, 5, 517, 2, 1, true, false, false, false},
+        {32, 32, 1, 3, 1000, 1, 1, true, false, false, true},
+        {96, 40, 1, 1, 77, 2, 1, false, true, true, false},
+        {512, 256, 1, 3, 33, 2, 1, true, false, true, false},
+        {64, 32, 2, 3, 300, 2, 1, false, false, false, false},
+        {48, 24, 5, 3, 203, 1, 1, false, false, false, false},
+        {642, 1, 160, 4, 1600, 1, 1, false, false, false, false},   // STFT as a framed GEMM
+        {128, 256, 1, 3, 41, 2, 4, true, false, false, false},      // transposed conv, 4 phases
+        {160, 96, 1, 3, 67, 1, 5, false, false, false, false},      // M = 800, partial m-groups
+    };
+    const int only = argc > 1 ? std::atoi(argv[1]) : -1;
+    int n = 0;
+    for (int gi = 0; gi < (int)(sizeof(geoms) / sizeof(geoms[0])); ++gi) {
+        if (only >= 0 && gi != only) continue;
+        const Geom& g = geoms[gi];
+        for (int t = 0; t < ou_conv_num_tiles(); ++t) {
+            if (!ou_conv_tile_ok(g.kt, t)) continue;
+            for (int tpw = 0; tpw < 3; ++tpw) {
+                if (std::getenv("OUHIP_EMU_VERBOSE")) std::fprintf(stderr, "geom %d tile %d tpw %d\n", gi, t, tpw);
+                const int rc = run(g, t | (tpw << 8));
+                if (rc != 0) {
+                    std::fprintf(stderr, "geom %d tile %d tpw %d: ou_conv returned %d\n", gi, t, tpw, rc);
+                    return 2;
+                }
+                ++n;
+            }
+        }
+    }
+    std::printf("ok: %d launches bounds-checked\n", n);
+    return 0;
+}

@@ -1,0 +1,110 @@
+// Numerics of every ou_conv tile configuration on the CPU (fiber emulator,
+// tests/emu/hip/hip_runtime.h with OU_EMU_FIBERS): each launch is compared
+// with a double-precision evaluation of the ou_conv_desc formula in
+// include/ouhip.h.  Prints one line per failing (geometry, tile) and exits 1.
+#include "../../open_universe_amd/csrc/ou_conv.hip"
+
+#include <cmath>
+
+struct Geom {
+    int cout, cin, frame, kt, T, B, rout;
+    bool res1, res2, film, scale;
+};
+
+static uint32_t g_seed = 12345;
+static float rnd()
+{
+    g_seed = g_seed * 1664525u + 1013904223u;
+    return ((g_seed >> 8) & 0xffff) / 32768.0f - 1.0f;
+}
+
+int main(int argc, char** argv)
+{
+    const Geom geoms[] = {
+        {64, 64, 1, 3, 133, 2, 1, false, false, false, false},
+        {64, 64, 1, 3, 517, 2, 1, false, false, false, false},   // test_same_conv_layer[conv3-3-1-517]
+        {64, 64, 1, 5, 70, 2, 1, true, false, false, false},
+        {32, 32, 1, 3, 300, 1, 1, true, false, false, true},
+        {96, 40, 1, 1, 41, 2, 1, false, true, true, false},
+        {64, 32, 2, 3, 100, 2, 1, false, false, false, false},
+        {48, 24, 5, 3, 103, 1, 1, false, false, false, false},
+        {64, 48, 1, 3, 29, 2, 4, true, false, false, false},   // transposed conv, 4 phases
+    };
+    const int only = argc > 1 ? std::atoi(argv[1]) : -1;
+    int bad = 0, n = 0;
+    for (int gi = 0; gi < (int)(sizeof(geoms) / sizeof(geoms[0])); ++gi) {
+        if (only >= 0 && gi != only) continue;
+        const Geom& g = geoms[gi];
+        const int cin_eff = g.cin * g.frame, m = g.cout * g.rout;
+        const int U = g.rout > 1 ? g.T : (g.T + g.frame - 1) / g.frame;
+        const int out_len = U * g.rout, valid = out_len - 2, pad = (g.kt - 1) / 2;
+        std::vector<float> wl((size_t)m * cin_eff * g.kt), x((size_t)g.B * g.cin * g.T), bias(g.cout),
+            r1((size_t)g.B * g.cout * out_len), r2(r1.size()), fm((size_t)g.B * 2 * g.cout), sc(g.B);
+        for (auto* v : {&wl, &x, &bias, &r1, &r2, &fm, &sc})
+            for (auto& e : *v) e = rnd();
+        std::vector<float> packed(ou_conv_packed_size(m, cin_eff, g.kt, 0));
+        ou_conv_pack(wl.data(), m, cin_eff, g.kt, 0, packed.data());
+        // reference
+        std::vector<double> ref((size_t)g.B * g.cout * out_len, 0.0);
+        for (int b = 0; b < g.B; ++b)
+            for (int mm = 0; mm < m; ++mm) {
+                const int ph = mm / g.cout, co = mm % g.cout;
+                for (int u = 0; u < U; ++u) {
+                    double acc = 0.0;
+                    for (int c = 0; c < cin_eff; ++c)
+                        for (int k = 0; k < g.kt; ++k) {
+                            const int fu = u + k - pad;
+                            if (fu < 0 || fu >= U) continue;
+                            const int ci = c % g.cin, fph = c / g.cin;
+                            const int pos = fu * g.frame + fph;
+                            if (pos >= g.T) continue;
+                            double xv = x[((size_t)b * g.cin + ci) * g.T + pos] * (g.scale ? sc[b] : 1.0f);
+                            if (xv < 0) xv *= 0.25;
+                            acc += (double)wl[((size_t)mm * cin_eff + c) * g.kt + k] * xv;
+                        }
+                    const int t = u * g.rout + ph;
+                    double v = acc + bias[co];
+                    if (t >= valid) v = 0;
+                    const size_t o = ((size_t)b * g.cout + co) * out_len + t;
+                    if (g.res1) v = (v + r1[o]) * 0.7;
+                    if (g.film) v = fm[(size_t)b * 2 * g.cout + co] * v + fm[(size_t)b * 2 * g.cout + g.cout + co];
+                    if (g.res2) v = (v + r2[o]) * 0.5;
+                    ref[o] = v;
+                }
+            }
+        double rn = 0;
+        for (double v : ref) rn += v * v;
+        for (int t = 0; t < ou_conv_num_tiles(); ++t) {
+            if (!ou_conv_tile_ok(g.kt, t)) continue;
+            for (int tpw = 0; tpw < 3; ++tpw) {
+                std::vector<float> y(ref.size(), 1e30f);
+                ou_conv_desc d{};
+                d.x = x.data(); d.x_bstride = (int64_t)g.cin * g.T; d.x_cstride = g.T;
+                d.cin = g.cin; d.in_len = g.T; d.frame = g.frame; d.in_scale = g.scale ? sc.data() : nullptr;
+                d.slope = 0.25f; d.w = packed.data(); d.m = m; d.kt = g.kt; d.pad = pad;
+                d.n_frames = U; d.batch = g.B; d.y = y.data(); d.y_bstride = (int64_t)g.cout * out_len;
+                d.y_cstride = out_len; d.rout = g.rout; d.out_len = out_len; d.valid_len = valid;
+                d.bias = bias.data();
+                d.res1 = g.res1 ? r1.data() : nullptr; d.r1_bstride = d.y_bstride; d.r1_cstride = out_len; d.s1 = 0.7f;
+                d.film = g.film ? fm.data() : nullptr; d.film_bstride = 2 * g.cout;
+                d.res2 = g.res2 ? r2.data() : nullptr; d.r2_bstride = d.y_bstride; d.r2_cstride = out_len; d.s2 = 0.5f;
+                d.tile = t | (tpw << 8);
+                if (ou_conv(&d, nullptr) != 0) {
+                    std::printf("geom %d tile %d tpw %d: launch error\n", gi, t, tpw);
+                    ++bad;
+                    continue;
+                }
+                double en = 0;
+                for (size_t i = 0; i < y.size(); ++i) en += (y[i] - ref[i]) * (y[i] - ref[i]);
+                const double rel = std::sqrt(en / rn);
+                ++n;
+                if (!(rel < 1e-5)) {
+                    std::printf("geom %d tile %d tpw %d: rel err %.3g\n", gi, t, tpw, rel);
+                    ++bad;
+                }
+            }
+        }
+    }
+    std::printf("%s: %d launches checked, %d bad\n", bad ? "FAIL" : "ok", n, bad);
+    return bad ? 1 : 0;
+}

@@ -5,7 +5,7 @@ import sys
 
 rows, cur = [], None
 for line in sys.stdin:
-    m = re.search(r"remark: \S+ (.*?) \[-Rpass", line)
+    m = re.search(r"remark:\s+(?:\S+:\d+:\d+:\s+)?(.*?) \[-Rpass", line)
     if not m:
         continue
     t = m.group(1).strip()
