@@ -85,7 +85,9 @@ typedef struct ou_conv_desc {
     int64_t r2_bstride, r2_cstride;
     float s2;
     int32_t tile;              /* -1 = auto; bits 0-7 tile shape (< ou_conv_     */
-                               /* num_tiles()); bits 8-9 reserved (0)            */
+                               /* num_tiles()), bits 8-9 log2(output tiles per   */
+                               /* workgroup; > 0: persistent kernel, see         */
+                               /* ou_conv_tile_ok)                               */
     int32_t _reserved;
 } ou_conv_desc;
 

@@ -388,6 +388,290 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     OU_CSTAMP_SAVE;
 }
 
+// ---------------------------------------------------------------------------
+// Persistent variant (tiles-per-workgroup >= 2, shapes without split-K).
+//
+// All workgroups of the one-tile kernel above run in lockstep, so the whole
+// grid loads X, then computes, then writes its outputs at the same moment:
+// the HBM bursts and the MFMA phases add up.  Here a workgroup walks output
+// tiles blockIdx.x, +gridDim.x, ...; its (tile, chunk) work items form one
+// stream whose next item -- the next tile's first chunk included -- is loaded
+// while the current item's MFMAs run, and the residual + bias of a tile's
+// epilogue are loaded at the start of its last chunk.  The epilogue's stores
+// then drain while the next tile computes.
+// ---------------------------------------------------------------------------
+template <int KT, int CC, int WM, int WN, int MR, int NR>
+__global__ __launch_bounds__(256) void conv_pkernel(ou_conv_desc d, int nchunks, int mtiles,
+                                                    int64_t a_mt_stride, int ntn, int mgroups, int ntiles)
+{
+    constexpr int WK = 1;
+    using C = Cfg<KT, CC, WM, WN, WK, MR, NR>;
+    static_assert(CC % 8 == 0 && WM * WN == 4, "4 waves, no split-K");
+    static_assert((C::SX / 4) % 2 == 1, "X row stride must be an odd number of 16-B slots");
+    OU_DYNAMIC_LDS(float4, lds4);
+    float* lds = (float*)lds4;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wn = wave % WN;
+    const int wm = wave / WN;
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+    const int R = d.frame;
+    const int cin = d.cin;
+    const int in_len = d.in_len;
+    const int xc = (int)d.x_cstride;
+    const float slope = d.slope;
+
+    // staging geometry independent of the tile
+    int xdst[C::XE], xw[C::XE], xcl[C::XE];
+#pragma unroll
+    for (int e = 0; e < C::XE; ++e) {
+        const int g = tid + e * 256;
+        const int w = g % C::W;
+        const int r = g / C::W;
+        xdst[e] = g < C::XG ? w * C::SX + (r & 1) * C::HALF + 4 * (r >> 1) : -1;
+        xw[e] = w;
+        xcl[e] = 8 * (r >> 1) + (r & 1);
+    }
+    const __amdgpu_buffer_rsrc_t wrs = ou_rsrc(d.w, (int64_t)mtiles * a_mt_stride * 4);
+    int aoff[C::AE], aml[C::AE];
+#pragma unroll
+    for (int e = 0; e < C::AE; ++e) {
+        const int f = min(tid + e * 256, C::AG - 1);
+        const int ml = f / (C::HQ * KT * 64);
+        aml[e] = ml;
+        aoff[e] = (int)((ml * a_mt_stride + (f - ml * (C::HQ * KT * 64)) * 4) * 4);
+    }
+
+    float xr[4 * C::XE];
+    float ar[4 * C::AE];
+    float xscale = 1.f;   // in_scale of the item held in xr
+
+#define OU_DECODE(tile_, b_, n0_, mt0_)                                                        \
+    const int b_ = (tile_) / ntn / mgroups;                                                    \
+    const int n0_ = ((tile_) % ntn) * C::BN;                                                   \
+    const int mt0_ = (((tile_) / ntn) % mgroups) * (WM * MR);
+
+    auto load_item = [&](int tile, int q) {
+        OU_DECODE(tile, b, n0, mt0)
+        const int t0 = n0 - d.pad;
+        const float* xb = d.x + (int64_t)b * d.x_bstride;
+        xscale = d.in_scale ? d.in_scale[b] : 1.0f;
+        if (R == 1) {
+            const int nch = cin - q * CC;
+            const __amdgpu_buffer_rsrc_t rs = ou_rsrc(xb + (int64_t)q * CC * xc, nch > 0 ? (int64_t)nch * xc * 4 : 0);
+#pragma unroll
+            for (int e = 0; e < C::XE; ++e) {
+                const int pos = t0 + xw[e] + d.shift;
+                const bool ok = xdst[e] >= 0 && pos >= 0 && pos < in_len;
+                const unsigned o = ok ? (unsigned)((xcl[e] * xc + pos) * 4) : (unsigned)kSentinel;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    xr[4 * e + j] = __uint_as_float(
+                        __builtin_amdgcn_raw_buffer_load_b32(rs, o + j * 8u * (unsigned)xc, 0, 0));
+            }
+        } else if (cin % CC == 0) {
+            const int ph = (q * CC) / cin;
+            const int ci0 = q * CC - ph * cin;
+            const __amdgpu_buffer_rsrc_t rs = ou_rsrc(xb + (int64_t)ci0 * xc, (int64_t)(cin - ci0) * xc * 4);
+#pragma unroll
+            for (int e = 0; e < C::XE; ++e) {
+                const int pos = (t0 + xw[e]) * R + d.shift + ph;
+                const bool ok = xdst[e] >= 0 && pos >= 0 && pos < in_len;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    xr[4 * e + j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        rs, ok ? ((xcl[e] + 2 * j) * xc + pos) * 4 : kSentinel, 0, 0));
+            }
+        } else {
+            const __amdgpu_buffer_rsrc_t rs = ou_rsrc(xb, (int64_t)cin * xc * 4);
+#pragma unroll
+            for (int e = 0; e < C::XE; ++e) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int cq = q * CC + xcl[e] + 2 * j;
+                    const int ph = cq / cin;
+                    const int ci = cq - ph * cin;
+                    const int pos = (t0 + xw[e]) * R + d.shift + ph;
+                    const int off = (xdst[e] >= 0 && ph < R && pos >= 0 && pos < in_len) ? (ci * xc + pos) * 4
+                                                                                         : kSentinel;
+                    xr[4 * e + j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+                }
+            }
+        }
+        // the range check covers the voffset only: m-tiles past the weights
+        // get the sentinel voffset (the tile offset travels in soffset)
+        const int soff = (int)((mt0 * a_mt_stride + (int64_t)q * (C::HQ * KT * 256)) * 4);
+#pragma unroll
+        for (int e = 0; e < C::AE; ++e) {
+            const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(wrs, mt0 + aml[e] < mtiles ? aoff[e] : kSentinel,
+                                                                   soff, 0);
+            ar[4 * e] = __uint_as_float(v4[0]);
+            ar[4 * e + 1] = __uint_as_float(v4[1]);
+            ar[4 * e + 2] = __uint_as_float(v4[2]);
+            ar[4 * e + 3] = __uint_as_float(v4[3]);
+        }
+    };
+
+    auto store_item = [&](int buf) {
+        float* xs = lds + buf * C::STAGE;
+        const float sc = xscale;
+#define OU_PRELU(v) ((v) * sc >= 0.f ? (v) * sc : (v) * sc * slope)
+#pragma unroll
+        for (int e = 0; e < C::XE; ++e)
+            if (xdst[e] >= 0)
+                *(float4*)(xs + xdst[e]) = make_float4(OU_PRELU(xr[4 * e]), OU_PRELU(xr[4 * e + 1]),
+                                                       OU_PRELU(xr[4 * e + 2]), OU_PRELU(xr[4 * e + 3]));
+#undef OU_PRELU
+        float4* as = (float4*)(xs + C::XBUF);
+#pragma unroll
+        for (int e = 0; e < C::AE; ++e)
+            if (C::AG % 256 == 0 || tid + e * 256 < C::AG)
+                as[tid + e * 256] = make_float4(ar[4 * e], ar[4 * e + 1], ar[4 * e + 2], ar[4 * e + 3]);
+    };
+
+    const int M = d.m;
+    const int rout = d.rout;
+    const int cout = M / rout;
+    const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr;
+    float ev1[MR][NR][16];
+    float ebias[MR][16];
+    auto row_of = [&](int mt, int r, int& co, int& ph) {
+        const int m = min(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
+        ph = rout > 1 ? m / cout : 0;
+        co = m - ph * cout;
+    };
+    // residual 1 and bias of a tile's epilogue, issued one chunk ahead
+    auto load_epilogue = [&](int tile) {
+        OU_DECODE(tile, b, n0, mt0)
+        const __amdgpu_buffer_rsrc_t r1s = ou_rsrc(has_r1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y,
+                                                   has_r1 ? (int64_t)cout * d.r1_cstride * 4 : 0);
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr) {
+            const int mt = mt0 + wm * MR + mr;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                int co, ph;
+                row_of(mt, r, co, ph);
+                ebias[mr][r] = d.bias ? d.bias[co] : 0.f;
+                const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr) {
+                    const int u = n0 + wn * (32 * NR) + nr * 32 + l32;
+                    const int t = u * rout + ph;
+                    const bool ok = has_r1 && m < M && u < d.n_frames && t < d.out_len;
+                    ev1[mr][nr][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        r1s, ok ? (co * (int)d.r1_cstride + t) * 4 : kSentinel, 0, 0));
+                }
+            }
+        }
+    };
+
+    floatx16 acc[MR][NR];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    int tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    load_item(tile, 0);
+    store_item(0);
+    __syncthreads();
+    int buf = 0;
+    while (true) {
+        for (int q = 0; q < nchunks; ++q) {
+            const int ntile = q + 1 < nchunks ? tile : tile + (int)gridDim.x;
+            const int nq = q + 1 < nchunks ? q + 1 : 0;
+            const bool has_next = ntile < ntiles;
+            if (q + 1 == nchunks) load_epilogue(tile);
+            if (has_next) load_item(ntile, nq);
+            {
+                const float* xs = lds + buf * C::STAGE;
+                const float4* ap = (const float4*)(xs + C::XBUF) + (wm * MR) * C::HQ * KT * 64 + lane;
+                const float* xp = xs + (wn * 32 * NR + l32) * C::SX + h * C::HALF;
+                constexpr int NS = C::CPW * KT;
+                float4 fa[2][MR], fb[2][NR];
+                auto frag = [&](int st, float4* a, float4* bq) {
+                    const int cpq = st / KT, k = st - (st / KT) * KT;
+#pragma unroll
+                    for (int mr = 0; mr < MR; ++mr) a[mr] = ap[((mr * C::HQ + cpq) * KT + k) * 64];
+#pragma unroll
+                    for (int nr = 0; nr < NR; ++nr)
+                        bq[nr] = *(const float4*)(xp + (nr * 32 + k) * C::SX + 4 * cpq);
+                };
+                frag(0, fa[0], fb[0]);
+#pragma unroll
+                for (int st = 0; st < NS; ++st) {
+                    if (st + 1 < NS) frag(st + 1, fa[(st + 1) & 1], fb[(st + 1) & 1]);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                            for (int nr = 0; nr < NR; ++nr)
+                                acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                                    fa[st & 1][mr][j], fb[st & 1][nr][j], acc[mr][nr], 0, 0, 0);
+                }
+            }
+            if (has_next) store_item(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+        }
+
+        // epilogue of `tile`: branch-free, out-of-range elements dropped
+        {
+            OU_DECODE(tile, b, n0, mt0)
+            const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)cout * d.y_cstride * 4);
+            const __amdgpu_buffer_rsrc_t r2s = ou_rsrc(has_r2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y,
+                                                       has_r2 ? (int64_t)cout * d.r2_cstride * 4 : 0);
+            const float* fm = d.film ? d.film + (int64_t)b * d.film_bstride : nullptr;
+#pragma unroll
+            for (int mr = 0; mr < MR; ++mr) {
+                const int mt = mt0 + wm * MR + mr;
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr) {
+                    const int u = n0 + wn * (32 * NR) + nr * 32 + l32;
+                    int off[16];
+                    float v2[16];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        int co, ph;
+                        row_of(mt, r, co, ph);
+                        const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        const int t = u * rout + ph;
+                        const bool ok = m < M && u < d.n_frames && t < d.out_len;
+                        off[r] = ok ? t : -1;
+                        v2[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                            r2s, (has_r2 && ok) ? (co * (int)d.r2_cstride + t) * 4 : kSentinel, 0, 0));
+                    }
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        int co, ph;
+                        row_of(mt, r, co, ph);
+                        float v = acc[mr][nr][r] + ebias[mr][r];
+                        if (off[r] >= d.valid_len) v = 0.f;
+                        if (has_r1) v = (v + ev1[mr][nr][r]) * d.s1;
+                        if (fm) v = fm[co] * v + fm[cout + co];
+                        if (has_r2) v = (v + v2[r]) * d.s2;
+                        __builtin_amdgcn_raw_buffer_store_b32(
+                            __float_as_uint(v), ys, off[r] >= 0 ? (co * (int)d.y_cstride + off[r]) * 4 : kSentinel,
+                            0, 0);
+                        acc[mr][nr][r] = 0.f;
+                    }
+                }
+            }
+        }
+        tile += gridDim.x;
+        if (tile >= ntiles) break;
+    }
+#undef OU_DECODE
+}
+
 // ---- tile table ------------------------------------------------------------
 struct Tile {
     int wm, wn, wk, mr, nr, big;
@@ -465,6 +749,37 @@ int launch_t(const ou_conv_desc& d, int tpw, hipStream_t s)
     return ou_check_launch("conv");
 }
 
+// persistent launch: ceil(tiles / tpw) workgroups, each walking tpw tiles
+template <int KT, int WM, int WN, int WK, int MR, int NR, int BIG>
+int launch_p(const ou_conv_desc& d, int tpw, hipStream_t s)
+{
+    if constexpr (WK != 1) {
+        return ou_fail(-2, "conv: tiles per workgroup > 1 needs a tile without split-K");
+    } else {
+        constexpr int CC = chunk_for<KT, WM, WN, WK, MR, NR, BIG>();
+        using C = Cfg<KT, CC, WM, WN, WK, MR, NR>;
+        const int mtiles = (d.m + 31) / 32;
+        const int cin_eff = d.cin * d.frame;
+        const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
+        const int nchunks = (cin_eff + CC - 1) / CC;
+        const int64_t a_mt_stride = (int64_t)cin_pad * KT * 32;
+        const int ntn = (d.n_frames + C::BN - 1) / C::BN;
+        const int mgroups = (mtiles + WM * MR - 1) / (WM * MR);
+        const int ntiles = ntn * mgroups * d.batch;
+        const int lds = 2 * C::STAGE * (int)sizeof(float);
+        auto kern = conv_pkernel<KT, CC, WM, WN, MR, NR>;
+        static bool attr = false;
+        if (!attr && lds > 64 * 1024) {
+            OU_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds),
+                         "conv: LDS attribute");
+            attr = true;
+        }
+        hipLaunchKernelGGL(kern, dim3((ntiles + tpw - 1) / tpw), dim3(256), lds, s, d, nchunks, mtiles, a_mt_stride,
+                           ntn, mgroups, ntiles);
+        return ou_check_launch("conv");
+    }
+}
+
 template <int KT>
 int lds_bytes_kt(int tile)
 {
@@ -491,7 +806,10 @@ template <int KT>
 int launch_kt(const ou_conv_desc& d, int tile, int tpw, hipStream_t s)
 {
     switch (tile) {
-#define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) case id: return launch_t<KT, wm, wn, wk, mr, nr, big>(d, tpw, s);
+#define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big)                                              \
+    case id:                                                                                   \
+        return tpw > 1 ? launch_p<KT, wm, wn, wk, mr, nr, big>(d, tpw, s)                     \
+                       : launch_t<KT, wm, wn, wk, mr, nr, big>(d, tpw, s);
         OU_TILES(OU_TILE_CASE)
 #undef OU_TILE_CASE
     }
@@ -567,7 +885,8 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     if (!d.x || !d.w || !d.y || d.m <= 0 || d.batch <= 0 || d.n_frames <= 0 || d.cin <= 0 ||
         d.frame <= 0 || d.rout <= 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0)
         return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d frame=%d)", d.m, d.rout, d.frame);
-    // d.tile: bits 0-7 tile shape (kTiles), bits 8-9 log2(output tiles per workgroup)
+    // d.tile: bits 0-7 tile shape (kTiles), bits 8-9 log2(output tiles per
+    // workgroup: > 1 selects the persistent kernel, shapes without split-K)
     const int tile = d.tile >= 0 && (d.tile & 0xff) < kNumTiles ? (d.tile & 0xff) : pick_tile(d);
     const int tpw = d.tile >= 0 ? 1 << ((d.tile >> 8) & 3) : 1;
     if (lds_bytes(d.kt, tile) > kMaxLds)
@@ -605,6 +924,10 @@ extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile(*
 extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int ou_conv_tile_ok(int kt, int tile)
 {
+    if ((tile >> 8) & 3) {   // persistent: shapes without split-K only
+        const int t = tile & 0xff;
+        if (t >= kNumTiles || kTiles[t].wk != 1) return 0;
+    }
     tile &= 0xff;
     return tile >= 0 && tile < kNumTiles && lds_bytes(kt, tile) > 0 && lds_bytes(kt, tile) <= kMaxLds;
 }

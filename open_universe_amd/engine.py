@@ -368,8 +368,9 @@ class ConvTuner:
         lib = L.load()
         stream = torch.cuda.current_stream().cuda_stream
         best, best_ms = -1, float("inf")
-        cands = [t | (tpw << 8) for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t)
-                 for tpw in (0,)]   # tile shape (bits 8-9, tiles per workgroup: reserved)
+        # tile shape x log2(output tiles per workgroup); > 0 = persistent kernel
+        cands = [t | (tpw << 8) for t in range(lib.ou_conv_num_tiles()) for tpw in (0, 1, 2)
+                 if lib.ou_conv_tile_ok(d.kt, t | (tpw << 8))]
         log = os.environ.get("OUHIP_TUNE_LOG")
         for t in cands:
             d.tile = t

@@ -74,6 +74,7 @@ int main(int argc, char** argv)
         for (int t = 0; t < ou_conv_num_tiles(); ++t) {
             if (!ou_conv_tile_ok(g.kt, t)) continue;
             for (int tpw = 0; tpw < 3; ++tpw) {
+                if (!ou_conv_tile_ok(g.kt, t | (tpw << 8))) continue;
                 if (std::getenv("OUHIP_EMU_VERBOSE")) std::fprintf(stderr, "geom %d tile %d tpw %d\n", gi, t, tpw);
                 const int rc = run(g, t | (tpw << 8));
                 if (rc != 0) {

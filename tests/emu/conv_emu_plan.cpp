@@ -52,6 +52,7 @@ int main(int argc, char** argv)
         for (int t = 0; t < ou_conv_num_tiles(); ++t) {
             if (!ou_conv_tile_ok(d.kt, t)) continue;
             for (int tpw = 0; tpw < 3; ++tpw) {
+                if (!ou_conv_tile_ok(d.kt, t | (tpw << 8))) continue;
                 if (std::getenv("OUHIP_EMU_VERBOSE"))
                     std::fprintf(stderr, "conv %zu (m %d cin %d frame %d kt %d n %d rout %d) tile %d tpw %d\n", ci, d.m,
                                  d.cin, d.frame, d.kt, d.n_frames, d.rout, t, tpw);

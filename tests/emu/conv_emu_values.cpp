@@ -77,6 +77,7 @@ int main(int argc, char** argv)
         for (int t = 0; t < ou_conv_num_tiles(); ++t) {
             if (!ou_conv_tile_ok(g.kt, t)) continue;
             for (int tpw = 0; tpw < 3; ++tpw) {
+                if (!ou_conv_tile_ok(g.kt, t | (tpw << 8))) continue;
                 std::vector<float> y(ref.size(), 1e30f);
                 ou_conv_desc d{};
                 d.x = x.data(); d.x_bstride = (int64_t)g.cin * g.T; d.x_cstride = g.T;

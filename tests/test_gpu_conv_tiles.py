@@ -60,6 +60,8 @@ def test_conv_every_tile(geom):
         if not lib.ou_conv_tile_ok(kt, t):
             continue
         for tpw in (0, 1, 2):
+            if not lib.ou_conv_tile_ok(kt, t | (tpw << 8)):
+                continue
             y = E.new_act(B, cout, U, DEV)
             ra = E.Act(res.to(DEV)) if with_res else None
             d = E.conv_desc(cw, xa, y, res1=ra, s1=0.7, n_frames=U)

@@ -81,8 +81,8 @@ def main():
     names = [a.layer] if a.layer else list(LAYERS)
     for name in names:
         d, keep = make(name, dev)
-        tiles = [a.tile] if a.tile is not None else [t for t in range(lib.ou_conv_num_tiles())
-                                                      if lib.ou_conv_tile_ok(d.kt, t)]
+        tiles = [a.tile] if a.tile is not None else [t | (p << 8) for t in range(lib.ou_conv_num_tiles())
+                                                      for p in (0, 1, 2) if lib.ou_conv_tile_ok(d.kt, t | (p << 8))]
         res = []
         for t in tiles:
             ms = time_tile(d, t, a.reps, stream)
@@ -90,8 +90,9 @@ def main():
                 res.append((ms, t))
         res.sort()
         fl = d._flops
-        line = "  ".join(f"t{t}:{ms * 1e3:.1f}us/{fl / ms / 1e9:.0f}TF" for ms, t in res)
-        print(f"{name:5s} {fl / 1e9:6.2f} GFLOP  best t{res[0][1]} {res[0][0] * 1e3:.1f} us "
+        nm = lambda t: f"t{t & 0xff}" + (f"p{1 << (t >> 8)}" if t >> 8 else "")
+        line = "  ".join(f"{nm(t)}:{ms * 1e3:.1f}us" for ms, t in res[:12])
+        print(f"{name:5s} {fl / 1e9:6.2f} GFLOP  best {nm(res[0][1])} {res[0][0] * 1e3:.1f} us "
               f"{fl / res[0][0] / 1e9:.1f} TF/s | {line}", flush=True)
         if a.stamps:
             import ctypes

@@ -11,8 +11,8 @@ for line in sys.stdin:
     t = m.group(1).strip()
     if t.startswith("Function Name:"):
         nm = t.split(":", 1)[1].strip()
-        a = re.search(r"_kernelI(.*?)EEv", nm)
-        base = re.search(r"N_\d+(\w+?_kernel)", nm)
+        a = re.search(r"kernelI(.*?)EEv", nm)
+        base = re.search(r"N_\d+([A-Za-z_]+?kernel)I", nm)
         cur = {"n": (base.group(1) if base else nm[:30]) + "<" +
                ",".join(re.findall(r"Li(\d+)E", a.group(1) if a else "")) + ">"}
         rows.append(cur)
