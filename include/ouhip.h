@@ -236,6 +236,15 @@ int ou_finish(const float* x, int64_t x_bstride, int left, float* y, int batch,
 int ou_ensemble_reduce(const float* x, float* y, int ensemble, int64_t n,
                        int mode /* 0 mean, 1 median */, void* stream);
 
+/* Audio-rate resampling around enhance(): replaces
+ * torchaudio.functional.resample(x, orig, new) with its defaults
+ * (sinc_interp_hann, lowpass width 6, rolloff 0.99) that the reference CLI
+ * applies before and after the model (bin/enhance.py:61-64, 186-190).
+ * orig/new reduced by their gcd; kernel = [phases = new][taps = 2*width + orig]
+ * (dsp.sinc_resample_kernel); n_out = ceil(new * n_in / orig). */
+int ou_resample(const float* x, int64_t x_bstride, float* y, int64_t y_bstride, int batch, int n_in,
+                int n_out, const float* kernel, int phases, int taps, int orig, int width, void* stream);
+
 /* Alias-free Snake of the signal-decoupling layer (universe_gan.py:119-151;
  * bigvgan/snake.py:131-157, alias_free_act.py:8-30): torchaudio-style 2x
  * sinc up-sampling, Snake x + sin^2(a x)/(a + 1e-9), 2x down-sampling.  The

@@ -150,6 +150,8 @@ EXPORTS = {
     "ou_finish": (c_int, [fp, c_int64, c_int, fp, c_int, c_int, fp, c_void_p]),
     "ou_ensemble_reduce": (c_int, [fp, fp, c_int, c_int64, c_int, c_void_p]),
     "ou_snake_aa": (c_int, [POINTER(SnakeDesc), c_void_p]),
+    "ou_resample": (c_int, [fp, c_int64, fp, c_int64, c_int, c_int, c_int, fp, c_int, c_int, c_int, c_int,
+                            c_void_p]),
     "ou_program_create": (c_void_p, []),
     "ou_program_destroy": (None, [c_void_p]),
     "ou_program_add": (c_int, [c_void_p, c_int, c_void_p, c_size_t]),

@@ -1,0 +1,87 @@
+#!/usr/bin/env python
+"""Enhance a WAV file or a folder of WAV files (mirrors the reference's
+open_universe/bin/enhance.py:1-192): same positional arguments, ``--model``,
+``--model-strict``, ``--seed``, ``--device`` and the ``enhance()`` options
+added from the model's signature (``inference_utils.add_enhance_arguments``).
+The folder structure is kept.
+
+Differences: audio is resampled to ``model.fs`` and back on the GPU
+(``audio.resample``); only WAV is read; the model must be a local checkpoint
+(the Hugging Face hub needs the network).  Under torchrun (WORLD_SIZE > 1)
+each rank enhances its share of the files on ``cuda:LOCAL_RANK``
+(``sharding.shard_utterances``, balanced by file size) -- no collectives.
+
+    python -m open_universe_amd.bin.enhance noisy/ enhanced/ --model exp/ckpt.ckpt
+    python -m torch.distributed.run --nproc-per-node 8 -m open_universe_amd.bin.enhance noisy/ out/ --model ...
+"""
+import argparse
+import os
+import sys
+from pathlib import Path
+
+import torch
+
+from open_universe_amd import inference_utils
+from open_universe_amd.audio import load_audio, resample, save_audio
+from open_universe_amd.sharding import dist_env, shard_utterances
+
+AUDIO_SUFFIXES = [".wav"]
+
+
+def find_files(path):
+    """(files, root, is_dir) as bin/enhance.py:46-58."""
+    if not path.is_dir():
+        return [path], path.parent, False
+    return sorted(p for p in path.rglob("*") if p.suffix.lower() in AUDIO_SUFFIXES), path, True
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser(description="Enhance a file or a directory of audio files")
+    parser.add_argument("input", type=Path, help="Path to an audio file or a folder of audio files")
+    parser.add_argument("output", type=Path, help="Output path; for a folder the structure is retained")
+    parser.add_argument("--model", type=str, required=True, help="Local checkpoint (.ckpt) of the model")
+    parser.add_argument("--model-strict", action="store_true", help="Strict state-dict loading")
+    parser.add_argument("--seed", type=int, default=1028282, help="Seed of the sampler noise")
+    parser.add_argument("--device", type=str, default=None, help="cuda:X (default: cuda:LOCAL_RANK)")
+    args, _ = parser.parse_known_args(argv)
+
+    rank, local, world = dist_env()
+    device = args.device or f"cuda:{local}"
+    if not device.startswith("cuda") or not torch.cuda.is_available():
+        raise SystemExit("open_universe_amd runs on a ROCm device (cuda:X); the CPU path is the reference")
+    torch.cuda.set_device(torch.device(device))
+    model = inference_utils.load_model(args.model, device=device, strict=args.model_strict)
+    rng = torch.Generator(device=device)
+    rng.manual_seed(args.seed + rank)
+
+    inference_utils.add_enhance_arguments(model, parser)
+    args = parser.parse_args(argv)
+    groups = {g.title: {a.dest: getattr(args, a.dest, None) for a in g._group_actions}
+              for g in parser._action_groups}
+    enhance_kwargs = dict(groups.get("enhance", {}))
+    enhance_kwargs["rng"] = rng
+
+    files, root, is_dir = find_files(args.input)
+    if world > 1:
+        mine = shard_utterances([p.stat().st_size for p in files], world)[rank]
+        files = [files[i] for i in mine]
+    for path in files:
+        if is_dir:
+            out = args.output / path.relative_to(root)
+        elif args.output.is_dir() or args.output.suffix == "":
+            out = args.output / path.name
+        else:
+            out = args.output
+        out.parent.mkdir(parents=True, exist_ok=True)
+        audio, fs = load_audio(path)
+        with torch.no_grad():
+            x = resample(audio.to(device), fs, model.fs)
+            enh = model.enhance(x, **enhance_kwargs)
+            enh = resample(enh, model.fs, fs)
+        save_audio(out, enh, fs)
+        print(f"[rank {rank}] {path} -> {out}", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

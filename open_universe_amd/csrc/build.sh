@@ -6,7 +6,7 @@ OUT="${1:-$HERE/../libouhip.so}"
 ARCH="${OUHIP_ARCH:-gfx950}"
 OBJDIR="$HERE/build${OUHIP_BUILD_TAG:-}"
 mkdir -p "$OBJDIR"
-SRCS="ou_conv.hip ou_gru.hip ou_misc.hip ou_program.hip"
+SRCS="ou_conv.hip ou_gru.hip ou_misc.hip ou_program.hip ou_audio.hip"
 pids=()
 for s in $SRCS; do
   /opt/rocm/bin/hipcc --offload-arch="$ARCH" -O3 -fPIC -std=c++17 -Wall -Wno-unused-function ${OUHIP_CFLAGS:-} \
