@@ -21,6 +21,65 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ou_rsrc(const void* p, long lo
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, n,
                                              0x00020000);
 }
+
+// LDS-DMA of one dword per lane: lane l's *src lands at dst + 4 l (dst is
+// wave-uniform).  Ordered for this wave's ds_reads only by a covering vmcnt:
+// OU_WAIT_VMCNT0.  Issued from inline asm on purpose: hipcc (ROCm 7.2) cannot
+// tell an LDS-DMA from the kernel's other LDS traffic and drains vmcnt(0)
+// before the next ds_read (here: the MFMA fragment reads right after the
+// prefetch), which would expose the DMA latency the prefetch exists to hide.
+// The asm is invisible to the compiler's counters, so a kernel using it must
+// not rely on compiler-inserted vmcnt waits for other vector loads issued
+// after it (the MFMA waves of conv_wkernel issue none).
+__device__ __forceinline__ void ou_glds4(const void* src, const void* lds_dst)
+{
+    const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(m0v)
+                 : "memory");
+}
+__device__ __forceinline__ void ou_glds16(const void* src, const void* lds_dst)
+{
+    const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)lds_dst);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(m0v)
+                 : "memory");
+}
+// Buffer-resource LDS-DMA (range-checked: an out-of-range voffset lands 0):
+// lane l's dword / 16 bytes at voff + soff land at LDS byte address
+// lds_addr + 4 l / 16 l.  soff and lds_addr are wave-uniform (SGPRs), so the
+// per-piece address arithmetic stays on the scalar unit.
+__device__ __forceinline__ void ou_blds4(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff, unsigned lds_addr)
+{
+    soff = __builtin_amdgcn_readfirstlane(soff);          // wave-uniform by contract
+    lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %3 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(rs), "s"(soff), "s"(lds_addr)
+                 : "memory");
+}
+__device__ __forceinline__ void ou_blds16(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff, unsigned lds_addr)
+{
+    soff = __builtin_amdgcn_readfirstlane(soff);          // wave-uniform by contract
+    lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(rs), "s"(soff), "s"(lds_addr)
+                 : "memory");
+}
+// LDS byte address of a pointer into the kernel's dynamic LDS (wave-uniform)
+typedef unsigned ou_ldsa_t;
+#define OU_LDS_ADDR(p) __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(const void*)(p))
+#define OU_GLDS4(src, dst) ou_glds4((const void*)(src), (const void*)(dst))
+#define OU_GLDS16(src, dst) ou_glds16((const void*)(src), (const void*)(dst))
+#define OU_WAIT_VMCNT0() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#define OU_WAIT_VMCNT(n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory")
 #endif
 
 // dynamic LDS of a kernel (tests/emu replaces it with a bounds-checked block)

@@ -92,10 +92,25 @@ __device__ uint64_t g_conv_stamps[kStampWGs * kStampPhases];
         if (threadIdx.x == 0 && wg_ < kStampWGs)                                               \
             for (int i_ = 0; i_ < kStampPhases; ++i_) g_conv_stamps[wg_ * kStampPhases + i_] = cst_[i_]; \
     } while (0)
+// warp-specialised kernel: MFMA wave 0 -> slots 0-7 (0 prefetch/setup, 1 MFMA,
+// 2 epilogue, 3 tick barrier, 4 first barrier, 6/7 start/end realtime), staging
+// wave 0 -> slots 8-15 (8 DMA issue, 9 vmcnt wait, 10 barrier, 14/15 realtime)
+#define OU_WSTAMP_INIT uint64_t wst_[8] = {}; uint64_t wtp_ = __builtin_amdgcn_s_memtime(); \
+    wst_[6] = __builtin_amdgcn_s_memrealtime();
+#define OU_WSTAMP(i) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); wst_[i] += n_ - wtp_; wtp_ = n_; } while (0)
+#define OU_WSTAMP_SAVE(cond, base)                                                              \
+    do {                                                                                        \
+        wst_[7] = __builtin_amdgcn_s_memrealtime();                                             \
+        if ((cond) && blockIdx.x < kStampWGs / 2)                                               \
+            for (int i_ = 0; i_ < 8; ++i_) g_conv_stamps[blockIdx.x * 16 + (base) + i_] = wst_[i_]; \
+    } while (0)
 #else
 #define OU_CSTAMP_INIT
 #define OU_CSTAMP(i) do { } while (0)
 #define OU_CSTAMP_SAVE do { } while (0)
+#define OU_WSTAMP_INIT
+#define OU_WSTAMP(i) do { } while (0)
+#define OU_WSTAMP_SAVE(cond, base) do { } while (0)
 #endif
 
 // LDS images of one K chunk (CC frame-view channels x KT taps):
@@ -338,8 +353,15 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)yrows * d.y_cstride * 4);
     const __amdgpu_buffer_rsrc_t r1s = ou_rsrc(d.res1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y, d.res1 ? (int64_t)yrows * d.r1_cstride * 4 : 0);
     const __amdgpu_buffer_rsrc_t r2s = ou_rsrc(d.res2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y, d.res2 ? (int64_t)yrows * d.r2_cstride * 4 : 0);
-    const float* fm = d.film ? d.film + (int64_t)b * d.film_bstride : nullptr;
-    const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr;
+    // absent operands get zero-size resources (their loads return 0): every
+    // load is unconditional -- a per-element `ptr ? load : default` makes hipcc
+    // branch around each load and drain vmcnt(0) per element
+    const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr, has_fm = d.film != nullptr;
+    // branch-free epilogue: an absent operand loads 0 and meets a unit scale
+    const float s1e = has_r1 ? d.s1 : 1.f, s2e = has_r2 ? d.s2 : 1.f, fadd = has_fm ? 0.f : 1.f;
+    const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
+    const __amdgpu_buffer_rsrc_t fs = ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y,
+                                              has_fm ? (int64_t)cout * 8 : 0);
 #pragma unroll
     for (int mr = 0; mr < MR; ++mr) {
         const int mt = mt0 + wm * MR + mr;
@@ -350,9 +372,9 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
             const int m = min(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
             ph[r] = rout > 1 ? m / cout : 0;
             co[r] = m - ph[r] * cout;
-            bias[r] = d.bias ? d.bias[co[r]] : 0.f;
-            fa[r] = fm ? fm[co[r]] : 1.f;
-            fb[r] = fm ? fm[cout + co[r]] : 0.f;
+            bias[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, co[r] * 4, 0, 0));
+            fa[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, co[r] * 4, 0, 0));
+            fb[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, (cout + co[r]) * 4, 0, 0));
         }
 #pragma unroll
         for (int nr = 0; nr < NR; ++nr) {
@@ -365,20 +387,18 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
                 const int t = u * rout + ph[r];
                 const bool ok = m < M && u < d.n_frames && t < ylen;
                 off[r] = ok ? t : -1;   // column; row offsets differ per tensor
-                v1[r] = has_r1 ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                     r1s, ok ? (co[r] * (int)d.r1_cstride + t) * 4 : kSentinel, 0, 0))
-                               : 0.f;
-                v2[r] = has_r2 ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                     r2s, ok ? (co[r] * (int)d.r2_cstride + t) * 4 : kSentinel, 0, 0))
-                               : 0.f;
+                v1[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    r1s, ok ? (co[r] * (int)d.r1_cstride + t) * 4 : kSentinel, 0, 0));
+                v2[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    r2s, ok ? (co[r] * (int)d.r2_cstride + t) * 4 : kSentinel, 0, 0));
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 float v = acc[mr][nr][r] + bias[r];
                 if (off[r] >= d.valid_len) v = 0.f;
-                if (has_r1) v = (v + v1[r]) * d.s1;
-                v = fa[r] * v + fb[r];
-                if (has_r2) v = (v + v2[r]) * d.s2;
+                v = (v + v1[r]) * s1e;
+                v = (fa[r] + fadd) * v + fb[r];
+                v = (v + v2[r]) * s2e;
                 __builtin_amdgcn_raw_buffer_store_b32(
                     __float_as_uint(v), ys, off[r] >= 0 ? (co[r] * (int)d.y_cstride + off[r]) * 4 : kSentinel, 0, 0);
             }
@@ -544,6 +564,7 @@ __global__ __launch_bounds__(256) void conv_pkernel(ou_conv_desc d, int nchunks,
         co = m - ph * cout;
     };
     // residual 1 and bias of a tile's epilogue, issued one chunk ahead
+    const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
     auto load_epilogue = [&](int tile) {
         OU_DECODE(tile, b, n0, mt0)
         const __amdgpu_buffer_rsrc_t r1s = ou_rsrc(has_r1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y,
@@ -555,7 +576,7 @@ __global__ __launch_bounds__(256) void conv_pkernel(ou_conv_desc d, int nchunks,
             for (int r = 0; r < 16; ++r) {
                 int co, ph;
                 row_of(mt, r, co, ph);
-                ebias[mr][r] = d.bias ? d.bias[co] : 0.f;
+                ebias[mr][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, co * 4, 0, 0));
                 const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
 #pragma unroll
                 for (int nr = 0; nr < NR; ++nr) {
@@ -629,7 +650,10 @@ __global__ __launch_bounds__(256) void conv_pkernel(ou_conv_desc d, int nchunks,
             const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)cout * d.y_cstride * 4);
             const __amdgpu_buffer_rsrc_t r2s = ou_rsrc(has_r2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y,
                                                        has_r2 ? (int64_t)cout * d.r2_cstride * 4 : 0);
-            const float* fm = d.film ? d.film + (int64_t)b * d.film_bstride : nullptr;
+            const bool has_fm = d.film != nullptr;
+            const float s1e = has_r1 ? d.s1 : 1.f, s2e = has_r2 ? d.s2 : 1.f, fadd = has_fm ? 0.f : 1.f;
+            const __amdgpu_buffer_rsrc_t fs = ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y,
+                                                      has_fm ? (int64_t)cout * 8 : 0);
 #pragma unroll
             for (int mr = 0; mr < MR; ++mr) {
                 const int mt = mt0 + wm * MR + mr;
@@ -655,9 +679,10 @@ __global__ __launch_bounds__(256) void conv_pkernel(ou_conv_desc d, int nchunks,
                         row_of(mt, r, co, ph);
                         float v = acc[mr][nr][r] + ebias[mr][r];
                         if (off[r] >= d.valid_len) v = 0.f;
-                        if (has_r1) v = (v + ev1[mr][nr][r]) * d.s1;
-                        if (fm) v = fm[co] * v + fm[cout + co];
-                        if (has_r2) v = (v + v2[r]) * d.s2;
+                        v = (v + ev1[mr][nr][r]) * s1e;
+                        v = (__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, co * 4, 0, 0)) + fadd) * v +
+                            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, (cout + co) * 4, 0, 0));
+                        v = (v + v2[r]) * s2e;
                         __builtin_amdgcn_raw_buffer_store_b32(
                             __float_as_uint(v), ys, off[r] >= 0 ? (co * (int)d.y_cstride + off[r]) * 4 : kSentinel,
                             0, 0);
@@ -670,6 +695,380 @@ __global__ __launch_bounds__(256) void conv_pkernel(ou_conv_desc d, int nchunks,
         if (tile >= ntiles) break;
     }
 #undef OU_DECODE
+}
+
+// ---------------------------------------------------------------------------
+// Warp-specialised persistent variant (tile bit 10): 512 threads = 4 MFMA
+// waves (WM x WN x WK) + 4 staging waves, one of each per SIMD.  The MFMA
+// waves only read LDS, issue MFMAs and write their accumulators back to LDS;
+// every global memory access belongs to the staging waves.
+//
+// Staging waves, per K chunk t ("tick", one workgroup barrier each):
+//   1. LDS-DMA (buffer_load ... lds) of chunk t + 2 into a 3-stage ring: the X
+//      window as [channel][frame] rows (64-frame dword pieces, coalesced) and
+//      the chunk's packed weights (16-B pieces, lane-linear);
+//   2. when chunk t is a tile's last: LDS-DMA of that tile's residual in
+//      row-major 16-B groups, each lane the groups it will itself finish;
+//   3. vmcnt: chunk t + 1 and the residual have landed (chunk t + 2 stays in
+//      flight across the barrier);
+//   4. PReLU(x * in_scale) in place on the X rows the wave DMA'd itself;
+//   5. the epilogue of the tile whose last chunk the MFMA waves finished in the
+//      previous tick: accumulator image (+ split-K partials, fixed order)
+//      + bias, zero past valid_len, residual 1, FiLM (bias / gamma / beta by
+//      scalar loads), residual 2 -> buffer_store_dwordx4.
+// A workgroup walks output tiles blockIdx.x, +gridDim.x, ... and its chunk
+// stream runs across tile boundaries, so staging, MFMA and the stores of
+// consecutive tiles overlap.  Tiles of one K chunk are refused (host): the
+// single accumulator image needs a tick between two tiles' last chunks.
+//
+// LDS: ring of 3 stages {X [CC][SW] (SW = 64 NI + 32: channels 2p and 2p+1 in
+// opposite bank halves), A [AG float4]}, the accumulator image
+// [WK][BM][BN + 8] (+8: conflict-free MFMA-order writes), the residual tile
+// [BM][BN].  B fragment of k-step (pair p, tap k): lane l reads
+// X[2p + l/32][n + l%32 + k].
+// ---------------------------------------------------------------------------
+template <int KT, int CC, int WM, int WN, int WK, int MR, int NR, int S>
+struct WCfg {
+    static constexpr int BM = 32 * WM * MR;
+    static constexpr int BN = 32 * NR * WN;
+    static constexpr int W = BN + KT - 1;                 // frames per chunk row
+    static constexpr int NI = (W + 63) / 64;              // 64-frame DMA pieces per row
+    static constexpr int SW = 64 * NI + 32;               // row stride (floats)
+    static constexpr int XBUF = CC * SW;
+    static constexpr int HQ = CC / 8;                     // 4-pair groups per chunk
+    static constexpr int CPW = HQ / WK;                   // ... per MFMA wave
+    static constexpr int AG = WM * MR * HQ * KT * 64;     // float4 of weights per chunk
+    static constexpr int STAGE = XBUF + AG * 4;           // floats
+    static constexpr int XPW = (CC / 4) * NI;             // X pieces per staging wave per chunk
+    static constexpr int APW = (AG / 64 + 3) / 4;         // A pieces per staging wave per chunk
+    static constexpr int NPI = XPW + APW;                 // DMAs per staging wave per chunk
+    static constexpr int OS = BN + 8;                     // accumulator image row stride
+    static constexpr int OUT = S * STAGE;                 // accumulator image offset
+    static constexpr int RES = OUT + WK * BM * OS;        // residual tile offset
+    static constexpr int DUMMY = RES + BM * BN;           // sink of padding A pieces (never read)
+    static constexpr int LDS = DUMMY + 256;               // floats
+    static constexpr int G4 = BM * BN / 4;                // 16-B epilogue groups per tile
+    static constexpr int GPT = G4 / 256;                  // ... per staging thread
+    static constexpr int RPP = 256 / BN;                  // rows per 64-group piece
+    static_assert(G4 % 256 == 0 && 256 % BN == 0 && BN % 4 == 0, "epilogue group mapping");
+};
+
+template <int KT, int CC, int WM, int WN, int WK, int MR, int NR, int S>
+__global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks, int mtiles,
+                                                    int64_t a_mt_stride, int ntn, int mgroups, int ntiles)
+{
+    using WC = WCfg<KT, CC, WM, WN, WK, MR, NR, S>;
+    static_assert(CC % 8 == 0 && WC::HQ % WK == 0, "chunk must split into 4-pair groups per wave");
+    static_assert(WM * WN * WK == 4, "4 MFMA waves");
+    static_assert(S == 3, "3-stage ring (DMA two chunks ahead)");
+    static_assert(WC::NPI <= 63, "vmcnt range");
+    OU_DYNAMIC_LDS(float4, lds4);
+    float* lds = (float*)lds4;
+
+    const int bx = (int)blockIdx.x, gx = (int)gridDim.x;
+    const int nt_wg = bx < ntiles ? (ntiles - 1 - bx) / gx + 1 : 0;
+    const int items = nt_wg * nchunks;   // (tile, chunk) work items of this workgroup
+    const int M = d.m;
+
+    // tile i of this workgroup -> (batch item, first frame, first m-tile)
+    auto decode = [&](int i, int& b, int& n0, int& mt0) {
+        const int tile = bx + i * gx;
+        b = tile / (ntn * mgroups);
+        const int r = tile - b * (ntn * mgroups);
+        mt0 = (r / ntn) * (WM * MR);
+        n0 = (r - (r / ntn) * ntn) * WC::BN;
+    };
+
+    if (threadIdx.x >= 256) {
+        // ======================= staging waves ==============================
+        const int tid = threadIdx.x - 256;
+        const int lane = tid & 63;
+        const int sw = __builtin_amdgcn_readfirstlane(tid >> 6);   // X rows [sw CC/4, (sw+1) CC/4)
+        const int R = d.frame;
+        const int cin = d.cin;
+        const int in_len = d.in_len;
+        const int xc = (int)d.x_cstride;
+        const float slope = d.slope;
+        const ou_ldsa_t lds0 = OU_LDS_ADDR(lds);
+        const __amdgpu_buffer_rsrc_t wrs = ou_rsrc(d.w, (int64_t)mtiles * a_mt_stride * 4);
+        const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr, has_fm = d.film != nullptr;
+        const float s1e = has_r1 ? d.s1 : 1.f, s2e = has_r2 ? d.s2 : 1.f, fadd = has_fm ? 0.f : 1.f;
+        const int ulim = min(d.n_frames, d.out_len);
+        const int r1c = (int)d.r1_cstride, r2c = (int)d.r2_cstride, yc = (int)d.y_cstride;
+
+        auto issue_item = [&](int t) {
+            const int i = t / nchunks;
+            const int q = t - i * nchunks;
+            int b, n0, mt0;
+            decode(i, b, n0, mt0);
+            const ou_ldsa_t st = lds0 + (unsigned)((t % S) * WC::STAGE * 4);
+            const __amdgpu_buffer_rsrc_t xrs = ou_rsrc(d.x + (int64_t)b * d.x_bstride, (int64_t)cin * xc * 4);
+            int fw[WC::NI];   // lane sample of each 64-frame piece (frame f -> sample f R + ph + shift)
+#pragma unroll
+            for (int pi = 0; pi < WC::NI; ++pi) fw[pi] = (n0 - d.pad + pi * 64 + lane) * R + d.shift;
+            const int cq0 = q * CC + sw * (CC / 4);
+            int ph = cq0 / cin;
+            int ci = cq0 - ph * cin;
+#pragma unroll
+            for (int c = 0; c < CC / 4; ++c) {
+                const bool chan_ok = ph < R;
+                const unsigned soff = (unsigned)(chan_ok ? ci : 0) * (unsigned)xc * 4u;
+                const ou_ldsa_t row = st + (unsigned)((sw * (CC / 4) + c) * WC::SW * 4);
+#pragma unroll
+                for (int pi = 0; pi < WC::NI; ++pi) {
+                    const int pos = fw[pi] + ph;
+                    const bool ok = chan_ok & ((unsigned)pos < (unsigned)in_len);
+                    ou_blds4(xrs, ok ? (unsigned)pos * 4u : (unsigned)kSentinel, soff, row + pi * 256);
+                }
+                if (++ci == cin) { ci = 0; ++ph; }
+            }
+            const unsigned wbase = (unsigned)((mt0 * a_mt_stride + (int64_t)q * (WC::HQ * KT * 256)) * 4);
+#pragma unroll
+            for (int jj = 0; jj < WC::APW; ++jj) {
+                const int j = sw * WC::APW + jj;            // piece = 64 float4
+                if (j * 64 < WC::AG) {
+                    const int ml = j / (WC::HQ * KT);        // m-tile of the piece
+                    const unsigned soff = wbase + (unsigned)(ml * a_mt_stride * 4) +
+                                          (unsigned)((j - ml * (WC::HQ * KT)) * 1024);
+                    ou_blds16(wrs, mt0 + ml < mtiles ? (unsigned)lane * 16u : (unsigned)kSentinel, soff,
+                              st + (unsigned)((WC::XBUF + j * 256) * 4));
+                } else {   // same DMA count in every staging wave
+                    ou_blds16(wrs, (unsigned)kSentinel, 0u, lds0 + (unsigned)(WC::DUMMY * 4));
+                }
+            }
+        };
+        // epilogue group k of this thread: piece (sw + 4 k) of the row-major tile, lane's group in it
+        auto group_of = [&](int k, int& row, int& c4) {
+            const int g = (sw + 4 * k) * 64 + lane;
+            row = g / (WC::BN / 4);
+            c4 = g - row * (WC::BN / 4);
+        };
+        // residual 1 of tile i: full groups by LDS-DMA into this lane's slots of the residual tile
+        auto issue_res = [&](int i) {
+            int b, n0, mt0;
+            decode(i, b, n0, mt0);
+            const __amdgpu_buffer_rsrc_t r1s = ou_rsrc(has_r1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y,
+                                                       has_r1 ? (int64_t)M * r1c * 4 : 0);
+#pragma unroll
+            for (int k = 0; k < WC::GPT; ++k) {
+                int row, c4;
+                group_of(k, row, c4);
+                const int m = mt0 * 32 + row, u = n0 + 4 * c4;
+                const bool full = (int)(m < M) & (int)(u + 3 < ulim);
+                ou_blds16(r1s, full ? (unsigned)(m * r1c + u) * 4u : (unsigned)kSentinel, 0u,
+                          lds0 + (unsigned)((WC::RES + (sw + 4 * k) * 256) * 4));
+            }
+        };
+        // PReLU(x * in_scale) in place on this wave's X rows of item t
+        auto prelu_item = [&](int t) {
+            const int i = t / nchunks;
+            int b, n0, mt0;
+            decode(i, b, n0, mt0);
+            const float sc = d.in_scale ? d.in_scale[b] : 1.0f;
+            float4* xs = (float4*)(lds + (t % S) * WC::STAGE + sw * (CC / 4) * WC::SW);
+            constexpr int N4 = (CC / 4) * WC::SW / 4;
+#pragma unroll
+            for (int k = 0; k < (N4 + 63) / 64; ++k) {
+                const int f = lane + 64 * k;
+                if (N4 % 64 == 0 || f < N4) {
+                    float4 v = xs[f];
+                    v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
+                    v.x = v.x >= 0.f ? v.x : v.x * slope;
+                    v.y = v.y >= 0.f ? v.y : v.y * slope;
+                    v.z = v.z >= 0.f ? v.z : v.z * slope;
+                    v.w = v.w >= 0.f ? v.w : v.w * slope;
+                    xs[f] = v;
+                }
+            }
+        };
+        auto epilogue = [&](int i) {
+            int b, n0, mt0;
+            decode(i, b, n0, mt0);
+            const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)M * yc * 4);
+            const __amdgpu_buffer_rsrc_t r1s = ou_rsrc(has_r1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y,
+                                                       has_r1 ? (int64_t)M * r1c * 4 : 0);
+            const __amdgpu_buffer_rsrc_t r2s = ou_rsrc(has_r2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y,
+                                                       has_r2 ? (int64_t)M * r2c * 4 : 0);
+            const float* fmb = has_fm ? d.film + (int64_t)b * d.film_bstride : nullptr;
+            const float* out = lds + WC::OUT;
+#pragma unroll
+            for (int k = 0; k < WC::GPT; ++k) {
+                int row, c4;
+                group_of(k, row, c4);
+                const int m = mt0 * 32 + row, u = n0 + 4 * c4;
+                const bool mok = m < M;
+                const bool full = mok & (u + 3 < ulim);
+                // per-row operands by scalar loads: the piece spans rows
+                // row0 .. row0 + RPP - 1 (wave-uniform row0)
+                const int row0 = ((sw + 4 * k) * 64) / (WC::BN / 4);
+                float pb = 0.f, pa = 0.f, pf = 0.f;
+#pragma unroll
+                for (int rr = 0; rr < WC::RPP; ++rr) {
+                    const int mm = min(mt0 * 32 + row0 + rr, M - 1);
+                    const float bb = d.bias ? d.bias[mm] : 0.f;
+                    const float aa = fmb ? fmb[mm] : 0.f;
+                    const float ff = fmb ? fmb[M + mm] : 0.f;
+                    if (row == row0 + rr) { pb = bb; pa = aa; pf = ff; }
+                }
+                float4 a = *(const float4*)(out + row * WC::OS + 4 * c4);
+#pragma unroll
+                for (int j = 1; j < WK; ++j) {   // split-K partials, fixed order
+                    const float4 p = *(const float4*)(out + (j * WC::BM + row) * WC::OS + 4 * c4);
+                    a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
+                }
+                float4 r1 = *(const float4*)(lds + WC::RES + ((sw + 4 * k) * 64 + lane) * 4);
+                float r2v[4] = {0.f, 0.f, 0.f, 0.f};
+                if (!full) {   // tile edge: per-element residual 1 (the DMA skipped the group)
+                    float t1[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        t1[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                            r1s, (mok & (u + e < ulim)) ? (m * r1c + u + e) * 4 : kSentinel, 0, 0));
+                    r1 = make_float4(t1[0], t1[1], t1[2], t1[3]);
+                }
+                if (has_r2) {   // rare: plain loads
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        r2v[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                            r2s, (mok & (u + e < ulim)) ? (m * r2c + u + e) * 4 : kSentinel, 0, 0));
+                }
+                float v[4] = {a.x, a.y, a.z, a.w};
+                const float r1v[4] = {r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float x = v[e] + pb;
+                    if (u + e >= d.valid_len) x = 0.f;
+                    x = (x + r1v[e]) * s1e;
+                    x = (pa + fadd) * x + pf;
+                    x = (x + r2v[e]) * s2e;
+                    v[e] = x;
+                }
+                if (full) {
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        (__attribute__((ext_vector_type(4))) unsigned){__float_as_uint(v[0]), __float_as_uint(v[1]),
+                                                                        __float_as_uint(v[2]), __float_as_uint(v[3])},
+                        ys, (m * yc + u) * 4, 0, 0);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        __builtin_amdgcn_raw_buffer_store_b32(
+                            __float_as_uint(v[e]), ys, (mok & (u + e < ulim)) ? (m * yc + u + e) * 4 : kSentinel, 0, 0);
+                }
+            }
+        };
+
+        // prologue: chunks 0, 1 in flight; chunk 0 landed and activated
+        OU_WSTAMP_INIT
+        for (int t = 0; t < 2 && t < items; ++t) issue_item(t);
+        if (items >= 2) OU_WAIT_VMCNT(WC::NPI);
+        else OU_WAIT_VMCNT0();
+        if (items > 0) prelu_item(0);
+        __syncthreads();
+        for (int t = 0; t < items; ++t) {
+            const int q = t % nchunks;
+            // the tile the MFMA waves finished last tick (its image is complete)
+            const int fin = (t > 0 && q == 0) ? t / nchunks - 1 : -1;
+            OU_WSTAMP(5);
+            if (t + 2 < items) issue_item(t + 2);
+            OU_WSTAMP(0);
+            // chunk t + 1 (and everything older) landed; chunk t + 2 stays in flight
+            if (t + 2 < items) OU_WAIT_VMCNT(WC::NPI);
+            else OU_WAIT_VMCNT0();
+            OU_WSTAMP(1);
+            if (t + 1 < items) prelu_item(t + 1);
+            OU_WSTAMP(3);
+            if (fin >= 0) epilogue(fin);
+            OU_WSTAMP(4);
+            if (q == nchunks - 1) {
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this lane's RES reads are done
+                issue_res(t / nchunks);
+            }
+            OU_WSTAMP(5);
+            __syncthreads();
+            OU_WSTAMP(2);
+        }
+        // the last tile: its chunk finished before the final barrier
+        if (items > 0) {
+            OU_WAIT_VMCNT0();
+            epilogue(items / nchunks - 1);
+        }
+        OU_WSTAMP(4);
+        OU_WSTAMP_SAVE(threadIdx.x == 256, 8);
+        return;
+    }
+
+    // ========================= MFMA waves ===================================
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wave % WN;
+    const int wm = (wave / WN) % WM;
+    const int wk = wave / (WN * WM);
+    const int h = lane >> 5;
+    const int l32 = lane & 31;
+
+    floatx16 acc[MR][NR];
+    OU_WSTAMP_INIT
+    __syncthreads();
+    OU_WSTAMP(4);
+    for (int t = 0; t < items; ++t) {
+        const int q = t % nchunks;
+        if (q == 0) {
+#pragma unroll
+            for (int a = 0; a < MR; ++a)
+#pragma unroll
+                for (int c = 0; c < NR; ++c)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[a][c][r] = 0.f;
+        }
+        {
+            const float* xs = lds + (t % S) * WC::STAGE;
+            const float4* ap = (const float4*)(xs + WC::XBUF) + ((wm * MR) * WC::HQ + wk * WC::CPW) * KT * 64 + lane;
+            // lane's B column: row 2p + h, frame wn*32*NR + nr*32 + l32 + tap
+            const float* xp = xs + (8 * wk * WC::CPW + h) * WC::SW + wn * 32 * NR + l32;
+            constexpr int NS = WC::CPW * KT;
+            float4 fa[2][MR];
+            float fb[2][4][NR];
+            auto frag = [&](int st, float4* a, float (*bq)[NR]) {
+                const int cpq = st / KT, k = st - (st / KT) * KT;
+#pragma unroll
+                for (int mr = 0; mr < MR; ++mr) a[mr] = ap[((mr * WC::HQ + cpq) * KT + k) * 64];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int nr = 0; nr < NR; ++nr) bq[j][nr] = xp[(2 * (4 * cpq + j)) * WC::SW + nr * 32 + k];
+            };
+            frag(0, fa[0], fb[0]);
+#pragma unroll
+            for (int st = 0; st < NS; ++st) {
+                if (st + 1 < NS) frag(st + 1, fa[(st + 1) & 1], fb[(st + 1) & 1]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                        for (int nr = 0; nr < NR; ++nr)
+                            acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                                fa[st & 1][mr][j], fb[st & 1][j][nr], acc[mr][nr], 0, 0, 0);
+            }
+        }
+        OU_WSTAMP(1);
+        if (q == nchunks - 1) {   // accumulator image: [wk][row][col]
+            float* out = lds + WC::OUT + wk * WC::BM * WC::OS;
+#pragma unroll
+            for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        out[((wm * MR + mr) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * WC::OS + wn * 32 * NR + nr * 32 +
+                            l32] = acc[mr][nr][r];
+        }
+        OU_WSTAMP(2);
+        __syncthreads();
+        OU_WSTAMP(3);
+    }
+    OU_WSTAMP_SAVE(threadIdx.x == 0, 0);
 }
 
 // ---- tile table ------------------------------------------------------------
@@ -689,7 +1088,7 @@ struct Tile {
 #define OU_TILE_ENTRY(id, wm, wn, wk, mr, nr, big) {wm, wn, wk, mr, nr, big},
 constexpr Tile kTiles[] = {OU_TILES(OU_TILE_ENTRY)};
 #undef OU_TILE_ENTRY
-constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
+[[maybe_unused]] constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
 constexpr int kMaxLds = 160 * 1024;     // gfx950: 160 KiB per CU
 constexpr int kLdsTwoPerCu = 80 * 1024; // fits two workgroups per CU
@@ -780,10 +1179,83 @@ int launch_p(const ou_conv_desc& d, int tpw, hipStream_t s)
     }
 }
 
+// warp-specialised kernel: the largest channel chunk whose S-stage ring (+
+// split-K area) fits one workgroup per CU
+constexpr int kWStages = 3;
+template <int KT, int WM, int WN, int WK, int MR, int NR, int CC>
+constexpr bool wchunk_ok()
+{
+    return CC / 8 % WK == 0 && WCfg<KT, CC, WM, WN, WK, MR, NR, kWStages>::LDS * 4 <= kMaxLds;
+}
+template <int KT, int WM, int WN, int WK, int MR, int NR>
+constexpr int wchunk_for()
+{
+    return wchunk_ok<KT, WM, WN, WK, MR, NR, 64>()   ? 64
+           : wchunk_ok<KT, WM, WN, WK, MR, NR, 32>() ? 32
+           : wchunk_ok<KT, WM, WN, WK, MR, NR, 16>() ? 16
+                                                     : 8 * WK;
+}
+template <int KT, int WM, int WN, int WK, int MR, int NR>
+constexpr int wlds_bytes_t()
+{
+    return WCfg<KT, wchunk_for<KT, WM, WN, WK, MR, NR>(), WM, WN, WK, MR, NR, kWStages>::LDS * 4;
+}
+
+int g_num_cus = 0;   // device CU count, queried once
+
+template <int KT, int WM, int WN, int WK, int MR, int NR>
+int launch_w(const ou_conv_desc& d, hipStream_t s)
+{
+    constexpr int CC = wchunk_for<KT, WM, WN, WK, MR, NR>();
+    using C = WCfg<KT, CC, WM, WN, WK, MR, NR, kWStages>;
+    constexpr int lds = C::LDS * 4;
+    const int mtiles = (d.m + 31) / 32;
+    const int cin_eff = d.cin * d.frame;
+    const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
+    const int nchunks = (cin_eff + CC - 1) / CC;
+    if (nchunks < 2)   // one accumulator image: two tiles' last chunks must be a tick apart
+        return ou_fail(-2, "conv: warp-specialised tile needs >= 2 K chunks (cin_eff %d, chunk %d)", cin_eff, CC);
+    const int64_t a_mt_stride = (int64_t)cin_pad * KT * 32;
+    const int ntn = (d.n_frames + C::BN - 1) / C::BN;
+    const int mgroups = (mtiles + WM * MR - 1) / (WM * MR);
+    const int ntiles = ntn * mgroups * d.batch;
+    auto kern = conv_wkernel<KT, CC, WM, WN, WK, MR, NR, kWStages>;
+    static bool attr = false;
+    static int per_cu = 1;
+    if (!attr) {
+        if (lds > 64 * 1024)
+            OU_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds),
+                         "conv: LDS attribute");
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 512, lds) == hipSuccess && n > 0) per_cu = n;
+        attr = true;
+    }
+    if (g_num_cus <= 0) {
+        int dev = 0;
+        OU_HIP_CHECK(hipGetDevice(&dev), "conv: device");
+        OU_HIP_CHECK(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev), "conv: CUs");
+        if (g_num_cus <= 0) g_num_cus = 1;
+    }
+    const int grid = std::min(ntiles, per_cu * g_num_cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, d, nchunks, mtiles, a_mt_stride, ntn, mgroups, ntiles);
+    return ou_check_launch("conv");
+}
+
+constexpr int kWsBit = 1 << 10;   // tile bit: warp-specialised persistent kernel
+
 template <int KT>
 int lds_bytes_kt(int tile)
 {
-    switch (tile) {
+    if (tile & kWsBit) {
+        switch (tile & 0xff) {
+#define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) \
+    case id: return big ? -1 : wlds_bytes_t<KT, wm, wn, wk, mr, nr>();
+            OU_TILES(OU_TILE_CASE)
+#undef OU_TILE_CASE
+        }
+        return -1;
+    }
+    switch (tile & 0xff) {
 #define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) case id: return lds_bytes_t<KT, wm, wn, wk, mr, nr, big>();
         OU_TILES(OU_TILE_CASE)
 #undef OU_TILE_CASE
@@ -791,20 +1263,21 @@ int lds_bytes_kt(int tile)
     return -1;
 }
 
-int lds_bytes(int kt, int tile)
-{
-    switch (kt) {
-    case 1: return lds_bytes_kt<1>(tile);
-    case 3: return lds_bytes_kt<3>(tile);
-    case 4: return lds_bytes_kt<4>(tile);
-    case 5: return lds_bytes_kt<5>(tile);
-    }
-    return -1;
-}
 
 template <int KT>
-int launch_kt(const ou_conv_desc& d, int tile, int tpw, hipStream_t s)
+int launch_kt(const ou_conv_desc& d, int tile, int tpw, bool ws, hipStream_t s)
 {
+    if (ws) {
+        switch (tile) {
+#define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) \
+    case id:                                      \
+        if constexpr (!big) return launch_w<KT, wm, wn, wk, mr, nr>(d, s); \
+        else return ou_fail(-2, "conv: tile %d has no warp-specialised form", tile);
+            OU_TILES(OU_TILE_CASE)
+#undef OU_TILE_CASE
+        }
+        return ou_fail(-2, "conv: bad warp-specialised tile %d", tile);
+    }
     switch (tile) {
 #define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big)                                              \
     case id:                                                                                   \
@@ -838,6 +1311,46 @@ int pick_tile(const ou_conv_desc& d)
     return 9;
 }
 
+}  // namespace
+
+// ---- translation-unit split (build speed) -----------------------------------
+// The build compiles this file once per tap count with -DOU_CONV_SPLIT_KT=K
+// (kernels and launchers for that K only, exported as ou_conv_launch_ktK /
+// ou_conv_lds_ktK) and once with -DOU_CONV_SPLIT_MAIN (the C ABI below, no
+// kernels).  Without either macro (tests/emu) everything is one unit.
+#define OU_CAT2(a, b) a##b
+#define OU_CAT(a, b) OU_CAT2(a, b)
+#if defined(OU_CONV_SPLIT_KT)
+int OU_CAT(ou_conv_launch_kt, OU_CONV_SPLIT_KT)(const ou_conv_desc& d, int tile, int tpw, bool ws, hipStream_t s)
+{
+    return launch_kt<OU_CONV_SPLIT_KT>(d, tile, tpw, ws, s);
+}
+int OU_CAT(ou_conv_lds_kt, OU_CONV_SPLIT_KT)(int tile) { return lds_bytes_kt<OU_CONV_SPLIT_KT>(tile); }
+#elif defined(OU_CONV_SPLIT_MAIN)
+#define OU_KT_DECL(K)                                                                           \
+    int ou_conv_launch_kt##K(const ou_conv_desc& d, int tile, int tpw, bool ws, hipStream_t s); \
+    int ou_conv_lds_kt##K(int tile);
+OU_KT_DECL(1) OU_KT_DECL(3) OU_KT_DECL(4) OU_KT_DECL(5)
+#undef OU_KT_DECL
+#define OU_LAUNCH_KT(K, ...) ou_conv_launch_kt##K(__VA_ARGS__)
+#define OU_LDS_KT(K, tile) ou_conv_lds_kt##K(tile)
+#else
+#define OU_LAUNCH_KT(K, ...) launch_kt<K>(__VA_ARGS__)
+#define OU_LDS_KT(K, tile) lds_bytes_kt<K>(tile)
+#endif
+
+#if !defined(OU_CONV_SPLIT_KT)
+namespace {
+int lds_bytes(int kt, int tile)
+{
+    switch (kt) {
+    case 1: return OU_LDS_KT(1, tile);
+    case 3: return OU_LDS_KT(3, tile);
+    case 4: return OU_LDS_KT(4, tile);
+    case 5: return OU_LDS_KT(5, tile);
+    }
+    return -1;
+}
 }  // namespace
 
 extern "C" int ou_conv_chunk(int kt, int frame)
@@ -886,17 +1399,21 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
         d.frame <= 0 || d.rout <= 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0)
         return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d frame=%d)", d.m, d.rout, d.frame);
     // d.tile: bits 0-7 tile shape (kTiles), bits 8-9 log2(output tiles per
-    // workgroup: > 1 selects the persistent kernel, shapes without split-K)
+    // workgroup: > 1 selects the persistent kernel, shapes without split-K),
+    // bit 10 the warp-specialised persistent kernel (shapes 0-12)
     const int tile = d.tile >= 0 && (d.tile & 0xff) < kNumTiles ? (d.tile & 0xff) : pick_tile(d);
-    const int tpw = d.tile >= 0 ? 1 << ((d.tile >> 8) & 3) : 1;
-    if (lds_bytes(d.kt, tile) > kMaxLds)
-        return ou_fail(-2, "conv: tile %d needs %d B of LDS for kt=%d", tile, lds_bytes(d.kt, tile), d.kt);
+    const bool ws = d.tile >= 0 && (d.tile & kWsBit);
+    const int tpw = d.tile >= 0 && !ws ? 1 << ((d.tile >> 8) & 3) : 1;
+    if (ws && d.rout != 1) return ou_fail(-2, "conv: the warp-specialised kernel has no transposed (rout %d) form", d.rout);
+    const int lb = lds_bytes(d.kt, tile | (ws ? kWsBit : 0));
+    if (lb <= 0 || lb > kMaxLds)
+        return ou_fail(-2, "conv: tile %d (ws %d) needs %d B of LDS for kt=%d", tile, (int)ws, lb, d.kt);
     hipStream_t s = (hipStream_t)stream;
     switch (d.kt) {
-    case 1: return launch_kt<1>(d, tile, tpw, s);
-    case 3: return launch_kt<3>(d, tile, tpw, s);
-    case 4: return launch_kt<4>(d, tile, tpw, s);
-    case 5: return launch_kt<5>(d, tile, tpw, s);
+    case 1: return OU_LAUNCH_KT(1, d, tile, tpw, ws, s);
+    case 3: return OU_LAUNCH_KT(3, d, tile, tpw, ws, s);
+    case 4: return OU_LAUNCH_KT(4, d, tile, tpw, ws, s);
+    case 5: return OU_LAUNCH_KT(5, d, tile, tpw, ws, s);
     }
     return ou_fail(-1, "conv: unsupported kt %d", d.kt);
 }
@@ -912,7 +1429,7 @@ extern "C" int ou_conv_read_stamps(uint64_t* host, int n)
 // per-workgroup LDS limit (diagnostics: tools/conv_bench.py --info)
 extern "C" int ou_conv_lds_info(int kt, int tile, int* lds_request, int* device_optin_max)
 {
-    if (lds_request) *lds_request = lds_bytes(kt, tile & 0xff);
+    if (lds_request) *lds_request = lds_bytes(kt, tile & (0xff | kWsBit));
     int dev = 0, v = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess) return -1;
@@ -924,6 +1441,13 @@ extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile(*
 extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int ou_conv_tile_ok(int kt, int tile)
 {
+    if (tile & kWsBit) {   // warp-specialised: shapes without the 'big' chunking, no tpw bits
+        if (tile & ~(kWsBit | 0xff)) return 0;
+        const int t = tile & 0xff;
+        if (t >= kNumTiles || kTiles[t].big) return 0;
+        const int lb = lds_bytes(kt, tile);
+        return lb > 0 && lb <= kMaxLds;
+    }
     if ((tile >> 8) & 3) {   // persistent: shapes without split-K only
         const int t = tile & 0xff;
         if (t >= kNumTiles || kTiles[t].wk != 1) return 0;
@@ -931,3 +1455,4 @@ extern "C" int ou_conv_tile_ok(int kt, int tile)
     tile &= 0xff;
     return tile >= 0 && tile < kNumTiles && lds_bytes(kt, tile) > 0 && lds_bytes(kt, tile) <= kMaxLds;
 }
+#endif  // !OU_CONV_SPLIT_KT

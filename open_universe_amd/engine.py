@@ -369,15 +369,16 @@ class ConvTuner:
         stream = torch.cuda.current_stream().cuda_stream
         best, best_ms = -1, float("inf")
         # tile shape x log2(output tiles per workgroup); > 0 = persistent kernel
-        cands = [t | (tpw << 8) for t in range(lib.ou_conv_num_tiles()) for tpw in (0, 1, 2)
-                 if lib.ou_conv_tile_ok(d.kt, t | (tpw << 8))]
+        # (bit 10: the warp-specialised persistent kernel)
+        cands = [t | v for t in range(lib.ou_conv_num_tiles()) for v in (0, 1 << 8, 2 << 8, 1 << 10)
+                 if lib.ou_conv_tile_ok(d.kt, t | v)]
         log = os.environ.get("OUHIP_TUNE_LOG")
         for t in cands:
             d.tile = t
             if log:   # diagnostics: name every candidate before it runs
                 with open(log, "a") as fh:
                     fh.write(f"m={d.m} cin={d.cin} frame={d.frame} kt={d.kt} n={d.n_frames} b={d.batch} "
-                             f"rout={d.rout} res1={bool(d.res1)} tile={t & 0xff} tpw={1 << (t >> 8)}\n")
+                             f"rout={d.rout} res1={bool(d.res1)} tile={t & 0xff} tpw={1 << ((t >> 8) & 3)} ws={t >> 10}\n")
                     fh.flush()
                     os.fsync(fh.fileno())
             if lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream)) != 0:

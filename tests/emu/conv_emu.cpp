@@ -73,10 +73,12 @@ int main(int argc, char** argv)
         const Geom& g = geoms[gi];
         for (int t = 0; t < ou_conv_num_tiles(); ++t) {
             if (!ou_conv_tile_ok(g.kt, t)) continue;
-            for (int tpw = 0; tpw < 3; ++tpw) {
-                if (!ou_conv_tile_ok(g.kt, t | (tpw << 8))) continue;
+            for (int tpw = 0; tpw < 4; ++tpw) {
+                if (tpw == 3 && g.rout != 1) continue;   // warp-specialised: plain convs only
+                if (!ou_conv_tile_ok(g.kt, t | (tpw == 3 ? 1024 : tpw << 8))) continue;
                 if (std::getenv("OUHIP_EMU_VERBOSE")) std::fprintf(stderr, "geom %d tile %d tpw %d\n", gi, t, tpw);
-                const int rc = run(g, t | (tpw << 8));
+                const int rc = run(g, t | (tpw == 3 ? 1024 : tpw << 8));
+                if (rc == -2 && tpw == 3) continue;   // warp-specialised form refused for this geometry
                 if (rc != 0) {
                     std::fprintf(stderr, "geom %d tile %d tpw %d: ou_conv returned %d\n", gi, t, tpw, rc);
                     return 2;

@@ -51,13 +51,16 @@ int main(int argc, char** argv)
         if (std::getenv("OUHIP_EMU_FRAMED") && d.frame == 1) continue;
         for (int t = 0; t < ou_conv_num_tiles(); ++t) {
             if (!ou_conv_tile_ok(d.kt, t)) continue;
-            for (int tpw = 0; tpw < 3; ++tpw) {
-                if (!ou_conv_tile_ok(d.kt, t | (tpw << 8))) continue;
+            for (int tpw = 0; tpw < 4; ++tpw) {
+                if (tpw == 3 && d.rout != 1) continue;   // warp-specialised: plain convs only
+                if (!ou_conv_tile_ok(d.kt, t | (tpw == 3 ? 1024 : tpw << 8))) continue;
                 if (std::getenv("OUHIP_EMU_VERBOSE"))
                     std::fprintf(stderr, "conv %zu (m %d cin %d frame %d kt %d n %d rout %d) tile %d tpw %d\n", ci, d.m,
                                  d.cin, d.frame, d.kt, d.n_frames, d.rout, t, tpw);
-                d.tile = t | (tpw << 8);
-                if (ou_conv(&d, nullptr) != 0) {
+                d.tile = t | (tpw == 3 ? 1024 : tpw << 8);
+                const int rc_ = ou_conv(&d, nullptr);
+                if (rc_ == -2 && tpw == 3) continue;   // warp-specialised form refused for this geometry
+                if (rc_ != 0) {
                     std::fprintf(stderr, "conv %zu tile %d: error %s\n", ci, t, ouhip_detail::err_buf());
                     return 3;
                 }

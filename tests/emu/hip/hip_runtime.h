@@ -47,9 +47,11 @@ inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4); retu
 inline uint32_t __float_as_uint(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 #ifdef OU_EMU_FIBERS
 void emu_barrier();
+void emu_wave_sync();
 inline void __syncthreads() { emu_barrier(); }
 #else
 inline void __syncthreads() {}
+inline void emu_wave_sync() {}
 #endif
 
 typedef int hipError_t;
@@ -60,8 +62,20 @@ inline hipError_t hipGetLastError() { return hipSuccess; }
 inline const char* hipGetErrorString(hipError_t) { return "emu"; }
 inline hipError_t hipFuncSetAttribute(const void*, int, int) { return hipSuccess; }
 inline hipError_t hipGetDevice(int* d) { *d = 0; return hipSuccess; }
-enum { hipDeviceAttributeSharedMemPerBlockOptin = 74 };
-inline hipError_t hipDeviceGetAttribute(int* v, int, int) { *v = 163840; return hipSuccess; }
+enum { hipDeviceAttributeSharedMemPerBlockOptin = 74, hipDeviceAttributeMultiprocessorCount = 63 };
+// a few "CUs" (OUHIP_EMU_CUS, default 3) so persistent kernels walk several tiles
+inline hipError_t hipDeviceGetAttribute(int* v, int attr, int)
+{
+    if (attr == hipDeviceAttributeMultiprocessorCount) {
+        const char* e = std::getenv("OUHIP_EMU_CUS");
+        *v = e ? std::atoi(e) : 3;
+    } else {
+        *v = 163840;
+    }
+    return hipSuccess;
+}
+template <typename K>
+inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* n, K, int, size_t) { *n = 1; return hipSuccess; }
 inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return hipSuccess; }
 #define HIP_SYMBOL(x) (&(x))
 
@@ -106,6 +120,14 @@ inline void emu_store_b32(uint32_t v, emu_rsrc r, int voff, int soff, int)
     if (!emu_in_range(r, (uint32_t)voff, (uint32_t)soff, 4, "store_b32")) return;
     std::memcpy((char*)r.base + (uint32_t)voff + (uint32_t)soff, &v, 4);
 }
+inline void emu_store_b128(emu_u4 v, emu_rsrc r, int voff, int soff, int)
+{
+    if (!emu_in_range(r, (uint32_t)voff, (uint32_t)soff, 16, "store_b128")) return;
+    std::memcpy((char*)r.base + (uint32_t)voff + (uint32_t)soff, &v, 16);
+}
+#define __builtin_amdgcn_raw_buffer_store_b128 emu_store_b128
+#define __builtin_amdgcn_readfirstlane(x) (x)
+#define __builtin_amdgcn_s_waitcnt(x) ((void)0)
 #define __builtin_amdgcn_raw_buffer_load_b32 emu_load_b32
 #define __builtin_amdgcn_raw_buffer_load_b128 emu_load_b128
 #define __builtin_amdgcn_raw_buffer_store_b32 emu_store_b32
@@ -165,7 +187,7 @@ inline void emu_launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t, A
 struct emu_fiber {
     ucontext_t ctx;
     std::vector<char> stack;
-    int state = 0;   // 0 runnable, 1 at barrier, 2 at mfma, 3 done
+    int state = 0;   // 0 runnable, 1 at barrier, 2 at mfma, 3 done, 4 at a wave-level wait
     float a = 0, b = 0;
     emu_f16v c;
 };
@@ -181,6 +203,14 @@ inline void emu_fiber_entry()
     emu_bs->body();
     emu_bs->f[emu_bs->cur].state = 3;
     swapcontext(&emu_bs->f[emu_bs->cur].ctx, &emu_bs->sched);
+}
+// s_waitcnt on LDS-DMA: the wave's 64 lanes issued the DMA as ONE instruction,
+// so after the wait every lane sees every lane's slots -- a wave rendezvous
+inline void emu_wave_sync()
+{
+    emu_fiber& me = emu_bs->f[emu_bs->cur];
+    me.state = 4;
+    swapcontext(&me.ctx, &emu_bs->sched);
 }
 inline void emu_barrier()
 {
@@ -255,6 +285,20 @@ inline void emu_launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t, A
                 swapcontext(&bs.sched, &bs.f[t].ctx);
                 progressed = true;
             }
+            // waves whose live lanes all wait at a wave-level wait continue together
+            for (int w = 0; w * 64 < nt; ++w) {
+                bool all = true, any = false;
+                for (int l = 0; l < 64; ++l) {
+                    const int st = bs.f[w * 64 + l].state;
+                    all &= st == 4 || st == 3;
+                    any |= st == 4;
+                }
+                if (all && any) {
+                    for (int l = 0; l < 64; ++l)
+                        if (bs.f[w * 64 + l].state == 4) bs.f[w * 64 + l].state = 0;
+                    progressed = true;
+                }
+            }
             // waves whose 64 lanes all wait at an MFMA execute it
             for (int w = 0; w * 64 < nt; ++w) {
                 bool all = true, any = false;
@@ -294,6 +338,23 @@ inline void emu_launch(K kern, dim3 grid, dim3 block, size_t lds, hipStream_t, A
 }
 #endif
 #define hipLaunchKernelGGL(kern, grid, block, lds, stream, ...) emu_launch(kern, grid, block, lds, stream, __VA_ARGS__)
+
+// LDS-DMA (ou_common.h OU_GLDS4): lane l's dword lands at dst + 4 l
+#define OU_GLDS4(src, dst) std::memcpy((char*)(dst) + 4 * (threadIdx.x & 63), (const void*)(src), 4)
+#define OU_GLDS16(src, dst) std::memcpy((char*)(dst) + 16 * (threadIdx.x & 63), (const void*)(src), 16)
+// buffer LDS-DMA: lds_addr is the host address of the LDS block here (OU_LDS_ADDR)
+inline void emu_blds(emu_rsrc r, unsigned voff, unsigned soff, uintptr_t lds, int size)
+{
+    char* dst = (char*)lds + size * (threadIdx.x & 63);
+    if (!emu_in_range(r, voff, soff, size, "blds")) { std::memset(dst, 0, size); return; }
+    std::memcpy(dst, r.base + voff + soff, size);
+}
+#define ou_blds4(r, v, s, l) emu_blds((r), (v), (s), (l), 4)
+#define ou_blds16(r, v, s, l) emu_blds((r), (v), (s), (l), 16)
+typedef uintptr_t ou_ldsa_t;
+#define OU_LDS_ADDR(p) ((uintptr_t)(const void*)(p))
+#define OU_WAIT_VMCNT0() emu_wave_sync()
+#define OU_WAIT_VMCNT(n) emu_wave_sync()
 
 // the product's uniform-resource helper (ou_common.h), host version
 inline emu_rsrc ou_rsrc(const void* p, long long bytes)

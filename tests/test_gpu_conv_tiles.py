@@ -1,4 +1,5 @@
-"""Every ou_conv tile shape x tiles-per-workgroup against a torch fp32
+"""Every ou_conv tile shape x kernel variant (one tile per workgroup,
+persistent, warp-specialised persistent) against a torch fp32
 reference of the same convolution (ragged lengths, batch 2, residual epilogue,
 frame view).  A tile the autotuner might pick must be exact up to fp32
 summation order."""
@@ -24,6 +25,10 @@ GEOMS = [
     (512, 256, 1, 3, 33, 2, True),
     (64, 32, 2, 3, 300, 2, False),     # frame view, cin % chunk == 0 or not
     (48, 24, 5, 3, 203, 1, False),
+    # more output tiles than CUs: persistent workgroups walk several tiles
+    # (warp-specialised chunk stream across tile boundaries; split-K parity)
+    (32, 32, 1, 3, 70000, 2, True),
+    (256, 256, 1, 3, 3000, 2, True),
 ]
 
 
@@ -59,16 +64,64 @@ def test_conv_every_tile(geom):
     for t in range(lib.ou_conv_num_tiles()):
         if not lib.ou_conv_tile_ok(kt, t):
             continue
-        for tpw in (0, 1, 2):
-            if not lib.ou_conv_tile_ok(kt, t | (tpw << 8)):
+        for v in (0, 1 << 8, 2 << 8, 1 << 10):   # one-tile, persistent x2 / x4, warp-specialised
+            if not lib.ou_conv_tile_ok(kt, t | v):
                 continue
             y = E.new_act(B, cout, U, DEV)
             ra = E.Act(res.to(DEV)) if with_res else None
             d = E.conv_desc(cw, xa, y, res1=ra, s1=0.7, n_frames=U)
-            d.tile = t | (tpw << 8)
-            assert lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream)) == 0
+            d.tile = t | v
+            rc = lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
+            if rc == -2 and v == 1 << 10:
+                continue   # warp-specialised form refused for this geometry (single K chunk, rout > 1)
+            assert rc == 0
             torch.cuda.synchronize()
             err = ((y.t.cpu() - ref).norm() / ref.norm()).item()
             if not err < 1e-5:
-                bad.append((t, tpw, err))
+                bad.append((t, v, err))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("geom", [(96, 40, 1, 3, 301, 2), (64, 64, 1, 3, 40000, 2)], ids=str)
+def test_conv_full_epilogue_every_tile(geom):
+    """bias + residual 1 + FiLM + residual 2 + valid_len zeroing, every tile
+    shape and kernel variant (ou_conv_desc formula, include/ouhip.h)."""
+    cout, cin, frame, kt, T, B = geom
+    g = torch.Generator().manual_seed(7)
+    w = torch.randn(cout, cin * frame, kt, generator=g) * 0.1
+    bias = torch.randn(cout, generator=g) * 0.1
+    spec = E.ConvSpec(w.numpy(), cin, frame, (kt - 1) // 2, 1, 0.25, bias.numpy())
+    cw = E.make_conv(spec, DEV)
+    x = torch.randn(B, cin, T, generator=g)
+    U = -(-T // frame)
+    r1 = torch.randn(B, cout, U, generator=g)
+    r2 = torch.randn(B, cout, U, generator=g)
+    film = torch.randn(B, 2 * cout, generator=g)
+    valid = U - 3
+    y0 = _ref(w, bias, x, frame, kt, 0.25, None, 1.0)
+    y0[:, :, valid:] = 0.0
+    ref = (y0 + r1) * 0.7
+    ref = film[:, :cout, None] * ref + film[:, cout:, None]
+    ref = (ref + r2) * 0.5
+    xa, r1a, r2a = E.Act(x.to(DEV)), E.Act(r1.to(DEV)), E.Act(r2.to(DEV))
+    fd = film.to(DEV)
+    lib = L.load()
+    stream = torch.cuda.current_stream().cuda_stream
+    bad = []
+    for t in range(lib.ou_conv_num_tiles()):
+        for v in (0, 1 << 8, 2 << 8, 1 << 10):
+            if not lib.ou_conv_tile_ok(kt, t | v):
+                continue
+            y = E.new_act(B, cout, U, DEV)
+            d = E.conv_desc(cw, xa, y, res1=r1a, s1=0.7, film=fd.data_ptr(), film_bs=2 * cout,
+                            res2=r2a, s2=0.5, n_frames=U, valid_len=valid)
+            d.tile = t | v
+            rc = lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
+            if rc == -2 and v == 1 << 10:
+                continue   # warp-specialised form refused for this geometry (single K chunk, rout > 1)
+            assert rc == 0
+            torch.cuda.synchronize()
+            err = ((y.t.cpu() - ref).norm() / ref.norm()).item()
+            if not err < 1e-5:
+                bad.append((t, v, err))
     assert not bad, bad

@@ -74,6 +74,7 @@ def main():
     ap.add_argument("--tile", type=int, default=None)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--stamps", action="store_true", help="diag library: per-phase cycles")
+    ap.add_argument("--wstamps", action="store_true", help="diag library: warp-specialised kernel phases")
     a = ap.parse_args()
     dev = "cuda:0"
     stream = torch.cuda.current_stream().cuda_stream
@@ -81,8 +82,9 @@ def main():
     names = [a.layer] if a.layer else list(LAYERS)
     for name in names:
         d, keep = make(name, dev)
-        tiles = [a.tile] if a.tile is not None else [t | (p << 8) for t in range(lib.ou_conv_num_tiles())
-                                                      for p in (0, 1, 2) if lib.ou_conv_tile_ok(d.kt, t | (p << 8))]
+        tiles = [a.tile] if a.tile is not None else [t | v for t in range(lib.ou_conv_num_tiles())
+                                                      for v in (0, 1 << 8, 2 << 8, 1 << 10)
+                                                      if lib.ou_conv_tile_ok(d.kt, t | v)]
         res = []
         for t in tiles:
             ms = time_tile(d, t, a.reps, stream)
@@ -90,10 +92,28 @@ def main():
                 res.append((ms, t))
         res.sort()
         fl = d._flops
-        nm = lambda t: f"t{t & 0xff}" + (f"p{1 << (t >> 8)}" if t >> 8 else "")
+        nm = lambda t: f"t{t & 0xff}" + ("w" if t >> 10 else (f"p{1 << (t >> 8)}" if t >> 8 else ""))
         line = "  ".join(f"{nm(t)}:{ms * 1e3:.1f}us" for ms, t in res[:12])
         print(f"{name:5s} {fl / 1e9:6.2f} GFLOP  best {nm(res[0][1])} {res[0][0] * 1e3:.1f} us "
               f"{fl / res[0][0] / 1e9:.1f} TF/s | {line}", flush=True)
+        if a.wstamps:
+            import ctypes
+
+            n = 4096 * 8
+            buf = (ctypes.c_uint64 * n)()
+            lib.ou_conv_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            assert lib.ou_conv_read_stamps(ctypes.cast(buf, ctypes.c_void_p), n) == 0
+            st = np.frombuffer(buf, dtype=np.uint64).reshape(2048, 16).astype(np.float64)
+            st = st[st[:, :5].sum(1) > 0]
+            c, l = st[:, :8], st[:, 8:]
+            print(f"      {len(st)} WGs; MFMA wave cycles: mfma={c[:, 1].mean():.0f} acc-image={c[:, 2].mean():.0f} "
+                  f"tick-barrier={c[:, 3].mean():.0f} first-barrier={c[:, 4].mean():.0f}; staging wave: "
+                  f"dma-issue={l[:, 0].mean():.0f} vmcnt-wait={l[:, 1].mean():.0f} prelu={l[:, 3].mean():.0f} "
+                  f"epilogue={l[:, 4].mean():.0f} res+other={l[:, 5].mean():.0f} barrier={l[:, 2].mean():.0f}",
+                  flush=True)
+            t0 = c[:, 6].min()
+            print(f"      realtime (us): MFMA wave start {(c[:, 6].max() - t0) / 100:.2f} max, end {(c[:, 7] - t0).min() / 100:.2f}.."
+                  f"{(c[:, 7] - t0).max() / 100:.2f}", flush=True)
         if a.stamps:
             import ctypes
 
