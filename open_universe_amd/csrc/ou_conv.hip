@@ -372,9 +372,28 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
             const int m = min(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
             ph[r] = rout > 1 ? m / cout : 0;
             co[r] = m - ph[r] * cout;
-            bias[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, co[r] * 4, 0, 0));
-            fa[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, co[r] * 4, 0, 0));
-            fb[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, (cout + co[r]) * 4, 0, 0));
+        }
+        // absent operands: one uniform branch around the whole group of loads
+        // (never a per-element select between a load and a default)
+        if (d.bias) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bias[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, co[r] * 4, 0, 0));
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bias[r] = 0.f;
+        }
+        if (has_fm) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                fa[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, co[r] * 4, 0, 0));
+                fb[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, (cout + co[r]) * 4, 0, 0));
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                fa[r] = 0.f;
+                fb[r] = 0.f;
+            }
         }
 #pragma unroll
         for (int nr = 0; nr < NR; ++nr) {
@@ -387,10 +406,24 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
                 const int t = u * rout + ph[r];
                 const bool ok = m < M && u < d.n_frames && t < ylen;
                 off[r] = ok ? t : -1;   // column; row offsets differ per tensor
-                v1[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                    r1s, ok ? (co[r] * (int)d.r1_cstride + t) * 4 : kSentinel, 0, 0));
-                v2[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                    r2s, ok ? (co[r] * (int)d.r2_cstride + t) * 4 : kSentinel, 0, 0));
+            }
+            if (has_r1) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    v1[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        r1s, off[r] >= 0 ? (co[r] * (int)d.r1_cstride + off[r]) * 4 : kSentinel, 0, 0));
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v1[r] = 0.f;
+            }
+            if (has_r2) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    v2[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        r2s, off[r] >= 0 ? (co[r] * (int)d.r2_cstride + off[r]) * 4 : kSentinel, 0, 0));
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v2[r] = 0.f;
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -739,9 +772,12 @@ struct WCfg {
     static constexpr int CPW = HQ / WK;                   // ... per MFMA wave
     static constexpr int AG = WM * MR * HQ * KT * 64;     // float4 of weights per chunk
     static constexpr int STAGE = XBUF + AG * 4;           // floats
-    static constexpr int XPW = (CC / 4) * NI;             // X pieces per staging wave per chunk
+    static constexpr int XPW = (CC / 4) * NI;             // X dword pieces per staging wave per chunk
+    static constexpr int PQ = XBUF / 256;                 // X 16-B pieces per chunk (quad path)
+    static constexpr int XPWQ = (PQ + 3) / 4;             // ... per staging wave
     static constexpr int APW = (AG / 64 + 3) / 4;         // A pieces per staging wave per chunk
     static constexpr int NPI = XPW + APW;                 // DMAs per staging wave per chunk
+    static constexpr int NPIQ = XPWQ + APW;               // ... on the quad path
     static constexpr int OS = BN + 8;                     // accumulator image row stride
     static constexpr int OUT = S * STAGE;                 // accumulator image offset
     static constexpr int RES = OUT + WK * BM * OS;        // residual tile offset
@@ -761,7 +797,14 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
     static_assert(CC % 8 == 0 && WC::HQ % WK == 0, "chunk must split into 4-pair groups per wave");
     static_assert(WM * WN * WK == 4, "4 MFMA waves");
     static_assert(S == 3, "3-stage ring (DMA two chunks ahead)");
-    static_assert(WC::NPI <= 63, "vmcnt range");
+    static_assert(WC::NPI <= 63 && WC::NPIQ <= 63, "vmcnt range");
+    static_assert(WC::XBUF % 256 == 0 && WC::SW >= WC::BN + 8, "quad X pieces tile the window");
+    // X staging path: "quad" (16-B DMA groups of 4 frames, lane-private
+    // activation) when the frame view is the plain signal and 4-frame groups
+    // align with sample 0; LDS column 0 is frame n0 - 4 there, n0 - pad on the
+    // dword path
+    const bool quad = d.frame == 1 && (d.shift & 3) == 0;
+    const int xoff = quad ? 4 - d.pad : 0;
     OU_DYNAMIC_LDS(float4, lds4);
     float* lds = (float*)lds4;
 
@@ -803,6 +846,20 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
             decode(i, b, n0, mt0);
             const ou_ldsa_t st = lds0 + (unsigned)((t % S) * WC::STAGE * 4);
             const __amdgpu_buffer_rsrc_t xrs = ou_rsrc(d.x + (int64_t)b * d.x_bstride, (int64_t)cin * xc * 4);
+            if (quad) {
+                // 16-B piece p = 64 lanes x 4 frames of the [channel][frame] image
+#pragma unroll
+                for (int kk = 0; kk < WC::XPWQ; ++kk) {
+                    const int p = sw * WC::XPWQ + kk;
+                    const int e = 256 * p + 4 * lane;
+                    const int row = e / WC::SW, col = e - (e / WC::SW) * WC::SW;
+                    const int cq = q * CC + row;
+                    const int smp = n0 - 4 + col + d.shift;
+                    const bool ok = (int)(p < WC::PQ) & (int)(cq < cin) & (int)(smp >= 0) & (int)(smp + 3 < in_len);
+                    ou_blds16(xrs, ok ? (unsigned)(cq * xc + smp) * 4u : (unsigned)kSentinel, 0u,
+                              p < WC::PQ ? st + (unsigned)(256 * p * 4) : lds0 + (unsigned)(WC::DUMMY * 4));
+                }
+            } else {
             int fw[WC::NI];   // lane sample of each 64-frame piece (frame f -> sample f R + ph + shift)
 #pragma unroll
             for (int pi = 0; pi < WC::NI; ++pi) fw[pi] = (n0 - d.pad + pi * 64 + lane) * R + d.shift;
@@ -821,6 +878,7 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
                     ou_blds4(xrs, ok ? (unsigned)pos * 4u : (unsigned)kSentinel, soff, row + pi * 256);
                 }
                 if (++ci == cin) { ci = 0; ++ph; }
+            }
             }
             const unsigned wbase = (unsigned)((mt0 * a_mt_stride + (int64_t)q * (WC::HQ * KT * 256)) * 4);
 #pragma unroll
@@ -865,6 +923,35 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
             int b, n0, mt0;
             decode(i, b, n0, mt0);
             const float sc = d.in_scale ? d.in_scale[b] : 1.0f;
+            if (quad) {   // the groups this lane DMA'd itself; the right edge's partial group by plain loads
+                const int q = t - i * nchunks;
+                float4* x4 = (float4*)(lds + (t % S) * WC::STAGE);
+#pragma unroll
+                for (int kk = 0; kk < WC::XPWQ; ++kk) {
+                    const int p = sw * WC::XPWQ + kk;
+                    if (p < WC::PQ) {
+                        float4 v = x4[64 * p + lane];
+                        const int e = 256 * p + 4 * lane;
+                        const int row = e / WC::SW, col = e - (e / WC::SW) * WC::SW;
+                        const int cq = q * CC + row;
+                        const int smp = n0 - 4 + col + d.shift;
+                        if (cq < cin && smp < in_len && smp + 3 >= in_len && smp >= 0) {
+                            const float* xr = d.x + (int64_t)b * d.x_bstride + (int64_t)cq * xc + smp;
+                            v.x = xr[0];
+                            v.y = smp + 1 < in_len ? xr[1] : 0.f;
+                            v.z = smp + 2 < in_len ? xr[2] : 0.f;
+                            v.w = 0.f;
+                        }
+                        v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
+                        v.x = v.x >= 0.f ? v.x : v.x * slope;
+                        v.y = v.y >= 0.f ? v.y : v.y * slope;
+                        v.z = v.z >= 0.f ? v.z : v.z * slope;
+                        v.w = v.w >= 0.f ? v.w : v.w * slope;
+                        x4[64 * p + lane] = v;
+                    }
+                }
+                return;
+            }
             float4* xs = (float4*)(lds + (t % S) * WC::STAGE + sw * (CC / 4) * WC::SW);
             constexpr int N4 = (CC / 4) * WC::SW / 4;
 #pragma unroll
@@ -960,8 +1047,12 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
         // prologue: chunks 0, 1 in flight; chunk 0 landed and activated
         OU_WSTAMP_INIT
         for (int t = 0; t < 2 && t < items; ++t) issue_item(t);
-        if (items >= 2) OU_WAIT_VMCNT(WC::NPI);
-        else OU_WAIT_VMCNT0();
+        if (items >= 2) {
+            if (quad) OU_WAIT_VMCNT(WC::NPIQ);
+            else OU_WAIT_VMCNT(WC::NPI);
+        } else {
+            OU_WAIT_VMCNT0();
+        }
         if (items > 0) prelu_item(0);
         __syncthreads();
         for (int t = 0; t < items; ++t) {
@@ -972,8 +1063,12 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
             if (t + 2 < items) issue_item(t + 2);
             OU_WSTAMP(0);
             // chunk t + 1 (and everything older) landed; chunk t + 2 stays in flight
-            if (t + 2 < items) OU_WAIT_VMCNT(WC::NPI);
-            else OU_WAIT_VMCNT0();
+            if (t + 2 < items) {
+                if (quad) OU_WAIT_VMCNT(WC::NPIQ);
+                else OU_WAIT_VMCNT(WC::NPI);
+            } else {
+                OU_WAIT_VMCNT0();
+            }
             OU_WSTAMP(1);
             if (t + 1 < items) prelu_item(t + 1);
             OU_WSTAMP(3);
@@ -1025,7 +1120,7 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
             const float* xs = lds + (t % S) * WC::STAGE;
             const float4* ap = (const float4*)(xs + WC::XBUF) + ((wm * MR) * WC::HQ + wk * WC::CPW) * KT * 64 + lane;
             // lane's B column: row 2p + h, frame wn*32*NR + nr*32 + l32 + tap
-            const float* xp = xs + (8 * wk * WC::CPW + h) * WC::SW + wn * 32 * NR + l32;
+            const float* xp = xs + (8 * wk * WC::CPW + h) * WC::SW + wn * 32 * NR + l32 + xoff;
             constexpr int NS = WC::CPW * KT;
             float4 fa[2][MR];
             float fb[2][4][NR];

@@ -136,19 +136,35 @@ __global__ __launch_bounds__(256) void head_kernel(ou_head_desc d)
     if (t >= d.length) return;
     const float* h = d.h + (int64_t)b * d.h_bstride;
     const int T = d.length;
+    // taps t-1, t, t+1 with zero padding: clamped (always valid) addresses and
+    // 0/1 masks, so the loads of a channel group issue back to back instead of
+    // one branch-guarded round trip each; the FMA order (c, then k) is the
+    // reference's conv1d summation order
+    const int tl = max(t - 1, 0), tr = min(t + 1, T - 1);
+    const float ml = t >= 1 ? 1.f : 0.f, mr = t + 1 < T ? 1.f : 0.f;
     float net = 0.f;
-    for (int c = 0; c < d.channels; ++c) {
-        const float* hc = h + (int64_t)c * T;
+    constexpr int CG = 8;   // channels per load group
+    for (int c0 = 0; c0 < d.channels; c0 += CG) {
+        float v[CG][3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int tt = t + k - 1;
-            float v = 0.f;
-            if (tt >= 0 && tt < T) {
-                v = hc[tt];
-                v = v >= 0.f ? v : v * d.slope1;
-                v = v >= 0.f ? v : v * d.slope2;
+        for (int j = 0; j < CG; ++j) {
+            const int c = min(c0 + j, d.channels - 1);
+            const float* hc = h + (int64_t)c * T;
+            v[j][0] = hc[tl];
+            v[j][1] = hc[t];
+            v[j][2] = hc[tr];
+        }
+#pragma unroll
+        for (int j = 0; j < CG; ++j) {
+            if (c0 + j >= d.channels) break;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                float x = v[j][k];
+                x = x >= 0.f ? x : x * d.slope1;
+                x = x >= 0.f ? x : x * d.slope2;
+                x = k == 0 ? x * ml : (k == 2 ? x * mr : x);
+                net = fmaf(d.w[(c0 + j) * 3 + k], x, net);
             }
-            net = fmaf(d.w[c * 3 + k], v, net);
         }
     }
     net += d.bias;
