@@ -47,15 +47,34 @@ def cpu_model():
     return "unknown"
 
 
-def build_model(device, nch=None, seed=0):
+# BASELINE.json configs: c2 is the headline (default); the others are measured
+# on request (--config) with the same harness.  Batch is per GPU for c3 and the
+# whole-node batch for c4 (32 clips sharded over the ranks: 32/N per rank).
+CONFIGS = {
+    "c2": dict(arch="pp16", batch=1, seconds=8.0, n_steps=None,
+               workload="UNIVERSE++ 16 kHz enhance(), batch=1, 8 s clip, 8 diffusion steps (BASELINE.json configs[1])"),
+    "c3": dict(arch="orig16", batch=8, seconds=8.0, n_steps=60,
+               workload="UNIVERSE (original) 16 kHz enhance(), batch=8, 8 s clips, 60 diffusion steps "
+                        "(BASELINE.json configs[2])"),
+    "c4": dict(arch="pp24", batch=32, seconds=10.0, n_steps=None, node_batch=True,
+               workload="UNIVERSE++ 24 kHz enhance(), batch=32 per node sharded over the GPUs, 10 s clips, "
+                        "8 diffusion steps (BASELINE.json configs[3])"),
+    "c5": dict(arch="pp16", batch=1, seconds=60.0, n_steps=None,
+               workload="UNIVERSE++ 16 kHz enhance(), batch=1, 60 s long-form clip, 8 diffusion steps, fp32 "
+                        "(BASELINE.json configs[4] names fp16; this build computes in fp32)"),
+}
+
+
+def build_model(device, nch=None, seed=0, arch="pp16"):
     import torch
 
     from open_universe_amd.configs import get_config
-    from open_universe_amd.networks.universe import UniverseGAN
+    from open_universe_amd.networks.universe import Universe, UniverseGAN
     from open_universe_amd.utils.synthetic import synth_state_dict
 
-    cfg = get_config("pp16", nch)
-    m = UniverseGAN(**{k: v for k, v in cfg.items() if k != "_target_"})
+    cfg = get_config(arch, nch)
+    cls = Universe if cfg["_target_"].endswith(".Universe") else UniverseGAN
+    m = cls(**{k: v for k, v in cfg.items() if k != "_target_"})
     m.load_state_dict(synth_state_dict([(k, v.shape) for k, v in m.state_dict().items()], seed),
                       strict=False)
     return cfg, m.to(device).eval()
@@ -119,7 +138,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--seconds", type=float, default=CLIP_S)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="BASELINE.json config (c2 = configs[1], the headline)")
+    ap.add_argument("--seconds", type=float, default=None, help="override the config's clip length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--dump-ops", default=None, help="write per-op profile rows (JSON)")
@@ -141,22 +162,29 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    cfg, model = build_model(dev)
-    T = int(args.seconds * FS)
+    C = CONFIGS[args.config]
+    if args.seconds is None:
+        args.seconds = C["seconds"]
+    B = C["batch"] // world if C.get("node_batch") else C["batch"]
+    assert B >= 1, "c4 shards 32 clips over at most 32 ranks"
+    cfg, model = build_model(dev, arch=C["arch"])
+    fs = int(cfg["fs"])
+    T = int(args.seconds * fs)
     n_clips = args.warmup + args.steps
-    clips = [torch.from_numpy(synth_audio(T, FS, rank * 100003 + i)[0])[None].to(dev)
-             for i in range(min(n_clips, 8))]
+    clips = [torch.from_numpy(np.stack([synth_audio(T, fs, rank * 100003 + i * 97 + j)[0] for j in range(B)]))
+             .to(dev) for i in range(min(n_clips, 4))]
     rng = torch.Generator(device=dev).manual_seed(1028282 + rank)
+    ekw = {"n_steps": C["n_steps"]} if C["n_steps"] else {}
 
     with torch.no_grad():
         for i in range(args.warmup):
-            model.enhance(clips[i % len(clips)], rng=rng)
+            model.enhance(clips[i % len(clips)], rng=rng, **ekw)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            model.enhance(clips[(args.warmup + i) % len(clips)], rng=rng)
+            model.enhance(clips[(args.warmup + i) % len(clips)], rng=rng, **ekw)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -167,20 +195,21 @@ def main():
     if not args.no_profile:
         plan = next(iter(model._plans.values()))
         with torch.no_grad():
-            plan.MIX.copy_(clips[0][:, None])
+            plan.MIX.copy_(clips[0].reshape(plan.MIX.shape))
             plan.draw_noise(rng)
             prof = profile_roofline(plan, torch.cuda.current_stream(dev).cuda_stream, args.dump_ops)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline(model, cfg, args.seconds)
 
     if rank == 0:
-        audio_s = world * args.steps * args.seconds
+        audio_s = world * B * args.steps * args.seconds
         value = audio_s / elapsed
         ms_per_step = 1000.0 * elapsed / args.steps
         out = {
             "metric": "sec-audio enhanced/sec/GPU + xRT, UNIVERSE++ 16 kHz 8 s clips @1/2/4/8 GPU",
+            "bench_config": args.config,
             "value": round(value, 3),
             "unit": "audio-s/s",
             "n_gpus": world,
@@ -192,10 +221,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (16 kHz harmonic+noise clips, seeded synthetic weights)",
-            "config": {"workload": "UNIVERSE++ 16 kHz enhance(), batch=1, 8 s clip, 8 diffusion steps "
-                                   "(BASELINE.json configs[1])",
-                       "model": "UniverseGAN PP16 (42.85 M params)", "global_batch": world,
-                       "clip_s": args.seconds, "n_steps": 8, "parallelism": f"utterance-shard x{world}"},
+            "config": {"workload": C["workload"],
+                       "model": {"pp16": "UniverseGAN PP16 (42.85 M params)", "orig16": "Universe ORIG16 (43.0 M params)",
+                                 "pp24": "UniverseGAN PP24 (107.5 M params)"}[C["arch"]],
+                       "global_batch": world * B, "batch_per_gpu": B,
+                       "clip_s": args.seconds, "n_steps": C["n_steps"] or 8,
+                       "parallelism": f"utterance-shard x{world}"},
             "xrt_per_gpu": round(value / world, 3),
         }
         if prof is not None:
