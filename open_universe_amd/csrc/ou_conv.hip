@@ -760,8 +760,11 @@ __global__ __launch_bounds__(256) void conv_pkernel(ou_conv_desc d, int nchunks,
 // [BM][BN].  B fragment of k-step (pair p, tap k): lane l reads
 // X[2p + l/32][n + l%32 + k].
 // ---------------------------------------------------------------------------
+constexpr int kWsLoaders = 8;   // staging waves per workgroup (4 MFMA waves)
+
 template <int KT, int CC, int WM, int WN, int WK, int MR, int NR, int S>
 struct WCfg {
+    static constexpr int NL = kWsLoaders;
     static constexpr int BM = 32 * WM * MR;
     static constexpr int BN = 32 * NR * WN;
     static constexpr int W = BN + KT - 1;                 // frames per chunk row
@@ -772,10 +775,10 @@ struct WCfg {
     static constexpr int CPW = HQ / WK;                   // ... per MFMA wave
     static constexpr int AG = WM * MR * HQ * KT * 64;     // float4 of weights per chunk
     static constexpr int STAGE = XBUF + AG * 4;           // floats
-    static constexpr int XPW = (CC / 4) * NI;             // X dword pieces per staging wave per chunk
+    static constexpr int XPW = (CC / NL) * NI;            // X dword pieces per staging wave per chunk
     static constexpr int PQ = XBUF / 256;                 // X 16-B pieces per chunk (quad path)
-    static constexpr int XPWQ = (PQ + 3) / 4;             // ... per staging wave
-    static constexpr int APW = (AG / 64 + 3) / 4;         // A pieces per staging wave per chunk
+    static constexpr int XPWQ = (PQ + NL - 1) / NL;       // ... per staging wave
+    static constexpr int APW = (AG / 64 + NL - 1) / NL;   // A pieces per staging wave per chunk
     static constexpr int NPI = XPW + APW;                 // DMAs per staging wave per chunk
     static constexpr int NPIQ = XPWQ + APW;               // ... on the quad path
     static constexpr int OS = BN + 8;                     // accumulator image row stride
@@ -784,13 +787,13 @@ struct WCfg {
     static constexpr int DUMMY = RES + BM * BN;           // sink of padding A pieces (never read)
     static constexpr int LDS = DUMMY + 256;               // floats
     static constexpr int G4 = BM * BN / 4;                // 16-B epilogue groups per tile
-    static constexpr int GPT = G4 / 256;                  // ... per staging thread
+    static constexpr int GPT = G4 / (64 * NL);            // ... per staging thread
     static constexpr int RPP = 256 / BN;                  // rows per 64-group piece
-    static_assert(G4 % 256 == 0 && 256 % BN == 0 && BN % 4 == 0, "epilogue group mapping");
+    static_assert(G4 % (64 * NL) == 0 && 256 % BN == 0 && BN % 4 == 0 && CC % NL == 0, "staging mapping");
 };
 
 template <int KT, int CC, int WM, int WN, int WK, int MR, int NR, int S>
-__global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks, int mtiles,
+__global__ __launch_bounds__(256 + 64 * kWsLoaders) void conv_wkernel(ou_conv_desc d, int nchunks, int mtiles,
                                                     int64_t a_mt_stride, int ntn, int mgroups, int ntiles)
 {
     using WC = WCfg<KT, CC, WM, WN, WK, MR, NR, S>;
@@ -826,7 +829,7 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
         // ======================= staging waves ==============================
         const int tid = threadIdx.x - 256;
         const int lane = tid & 63;
-        const int sw = __builtin_amdgcn_readfirstlane(tid >> 6);   // X rows [sw CC/4, (sw+1) CC/4)
+        const int sw = __builtin_amdgcn_readfirstlane(tid >> 6);   // X rows [sw CC/NL, (sw+1) CC/NL)
         const int R = d.frame;
         const int cin = d.cin;
         const int in_len = d.in_len;
@@ -863,14 +866,14 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
             int fw[WC::NI];   // lane sample of each 64-frame piece (frame f -> sample f R + ph + shift)
 #pragma unroll
             for (int pi = 0; pi < WC::NI; ++pi) fw[pi] = (n0 - d.pad + pi * 64 + lane) * R + d.shift;
-            const int cq0 = q * CC + sw * (CC / 4);
+            const int cq0 = q * CC + sw * (CC / WC::NL);
             int ph = cq0 / cin;
             int ci = cq0 - ph * cin;
 #pragma unroll
-            for (int c = 0; c < CC / 4; ++c) {
+            for (int c = 0; c < CC / WC::NL; ++c) {
                 const bool chan_ok = ph < R;
                 const unsigned soff = (unsigned)(chan_ok ? ci : 0) * (unsigned)xc * 4u;
-                const ou_ldsa_t row = st + (unsigned)((sw * (CC / 4) + c) * WC::SW * 4);
+                const ou_ldsa_t row = st + (unsigned)((sw * (CC / WC::NL) + c) * WC::SW * 4);
 #pragma unroll
                 for (int pi = 0; pi < WC::NI; ++pi) {
                     const int pos = fw[pi] + ph;
@@ -895,9 +898,9 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
                 }
             }
         };
-        // epilogue group k of this thread: piece (sw + 4 k) of the row-major tile, lane's group in it
+        // epilogue group k of this thread: piece (sw + NL k) of the row-major tile, lane's group in it
         auto group_of = [&](int k, int& row, int& c4) {
-            const int g = (sw + 4 * k) * 64 + lane;
+            const int g = (sw + WC::NL * k) * 64 + lane;
             row = g / (WC::BN / 4);
             c4 = g - row * (WC::BN / 4);
         };
@@ -914,7 +917,7 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
                 const int m = mt0 * 32 + row, u = n0 + 4 * c4;
                 const bool full = (int)(m < M) & (int)(u + 3 < ulim);
                 ou_blds16(r1s, full ? (unsigned)(m * r1c + u) * 4u : (unsigned)kSentinel, 0u,
-                          lds0 + (unsigned)((WC::RES + (sw + 4 * k) * 256) * 4));
+                          lds0 + (unsigned)((WC::RES + (sw + WC::NL * k) * 256) * 4));
             }
         };
         // PReLU(x * in_scale) in place on this wave's X rows of item t
@@ -952,8 +955,8 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
                 }
                 return;
             }
-            float4* xs = (float4*)(lds + (t % S) * WC::STAGE + sw * (CC / 4) * WC::SW);
-            constexpr int N4 = (CC / 4) * WC::SW / 4;
+            float4* xs = (float4*)(lds + (t % S) * WC::STAGE + sw * (CC / WC::NL) * WC::SW);
+            constexpr int N4 = (CC / WC::NL) * WC::SW / 4;
 #pragma unroll
             for (int k = 0; k < (N4 + 63) / 64; ++k) {
                 const int f = lane + 64 * k;
@@ -987,7 +990,7 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
                 const bool full = mok & (u + 3 < ulim);
                 // per-row operands by scalar loads: the piece spans rows
                 // row0 .. row0 + RPP - 1 (wave-uniform row0)
-                const int row0 = ((sw + 4 * k) * 64) / (WC::BN / 4);
+                const int row0 = ((sw + WC::NL * k) * 64) / (WC::BN / 4);
                 float pb = 0.f, pa = 0.f, pf = 0.f;
 #pragma unroll
                 for (int rr = 0; rr < WC::RPP; ++rr) {
@@ -1003,7 +1006,7 @@ __global__ __launch_bounds__(512) void conv_wkernel(ou_conv_desc d, int nchunks,
                     const float4 p = *(const float4*)(out + (j * WC::BM + row) * WC::OS + 4 * c4);
                     a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
                 }
-                float4 r1 = *(const float4*)(lds + WC::RES + ((sw + 4 * k) * 64 + lane) * 4);
+                float4 r1 = *(const float4*)(lds + WC::RES + ((sw + WC::NL * k) * 64 + lane) * 4);
                 float r2v[4] = {0.f, 0.f, 0.f, 0.f};
                 if (!full) {   // tile edge: per-element residual 1 (the DMA skipped the group)
                     float t1[4];
@@ -1322,7 +1325,8 @@ int launch_w(const ou_conv_desc& d, hipStream_t s)
             OU_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds),
                          "conv: LDS attribute");
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 512, lds) == hipSuccess && n > 0) per_cu = n;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, 256 + 64 * kWsLoaders, lds) == hipSuccess && n > 0)
+            per_cu = n;
         attr = true;
     }
     if (g_num_cus <= 0) {
@@ -1332,7 +1336,8 @@ int launch_w(const ou_conv_desc& d, hipStream_t s)
         if (g_num_cus <= 0) g_num_cus = 1;
     }
     const int grid = std::min(ntiles, per_cu * g_num_cus);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, s, d, nchunks, mtiles, a_mt_stride, ntn, mgroups, ntiles);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256 + 64 * kWsLoaders), lds, s, d, nchunks, mtiles, a_mt_stride, ntn,
+                       mgroups, ntiles);
     return ou_check_launch("conv");
 }
 
