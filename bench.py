@@ -34,6 +34,7 @@ sys.path.insert(0, HERE)
 FS = 16000
 CLIP_S = 8.0
 FP32_PEAK_TF = 157.3   # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md)
+F16_PEAK_TF = 2516.6   # dense F16/BF16 MFMA peak; split-f16 spends 3 MFMAs per f32 MAC
 HBM_PEAK = 8000.0      # GB/s
 
 
@@ -203,6 +204,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline(model, cfg, args.seconds)
 
+    prec = model._get_engine().conv_prec
+    if prec == 1:
+        dtype = "f32 (conv operands split into f16 hi/lo: 3 f16 MFMA passes, f32 accumulation)"
+        peak, peak_basis = round(F16_PEAK_TF / 3, 1), "dense f16 MFMA peak / 3 passes per f32 MAC"
+    else:
+        dtype, peak, peak_basis = "f32", FP32_PEAK_TF, "dense f32 MFMA peak"
     if rank == 0:
         audio_s = world * B * args.steps * args.seconds
         value = audio_s / elapsed
@@ -219,7 +226,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": dtype,
             "data": "synthetic (16 kHz harmonic+noise clips, seeded synthetic weights)",
             "config": {"workload": C["workload"],
                        "model": {"pp16": "UniverseGAN PP16 (42.85 M params)", "orig16": "Universe ORIG16 (43.0 M params)",
@@ -241,8 +248,8 @@ def main():
                     tsrc = (f"{os.path.relpath(args.traffic_json, HERE)} ({pmc.get('tag', '')}): "
                             "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes per ou_conv launch")
             out["roofline"] = {
-                "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TF,
-                "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TF, 4), "traffic": traffic,
+                "bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "peak_basis": peak_basis,
+                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                 "traffic_source": tsrc,
                 "kernel": "ou_conv (conv_kernel, all launches of one enhance)",
                 "launches": prof["n_conv"],

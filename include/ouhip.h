@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define OUHIP_ABI_VERSION 1
+#define OUHIP_ABI_VERSION 2
 
 int ou_abi_version(void);
 const char* ou_last_error(void);
@@ -88,7 +88,18 @@ typedef struct ou_conv_desc {
                                /* num_tiles()), bits 8-9 log2(output tiles per   */
                                /* workgroup; > 0: persistent kernel, see         */
                                /* ou_conv_tile_ok)                               */
+    int32_t prec;              /* 0: f32 operands (weights from ou_conv_pack);   */
+                               /* 1: split-f16 operands (ou_conv_pack_split),    */
+                               /*    f32-class accuracy, see ou_conv.hip         */
+    float w_unscale;           /* prec 1: power of two from ou_conv_pack_split   */
     int32_t _reserved;
+    int32_t* status;           /* prec 1: set to 1 when a staged input exceeds   */
+                               /* the split-f16 range, or NULL                   */
+    float* amax_out;           /* [64] or NULL: running max |y| of the stored    */
+                               /* outputs (atomic max, one slot per workgroup    */
+                               /* id mod 64; zeroed by the caller per enhance)   */
+    const float* amax_in;      /* prec 1: [64] amax_out of x's producer, sets    */
+                               /* the staging exponent; NULL: fixed 2^-6         */
 } ou_conv_desc;
 
 /* Default channel chunk of the kernel for a tap count (informational: the
@@ -103,6 +114,14 @@ int64_t ou_conv_packed_size(int m, int cin_eff, int kt, int cc);
  * 64 (one float4 per lane = 4 consecutive k-steps of the MFMA stream). */
 int ou_conv_pack(const float* w_logical, int m, int cin_eff, int kt, int cc,
                  float* packed);
+/* Split-f16 packing (prec 1): the same number of floats as ou_conv_pack, in
+ * the order [m-tile][8-pair group][hi | lo][tap][lane][8 halves] (lane l:
+ * row l & 31, channel 2*(8*group + j) + (l >> 5) in half j) of
+ * a = w * 2^e, hi = f16(a), lo = f16((a - hi) * 2^11), with e chosen per
+ * layer so max|a| lies in [2^9, 2^10).  *w_unscale receives 2^(6-e) (the
+ * kernel stages the input as x * 2^-6). */
+int ou_conv_pack_split(const float* w_logical, int m, int cin_eff, int kt,
+                       float* packed, float* w_unscale);
 int ou_conv(const ou_conv_desc* d, void* stream);
 /* The tile configuration ou_conv would use for this descriptor when
  * d->tile < 0; ou_conv_num_tiles() configurations exist, ou_conv_tile_ok()

@@ -12,7 +12,7 @@ from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OUHIP_LIB", os.path.join(_HERE, "libouhip.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 fp = c_void_p  # device pointers are passed as integers
 
@@ -36,7 +36,8 @@ class ConvDesc(ctypes.Structure):
         ("res1", fp), ("r1_bstride", c_int64), ("r1_cstride", c_int64), ("s1", c_float),
         ("film", fp), ("film_bstride", c_int64),
         ("res2", fp), ("r2_bstride", c_int64), ("r2_cstride", c_int64), ("s2", c_float),
-        ("tile", c_int32), ("_reserved", c_int32),
+        ("tile", c_int32), ("prec", c_int32), ("w_unscale", c_float), ("_reserved", c_int32),
+        ("status", fp), ("amax_out", fp), ("amax_in", fp),
     ]
 
 
@@ -132,6 +133,8 @@ EXPORTS = {
     "ou_conv_chunk": (c_int, [c_int, c_int]),
     "ou_conv_packed_size": (c_int64, [c_int, c_int, c_int, c_int]),
     "ou_conv_pack": (c_int, [POINTER(c_float), c_int, c_int, c_int, c_int, POINTER(c_float)]),
+    "ou_conv_pack_split": (c_int, [POINTER(c_float), c_int, c_int, c_int, POINTER(c_float),
+                                   POINTER(c_float)]),
     "ou_conv": (c_int, [POINTER(ConvDesc), c_void_p]),
     "ou_conv_pick_tile": (c_int, [POINTER(ConvDesc)]),
     "ou_conv_num_tiles": (c_int, []),
@@ -168,6 +171,11 @@ _lib = None
 
 class OuHipError(RuntimeError):
     pass
+
+
+class OuRangeError(OuHipError):
+    """A split-f16 conv saw an input outside its range (|x| >= 2^21): the
+    result of that launch is not valid; rerun with f32 operands."""
 
 
 def load():
@@ -211,6 +219,21 @@ def conv_pack(w_logical, cc):
     check(load().ou_conv_pack(w.ctypes.data_as(POINTER(c_float)), m, cin, kt, cc,
                               out.ctypes.data_as(POINTER(c_float))), "conv_pack")
     return out
+
+
+def conv_pack_split(w_logical):
+    """Split-f16 packing (ConvDesc.prec = 1): returns (packed, w_unscale)."""
+    import numpy as np
+
+    w = np.ascontiguousarray(w_logical, dtype=np.float32)
+    m, cin, kt = w.shape
+    n = load().ou_conv_packed_size(m, cin, kt, 0)
+    out = np.empty(n, dtype=np.float32)
+    un = c_float(0.0)
+    check(load().ou_conv_pack_split(w.ctypes.data_as(POINTER(c_float)), m, cin, kt,
+                                    out.ctypes.data_as(POINTER(c_float)), ctypes.byref(un)),
+          "conv_pack_split")
+    return out, float(un.value)
 
 
 # Optional per-layer tile autotuner for ou_conv (set by the engine on a GPU):

@@ -38,6 +38,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 
@@ -52,7 +53,9 @@ constexpr int kCinAlign = 64;   // packed weights pad the channel axis to this
 
 // Tile: 4 waves as WM x WN x WK; each wave owns MR x NR MFMA tiles of 32 x 32
 // (register blocking) over its share (1/WK) of every K chunk.
-template <int KT, int CC, int WM, int WN, int WK, int MR, int NR>
+// P = 0: f32 operands (v_mfma_f32_32x32x2_f32).  P = 1: split-f16 operands
+// (v_mfma_f32_32x32x16_f16, three passes per k-step, see conv_kernel).
+template <int KT, int CC, int WM, int WN, int WK, int MR, int NR, int P = 0>
 struct Cfg {
     static constexpr int BM = 32 * WM * MR;
     static constexpr int BN = 32 * NR * WN;
@@ -60,7 +63,11 @@ struct Cfg {
     static constexpr int HALF = CC / 2;              // channel pairs per chunk
     static constexpr int HQ = HALF / 4;              // 4-pair groups per chunk
     static constexpr int CPW = HQ / WK;              // 4-pair groups per wave
-    static constexpr int SX = CC + 4;                // X row stride (floats): SX/4 odd
+    static constexpr int HQ8 = HALF / 8;             // P: 8-pair groups per chunk (one f16 k-step)
+    static constexpr int CPW8 = P ? HQ8 / WK : 0;     // P: 8-pair groups per wave
+    // X row stride in elements: f32 CC + 4 (SX/4 odd), f16 CC + 8 (SX/8 odd);
+    // the f16 image holds two planes (hi, lo) of W * SX halves = W * SX floats
+    static constexpr int SX = P ? CC + 8 : CC + 4;
     static constexpr int XG = W * CC / 4;            // float4 groups of X per chunk
     static constexpr int XE = (XG + 255) / 256;      // per thread
     static constexpr int AG = WM * MR * HQ * KT * 64;  // float4 of A per chunk
@@ -118,14 +125,43 @@ __device__ uint64_t g_conv_stamps[kStampWGs * kStampPhases];
 //   A  [m-tile][p / 4][tap][lane][p % 4]  (the packed global order, copied)
 // so one ds_read_b128 gives a lane the operands of 4 consecutive k-steps
 // (channel pairs p .. p+3 at one tap) for both A and B, conflict-free.
-template <int KT, int CC, int WM, int WN, int WK, int MR, int NR>
+//
+// Split-f16 form (P = 1).  Every operand is split as v = hi + lo * 2^-11 with
+// hi = f16(v) and lo = f16((v - hi) * 2^11) (the weights on the host, the
+// PReLU'd input while it is staged), and the product is taken as
+//   a b ~= ha hb + (ha lb + la hb) * 2^-11        (la lb ~ 2^-22 |a b| dropped)
+// on v_mfma_f32_32x32x16_f16: exact f16 products, f32 accumulation, the main
+// and the cross terms in two accumulators that are combined (exact powers of
+// two) before the epilogue.  Representation error ~2^-22 relative, i.e. f32
+// class (the f32 MFMA rounds at 2^-24), at 3 x 32 instead of 8 x 64 MFMA
+// cycles per 16 k-steps.  The weights carry a per-layer power-of-two scale
+// (d.w_unscale undoes it) that keeps them in f16's normal range; the staged
+// activations must stay below 2^15 in magnitude (the engine keeps the f32
+// form for the STFT and mel layers, whose inputs are unbounded powers).
+// LDS planes: X [frame][h * HALF + p] of hi, then of lo (halves); A the packed
+// global order [m-tile][8-pair group][hi | lo][tap][lane][8 halves].
+// Input exponent.  The input is staged as x * 2^-s (exact).  By default
+// s = kSplitShift: |x| < 2^21 stays in f16's range, |x| >= 2^-8 keeps the full
+// 2^-22 relative precision and smaller values an absolute error <= 2^-29.
+// With d.amax_in (the running max |x| its producing conv recorded, times 4
+// for writers the slot does not see) s puts that bound just below 2^15
+// instead (the atomics cost 1-11 us per producing launch, so the engine
+// enables it only on request).  A staged |x| >= 2^15 sets *d.status: the host
+// reruns the enhance with f32 operands.
+constexpr int kSplitShift = 6;
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+
+template <int KT, int CC, int WM, int WN, int WK, int MR, int NR, int P = 0>
 __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, int mtiles,
                                                    int64_t a_mt_stride)
 {
-    using C = Cfg<KT, CC, WM, WN, WK, MR, NR>;
+    using C = Cfg<KT, CC, WM, WN, WK, MR, NR, P>;
     static_assert(CC % 8 == 0 && C::HQ % WK == 0, "chunk must split into 4-pair groups per wave");
     static_assert(WM * WN * WK == 4, "4 waves per workgroup");
-    static_assert((C::SX / 4) % 2 == 1, "X row stride must be an odd number of 16-B slots");
+    static_assert(P || (C::SX / 4) % 2 == 1, "X row stride must be an odd number of 16-B slots");
+    static_assert(!P || (CC % 16 == 0 && C::HQ8 % WK == 0 && (C::SX / 8) % 2 == 1),
+                  "split-f16: chunk must split into 8-pair groups per wave, odd 16-B row stride");
     OU_DYNAMIC_LDS(float4, lds4);
     float* lds = (float*)lds4;
 
@@ -146,6 +182,22 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const int xc = (int)d.x_cstride;
     const float* xb = d.x + (int64_t)b * d.x_bstride;
     const float scale = d.in_scale ? d.in_scale[b] : 1.0f;
+    float xsc = 1.f / (1 << kSplitShift), su = d.w_unscale;   // split-f16 staging / result scales
+    if constexpr (P) {
+        if (d.amax_in) {
+            float mx = 0.f;
+#pragma unroll 8
+            for (int i = 0; i < 64; ++i) mx = fmaxf(mx, d.amax_in[i]);
+            mx *= 4.f * fmaxf(1.f, fabsf(d.slope)) * fabsf(scale);
+            if (mx > 0.f) {
+                int ex = 0;
+                frexpf(mx, &ex);                          // mx < 2^ex
+                const int sh = min(60, max(-60, ex - 15));
+                xsc = ldexpf(1.f, -sh);
+                su = d.w_unscale * ldexpf(1.f, sh - kSplitShift);
+            }
+        }
+    }
     const float slope = d.slope;
     const int t0 = n0 - d.pad;
 
@@ -246,21 +298,46 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 #define OU_STORE_CHUNK(buf)                                                                    \
     {                                                                                          \
         float* xs_ = lds + (buf) * C::STAGE;                                                   \
-        _Pragma("unroll") for (int e = 0; e < C::XE; ++e) if (xdst[e] >= 0)                    \
-            *(float4*)(xs_ + xdst[e]) = make_float4(OU_PRELU(xr[4 * e]), OU_PRELU(xr[4 * e + 1]), \
-                                                    OU_PRELU(xr[4 * e + 2]), OU_PRELU(xr[4 * e + 3])); \
+        if constexpr (P) {                                                                     \
+            _Float16* xh_ = (_Float16*)xs_;                                                    \
+            _Pragma("unroll") for (int e = 0; e < C::XE; ++e) if (xdst[e] >= 0) {              \
+                half4_t hi_, lo_;                                                              \
+                _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                \
+                    const float v_ = OU_PRELU(xr[4 * e + j]) * xsc;                           \
+                    ovf |= !(__builtin_fabsf(v_) < 32768.f);                                   \
+                    hi_[j] = (_Float16)v_;                                                     \
+                    lo_[j] = (_Float16)((v_ - (float)hi_[j]) * 2048.f);                        \
+                }                                                                              \
+                *(half4_t*)(xh_ + xdst[e]) = hi_;                                              \
+                *(half4_t*)(xh_ + C::W * C::SX + xdst[e]) = lo_;                               \
+            }                                                                                  \
+        } else {                                                                               \
+            _Pragma("unroll") for (int e = 0; e < C::XE; ++e) if (xdst[e] >= 0)                \
+                *(float4*)(xs_ + xdst[e]) = make_float4(OU_PRELU(xr[4 * e]), OU_PRELU(xr[4 * e + 1]), \
+                                                        OU_PRELU(xr[4 * e + 2]), OU_PRELU(xr[4 * e + 3])); \
+        }                                                                                      \
         float4* as_ = (float4*)(xs_ + C::XBUF);                                                \
         _Pragma("unroll") for (int e = 0; e < C::AE; ++e) if (C::AG % 256 == 0 || tid + e * 256 < C::AG) \
             as_[tid + e * 256] = make_float4(ar[4 * e], ar[4 * e + 1], ar[4 * e + 2], ar[4 * e + 3]); \
     }
 
     floatx16 acc[MR][NR];
+    floatx16 accx[P ? MR : 1][P ? NR : 1];   // split-f16 cross terms
+    bool ovf = false;                        // split-f16: staged input out of range
 #pragma unroll
     for (int i = 0; i < MR; ++i)
 #pragma unroll
         for (int j = 0; j < NR; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    if constexpr (P) {
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) accx[i][j][r] = 0.f;
+    }
 
     OU_CSTAMP_INIT
     OU_LOAD_CHUNK(0);
@@ -271,7 +348,43 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
         const int cur = q & 1;
         if (q + 1 < nchunks) OU_LOAD_CHUNK(q + 1);
         OU_CSTAMP(1);
-        {
+        if constexpr (P) {
+            // one step = 8 channel pairs (16 k) at one tap: 3 f16 MFMAs per
+            // (mr, nr); fragments of step s + 1 are read during step s
+            const _Float16* xh = (const _Float16*)(lds + cur * C::STAGE);
+            const half8_t* ap = (const half8_t*)(lds + cur * C::STAGE + C::XBUF) +
+                                ((wm * MR) * C::HQ + wk * C::CPW8 * 2) * KT * 64 + lane;
+            const _Float16* xp = xh + (wn * 32 * NR + l32) * C::SX + h * C::HALF + 8 * wk * C::CPW8;
+            constexpr int NS = C::CPW8 * KT;
+            half8_t fa[2][MR], fal[2][MR], fb[2][NR], fbl[2][NR];
+            auto frag = [&](int st, half8_t* a, half8_t* al, half8_t* bq, half8_t* bl) {
+                const int c8 = st / KT, k = st - (st / KT) * KT;
+#pragma unroll
+                for (int mr = 0; mr < MR; ++mr) {
+                    a[mr] = ap[(mr * C::HQ * KT + (c8 * 2) * KT + k) * 64];
+                    al[mr] = ap[(mr * C::HQ * KT + (c8 * 2 + 1) * KT + k) * 64];
+                }
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr) {
+                    bq[nr] = *(const half8_t*)(xp + (nr * 32 + k) * C::SX + 8 * c8);
+                    bl[nr] = *(const half8_t*)(xp + C::W * C::SX + (nr * 32 + k) * C::SX + 8 * c8);
+                }
+            };
+            frag(0, fa[0], fal[0], fb[0], fbl[0]);
+#pragma unroll
+            for (int st = 0; st < NS; ++st) {
+                const int c = st & 1, n = c ^ 1;
+                if (st + 1 < NS) frag(st + 1, fa[n], fal[n], fb[n], fbl[n]);
+#pragma unroll
+                for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                    for (int nr = 0; nr < NR; ++nr) {
+                        acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[c][mr], fb[c][nr], acc[mr][nr], 0, 0, 0);
+                        accx[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[c][mr], fbl[c][nr], accx[mr][nr], 0, 0, 0);
+                        accx[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[c][mr], fb[c][nr], accx[mr][nr], 0, 0, 0);
+                    }
+            }
+        } else {
             const float* xs = lds + cur * C::STAGE;
             const float4* ap = (const float4*)(xs + C::XBUF) +
                                ((wm * MR) * C::HQ + wk * C::CPW) * KT * 64 + lane;
@@ -311,6 +424,16 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 #undef OU_LOAD_CHUNK
 #undef OU_STORE_CHUNK
 #undef OU_PRELU
+    if constexpr (P) {   // range flag, then combine the split-f16 terms (exact powers of two)
+        if (__any(ovf) && lane == 0 && d.status) atomicOr(d.status, 1);
+        const float sx = su * (1.f / 2048.f);
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = fmaf(accx[i][j][r], sx, acc[i][j][r] * su);
+    }
 
     // ---- intra-workgroup split-K reduction (fixed order: deterministic) ----
     if (WK > 1) {
@@ -362,6 +485,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
     const __amdgpu_buffer_rsrc_t fs = ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y,
                                               has_fm ? (int64_t)cout * 8 : 0);
+    float ymax = 0.f;   // max |stored y| of this wave (d.amax_out)
 #pragma unroll
     for (int mr = 0; mr < MR; ++mr) {
         const int mt = mt0 + wm * MR + mr;
@@ -432,10 +556,17 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
                 v = (v + v1[r]) * s1e;
                 v = (fa[r] + fadd) * v + fb[r];
                 v = (v + v2[r]) * s2e;
+                ymax = fmaxf(ymax, off[r] >= 0 ? fabsf(v) : 0.f);
                 __builtin_amdgcn_raw_buffer_store_b32(
                     __float_as_uint(v), ys, off[r] >= 0 ? (co[r] * (int)d.y_cstride + off[r]) * 4 : kSentinel, 0, 0);
             }
         }
+    }
+    if (d.amax_out) {   // wave max, then one atomic per wave into 64 spread slots
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) ymax = fmaxf(ymax, __shfl_xor(ymax, o));
+        if (lane == 0)
+            atomicMax((unsigned int*)d.amax_out + ((blockIdx.x + blockIdx.y + blockIdx.z) & 63), __float_as_uint(ymax));
     }
     OU_CSTAMP(5);
     OU_CSTAMP_SAVE;
@@ -1193,10 +1324,11 @@ constexpr int kLdsTwoPerCu = 80 * 1024; // fits two workgroups per CU
 
 // channel chunk: the largest of 64/32/16/8 that splits over the K waves and
 // whose double-buffered stage fits two workgroups per CU, else one per CU
-template <int KT, int WM, int WN, int WK, int MR, int NR, int CC>
+template <int KT, int WM, int WN, int WK, int MR, int NR, int CC, int P = 0>
 constexpr bool chunk_ok(int budget)
 {
-    return CC / 8 % WK == 0 && Cfg<KT, CC, WM, WN, WK, MR, NR>::LDS2 * 4 <= budget;
+    return CC / 8 % WK == 0 && (!P || (CC % 16 == 0 && CC / 16 % WK == 0)) &&
+           Cfg<KT, CC, WM, WN, WK, MR, NR, P>::LDS2 * 4 <= budget;
 }
 template <int KT, int WM, int WN, int WK, int MR, int NR, int BIG>
 constexpr int chunk_for()
@@ -1214,6 +1346,28 @@ constexpr int chunk_for()
                                                                 : 8 * WK;
 }
 
+// split-f16 chunk (8-pair groups per wave, 16-B aligned half rows); 0 when the
+// shape has no split-f16 form
+template <int KT, int WM, int WN, int WK, int MR, int NR, int BIG>
+constexpr int chunk_for_split()
+{
+    constexpr int b1 = BIG ? kMaxLds : kLdsTwoPerCu;
+    return chunk_ok<KT, WM, WN, WK, MR, NR, 64, 1>(b1)        ? 64
+           : chunk_ok<KT, WM, WN, WK, MR, NR, 32, 1>(b1)      ? 32
+           : chunk_ok<KT, WM, WN, WK, MR, NR, 16, 1>(b1)      ? 16
+           : chunk_ok<KT, WM, WN, WK, MR, NR, 64, 1>(kMaxLds) ? 64
+           : chunk_ok<KT, WM, WN, WK, MR, NR, 32, 1>(kMaxLds) ? 32
+           : chunk_ok<KT, WM, WN, WK, MR, NR, 16, 1>(kMaxLds) ? 16
+                                                              : 0;
+}
+template <int KT, int WM, int WN, int WK, int MR, int NR, int BIG>
+constexpr int lds_bytes_split_t()
+{
+    constexpr int CC = chunk_for_split<KT, WM, WN, WK, MR, NR, BIG>();
+    if constexpr (CC == 0) return -1;
+    else return Cfg<KT, CC, WM, WN, WK, MR, NR, 1>::LDS2 * 4;
+}
+
 template <int KT, int WM, int WN, int WK, int MR, int NR, int BIG>
 constexpr int lds_bytes_t()
 {
@@ -1221,11 +1375,16 @@ constexpr int lds_bytes_t()
     return Cfg<KT, CC, WM, WN, WK, MR, NR>::LDS2 * 4;
 }
 
-template <int KT, int WM, int WN, int WK, int MR, int NR, int BIG>
+template <int KT, int WM, int WN, int WK, int MR, int NR, int BIG, int P = 0>
 int launch_t(const ou_conv_desc& d, int tpw, hipStream_t s)
 {
-    constexpr int CC = chunk_for<KT, WM, WN, WK, MR, NR, BIG>();
-    using C = Cfg<KT, CC, WM, WN, WK, MR, NR>;
+    constexpr int CC = P ? chunk_for_split<KT, WM, WN, WK, MR, NR, BIG>() : chunk_for<KT, WM, WN, WK, MR, NR, BIG>();
+    if constexpr (CC == 0) {
+        (void)tpw;
+        (void)s;
+        return ou_fail(-2, "conv: tile shape has no split-f16 form (m %d, kt %d)", d.m, d.kt);
+    } else {
+    using C = Cfg<KT, CC, WM, WN, WK, MR, NR, P>;
     const int mtiles = (d.m + 31) / 32;
     const int cin_eff = d.cin * d.frame;
     const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
@@ -1234,7 +1393,7 @@ int launch_t(const ou_conv_desc& d, int tpw, hipStream_t s)
     (void)tpw;   // one output tile per workgroup
     dim3 grid((d.n_frames + C::BN - 1) / C::BN, (mtiles + WM * MR - 1) / (WM * MR), d.batch);
     const int lds = (nchunks > 1 ? C::LDS2 : C::LDS1) * (int)sizeof(float);
-    auto kern = conv_kernel<KT, CC, WM, WN, WK, MR, NR>;
+    auto kern = conv_kernel<KT, CC, WM, WN, WK, MR, NR, P>;
     static bool attr = false;   // opt in to more than 64 KiB of dynamic LDS, once
     if (!attr && C::LDS2 * 4 > 64 * 1024) {
         OU_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1244,6 +1403,7 @@ int launch_t(const ou_conv_desc& d, int tpw, hipStream_t s)
     }
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, d, nchunks, mtiles, a_mt_stride);
     return ou_check_launch("conv");
+    }
 }
 
 // persistent launch: ceil(tiles / tpw) workgroups, each walking tpw tiles
@@ -1342,10 +1502,19 @@ int launch_w(const ou_conv_desc& d, hipStream_t s)
 }
 
 constexpr int kWsBit = 1 << 10;   // tile bit: warp-specialised persistent kernel
+constexpr int kSplitBit = 1 << 11;   // tile-query bit (LDS size, tile_ok): the split-f16 kernel
 
 template <int KT>
 int lds_bytes_kt(int tile)
 {
+    if (tile & kSplitBit) {
+        switch (tile & 0xff) {
+#define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) case id: return lds_bytes_split_t<KT, wm, wn, wk, mr, nr, big>();
+            OU_TILES(OU_TILE_CASE)
+#undef OU_TILE_CASE
+        }
+        return -1;
+    }
     if (tile & kWsBit) {
         switch (tile & 0xff) {
 #define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) \
@@ -1367,6 +1536,14 @@ int lds_bytes_kt(int tile)
 template <int KT>
 int launch_kt(const ou_conv_desc& d, int tile, int tpw, bool ws, hipStream_t s)
 {
+    if (d.prec == 1) {   // split-f16: one-tile workgroups (checked by ou_conv)
+        switch (tile) {
+#define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) case id: return launch_t<KT, wm, wn, wk, mr, nr, big, 1>(d, 1, s);
+            OU_TILES(OU_TILE_CASE)
+#undef OU_TILE_CASE
+        }
+        return ou_fail(-2, "conv: bad tile %d", tile);
+    }
     if (ws) {
         switch (tile) {
 #define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) \
@@ -1451,6 +1628,16 @@ int lds_bytes(int kt, int tile)
     }
     return -1;
 }
+
+// static choice for a precision: the split-f16 form lacks some shapes (LDS)
+int pick_tile_for(const ou_conv_desc& d)
+{
+    const int t = pick_tile(d);
+    if (d.prec != 1 || lds_bytes(d.kt, t | kSplitBit) > 0) return t;
+    for (int c : {11, 3, 6, 5, 1, 0, 10, 8, 2, 4, 7, 12})
+        if (lds_bytes(d.kt, c | kSplitBit) > 0) return c;
+    return t;
+}
 }  // namespace
 
 extern "C" int ou_conv_chunk(int kt, int frame)
@@ -1491,6 +1678,46 @@ extern "C" int ou_conv_pack(const float* w, int m, int cin_eff, int kt, int cc, 
     return 0;
 }
 
+// Split-f16 packing (include/ouhip.h): [m-tile][8-pair group][hi | lo][tap]
+// [lane][8 halves] of a = w * 2^e; the same byte count per K chunk as the f32
+// packing, so the kernel's chunk addressing is unchanged.
+extern "C" int ou_conv_pack_split(const float* w, int m, int cin_eff, int kt, float* out, float* w_unscale)
+{
+    if (!w || !out || !w_unscale || m <= 0 || cin_eff <= 0 || kt <= 0)
+        return ou_fail(-1, "conv_pack_split: bad arguments");
+    const int64_t n = (int64_t)m * cin_eff * kt;
+    float mx = 0.f;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!std::isfinite(w[i])) return ou_fail(-1, "conv_pack_split: non-finite weight at %lld", (long long)i);
+        mx = std::max(mx, std::fabs(w[i]));
+    }
+    int e = 0;
+    if (mx > 0.f) {
+        int ex = 0;
+        std::frexp(mx, &ex);                  // mx in [2^(ex-1), 2^ex)
+        e = std::min(100, std::max(-100, 10 - ex));   // max|a| in [2^9, 2^10)
+    }
+    const float sc = std::ldexp(1.f, e);
+    const int mtiles = (m + 31) / 32;
+    const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
+    _Float16* o = (_Float16*)out;
+    for (int mt = 0; mt < mtiles; ++mt)
+        for (int g = 0; g < cin_pad / 16; ++g)
+            for (int part = 0; part < 2; ++part)
+                for (int k = 0; k < kt; ++k)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int j = 0; j < 8; ++j) {
+                            const int row = mt * 32 + (lane & 31);
+                            const int c = 2 * (8 * g + j) + (lane >> 5);
+                            const float a =
+                                (row < m && c < cin_eff) ? w[((int64_t)row * cin_eff + c) * kt + k] * sc : 0.f;
+                            const _Float16 hi = (_Float16)a;
+                            *o++ = part == 0 ? hi : (_Float16)((a - (float)hi) * 2048.f);
+                        }
+    *w_unscale = std::ldexp(1.f, kSplitShift - e);
+    return 0;
+}
+
 extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
 {
     if (!dp) return ou_fail(-1, "conv: null descriptor");
@@ -1501,11 +1728,18 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     // d.tile: bits 0-7 tile shape (kTiles), bits 8-9 log2(output tiles per
     // workgroup: > 1 selects the persistent kernel, shapes without split-K),
     // bit 10 the warp-specialised persistent kernel (shapes 0-12)
-    const int tile = d.tile >= 0 && (d.tile & 0xff) < kNumTiles ? (d.tile & 0xff) : pick_tile(d);
+    const int tile = d.tile >= 0 && (d.tile & 0xff) < kNumTiles ? (d.tile & 0xff) : pick_tile_for(d);
     const bool ws = d.tile >= 0 && (d.tile & kWsBit);
     const int tpw = d.tile >= 0 && !ws ? 1 << ((d.tile >> 8) & 3) : 1;
     if (ws && d.rout != 1) return ou_fail(-2, "conv: the warp-specialised kernel has no transposed (rout %d) form", d.rout);
-    const int lb = lds_bytes(d.kt, tile | (ws ? kWsBit : 0));
+    if (d.prec != 0 && d.prec != 1) return ou_fail(-1, "conv: bad precision %d", d.prec);
+    if (d.amax_out && (ws || tpw > 1))
+        return ou_fail(-2, "conv: amax_out needs the one-tile kernel (tile 0x%x)", d.tile);
+    if (d.prec == 1 && (ws || tpw > 1))
+        return ou_fail(-2, "conv: the split-f16 form has one-tile workgroups only (tile 0x%x)", d.tile);
+    if (d.prec == 1 && !(d.w_unscale > 0.f))
+        return ou_fail(-1, "conv: split-f16 needs the w_unscale of ou_conv_pack_split");
+    const int lb = lds_bytes(d.kt, tile | (ws ? kWsBit : 0) | (d.prec == 1 ? kSplitBit : 0));
     if (lb <= 0 || lb > kMaxLds)
         return ou_fail(-2, "conv: tile %d (ws %d) needs %d B of LDS for kt=%d", tile, (int)ws, lb, d.kt);
     hipStream_t s = (hipStream_t)stream;
@@ -1529,7 +1763,7 @@ extern "C" int ou_conv_read_stamps(uint64_t* host, int n)
 // per-workgroup LDS limit (diagnostics: tools/conv_bench.py --info)
 extern "C" int ou_conv_lds_info(int kt, int tile, int* lds_request, int* device_optin_max)
 {
-    if (lds_request) *lds_request = lds_bytes(kt, tile & (0xff | kWsBit));
+    if (lds_request) *lds_request = lds_bytes(kt, tile & (0xff | kWsBit | kSplitBit));
     int dev = 0, v = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -1;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess) return -1;
@@ -1537,10 +1771,16 @@ extern "C" int ou_conv_lds_info(int kt, int tile, int* lds_request, int* device_
     return 0;
 }
 
-extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile(*d) : -1; }
+extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile_for(*d) : -1; }
 extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int ou_conv_tile_ok(int kt, int tile)
 {
+    if (tile & kSplitBit) {   // split-f16 (d.prec = 1): one-tile workgroups, no other bits
+        if (tile & ~(kSplitBit | 0xff)) return 0;
+        if ((tile & 0xff) >= kNumTiles) return 0;
+        const int lb = lds_bytes(kt, tile);
+        return lb > 0 && lb <= kMaxLds;
+    }
     if (tile & kWsBit) {   // warp-specialised: shapes without the 'big' chunking, no tpw bits
         if (tile & ~(kWsBit | 0xff)) return 0;
         const int t = tile & 0xff;

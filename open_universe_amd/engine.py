@@ -24,6 +24,60 @@ from . import dsp
 
 NF2 = np.float32(1.0 / math.sqrt(2.0))
 
+# Operand precision of ou_conv (ConvDesc.prec): 1 = split-f16 (three f16 MFMA
+# passes on hi/lo operand halves, f32 accumulation, f32-class accuracy: see
+# csrc/ou_conv.hip), 0 = f32 MFMA.  OUHIP_CONV_PREC=f32|split picks the default
+# of every Engine; Engine(conv_prec=...) overrides it per model.
+_PREC_NAMES = {"f32": 0, "fp32": 0, "0": 0, "split": 1, "split16": 1, "1": 1}
+
+
+def default_conv_prec():
+    import os
+
+    v = os.environ.get("OUHIP_CONV_PREC", "split").strip().lower()
+    if v not in _PREC_NAMES:
+        raise ValueError(f"OUHIP_CONV_PREC={v!r}: expected f32 or split")
+    return _PREC_NAMES[v]
+
+
+_PREP_PREC = None     # set by Engine while it packs its weights
+_PREP_STATUS = 0      # device int32* the split-f16 convs flag range errors into
+
+# Optional per-tensor input exponents for split-f16 (OUHIP_SPLIT_AMAX=1): every
+# conv of a split engine records max |y| of what it stores (ConvDesc.amax_out,
+# one 64-float slot row per output buffer, zeroed by the plan's first op); a
+# split-f16 conv whose input buffer was produced by an earlier recorded conv
+# reads that row (amax_in) to pick its staging exponent.  Off by default: the
+# fixed exponent covers |x| < 2^21 (a range flag reruns anything beyond in
+# f32) and the atomics cost 1-11 us per launch (tools/conv_bench.py --amax).
+AMAX_SLOTS = 256
+_REC = None
+
+
+def split_amax_enabled():
+    import os
+
+    return os.environ.get("OUHIP_SPLIT_AMAX", "0") == "1"
+
+
+def begin_record(pool, prec):
+    global _REC
+    _REC = {"pool": pool, "slots": {}, "prec": prec} if prec == 1 and split_amax_enabled() else None
+
+
+def end_record():
+    global _REC
+    _REC = None
+
+
+def _amax_slot(act):
+    rec = _REC
+    i = rec["slots"].get(act.ptr)
+    if i is None:
+        i = rec["slots"][act.ptr] = len(rec["slots"])
+        assert i < AMAX_SLOTS, "amax slot pool exhausted"
+    return rec["pool"].data_ptr() + 4 * 64 * i
+
 
 # ---------------------------------------------------------------------------
 # weights
@@ -58,6 +112,9 @@ class ConvW:
     bias: Optional[torch.Tensor]
     shift: int = 0
     ref_macs: float = 0.0
+    prec: int = 0            # ConvDesc.prec the weights were packed for
+    w_unscale: float = 1.0   # split-f16 weight scale (ou_conv_pack_split)
+    status: int = 0          # device int32* for the split-f16 range flag (0 = none)
 
     @property
     def cout(self):
@@ -79,7 +136,11 @@ class ConvSpec:
     ref_macs: float = 0.0   # MACs of the replaced reference ops per output frame
 
 
-def make_conv(spec, device):
+def make_conv(spec, device, prec=None):
+    """prec: 0 f32 operands, 1 split-f16; None = the packing Engine's choice
+    (or OUHIP_CONV_PREC outside an Engine)."""
+    if prec is None:
+        prec = _PREP_PREC if _PREP_PREC is not None else default_conv_prec()
     w_logical = np.ascontiguousarray(spec.w, dtype=np.float32)
     m, cin_eff, kt = w_logical.shape
     assert cin_eff == spec.cin * spec.frame, (cin_eff, spec.cin, spec.frame)
@@ -88,10 +149,14 @@ def make_conv(spec, device):
         w_logical = np.ascontiguousarray(
             w_logical.reshape(m, spec.cin, spec.frame, kt).transpose(0, 2, 1, 3).reshape(m, cin_eff, kt))
     cc = L.conv_chunk(kt, spec.frame)
-    packed = torch.from_numpy(L.conv_pack(w_logical, cc)).to(device)
+    if prec == 1:
+        packed_np, unscale = L.conv_pack_split(w_logical)
+    else:
+        packed_np, unscale = L.conv_pack(w_logical, cc), 1.0
+    packed = torch.from_numpy(packed_np).to(device)
     b = None if spec.bias is None else torch.from_numpy(np.ascontiguousarray(spec.bias, np.float32)).to(device)
     return ConvW(m, spec.cin, kt, spec.frame, spec.pad, spec.rout, float(spec.slope), cc, packed, b,
-                 spec.shift, spec.ref_macs)
+                 spec.shift, spec.ref_macs, int(prec), float(unscale), _PREP_STATUS if prec == 1 else 0)
 
 
 def _slope(sd, p):
@@ -252,6 +317,11 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
     d.frame, d.shift = cw.frame, cw.shift
     d.in_scale, d.slope = in_scale or 0, cw.slope
     d.w, d.m, d.kt, d.pad, d.cc = cw.w.data_ptr(), cw.m, cw.kt, cw.pad, cw.cc
+    d.prec, d.w_unscale, d.status = cw.prec, cw.w_unscale, cw.status
+    if _REC is not None and _REC["prec"] == 1:
+        if cw.prec == 1 and x.ptr in _REC["slots"]:
+            d.amax_in = _amax_slot(x)
+        d.amax_out = _amax_slot(y)
     if n_frames is None:
         n_frames = -(-d.in_len // cw.frame) if cw.rout == 1 else x.T
     d.n_frames = n_frames
@@ -316,6 +386,8 @@ def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, re
     d.flags = GRU_FLAGS
     d._flops = 2.0 * 2 * 3 * H * H * x.T * x.B
     prog.add(L.OP_GRU, d)
+    if _REC is not None:   # y now holds GRU values its amax row has not seen
+        _REC["slots"].pop(y.ptr, None)
 
 
 def level_lengths(T, rates):
@@ -356,7 +428,8 @@ class ConvTuner:
     @staticmethod
     def key(d):
         return (d.m, d.cin, d.frame, d.kt, d.pad, d.n_frames, d.batch, d.rout, d.in_len,
-                d.out_len, bool(d.res1), bool(d.film), bool(d.res2), bool(d.in_scale))
+                d.out_len, bool(d.res1), bool(d.film), bool(d.res2), bool(d.in_scale), d.prec,
+                bool(d.amax_out))
 
     def __call__(self, d):
         import ctypes
@@ -370,9 +443,18 @@ class ConvTuner:
         best, best_ms = -1, float("inf")
         # tile shape x log2(output tiles per workgroup); > 0 = persistent kernel
         # (bit 10: the warp-specialised persistent kernel)
-        cands = [t | v for t in range(lib.ou_conv_num_tiles()) for v in (0, 1 << 8, 2 << 8, 1 << 10)
-                 if lib.ou_conv_tile_ok(d.kt, t | v)]
+        # (split-f16, bit 11 in the query only, and amax tracking: one-tile workgroups)
+        if d.prec == 1:
+            cands = [t for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))]
+        elif d.amax_out:
+            cands = [t for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t)]
+        else:
+            cands = [t | v for t in range(lib.ou_conv_num_tiles()) for v in (0, 1 << 8, 2 << 8, 1 << 10)
+                     if lib.ou_conv_tile_ok(d.kt, t | v)]
         log = os.environ.get("OUHIP_TUNE_LOG")
+        # candidates run on whatever the buffers hold at record time: keep
+        # their split-f16 range flags out of the engine's status word
+        status, d.status = d.status, None
         for t in cands:
             d.tile = t
             if log:   # diagnostics: name every candidate before it runs
@@ -400,6 +482,7 @@ class ConvTuner:
             if ms < best_ms:
                 best, best_ms = t, ms
         d.tile = -1
+        d.status = status
         self.cache[k] = best
         self._save()
         return best
@@ -424,8 +507,11 @@ def enable_autotune(flag=True):
 # engine
 # ---------------------------------------------------------------------------
 class Engine:
-    def __init__(self, model_cfg, sd, device, parts=("score", "cond", "sdl"), _record_only=False):
+    def __init__(self, model_cfg, sd, device, parts=("score", "cond", "sdl"), _record_only=False,
+                 conv_prec=None):
+        global _PREP_PREC, _PREP_STATUS
         self.device = torch.device(device)
+        self.conv_prec = default_conv_prec() if conv_prec is None else int(conv_prec)
         if self.device.type != "cuda" and not _record_only:
             raise L.OuHipError("open_universe_amd runs on a HIP device (got %s)" % device)
         L.load()
@@ -444,14 +530,20 @@ class Engine:
         sp = "_edm_model" if self.edm is not None else "score_model"
         dev = self.device
         self.has_sdl = False
-        with torch.no_grad():
-            if "score" in parts:
-                self._prep_score(sd, sp, dev)
-            if "cond" in parts:
-                self._prep_cond(sd, "condition_model", dev)
-            if "sdl" in parts:
-                self._prep_sdl(sd, "signal_decoupling_layer", dev)
+        # [0] GRU hand-off timeout, [1] split-f16 conv range error (plan.check)
         self.status = torch.zeros(4, dtype=torch.int32, device=dev)
+        saved = _PREP_PREC, _PREP_STATUS
+        _PREP_PREC, _PREP_STATUS = self.conv_prec, self.status.data_ptr() + 4
+        try:
+            with torch.no_grad():
+                if "score" in parts:
+                    self._prep_score(sd, sp, dev)
+                if "cond" in parts:
+                    self._prep_cond(sd, "condition_model", dev)
+                if "sdl" in parts:
+                    self._prep_sdl(sd, "signal_decoupling_layer", dev)
+        finally:
+            _PREP_PREC, _PREP_STATUS = saved
         enable_autotune(self.device.type == "cuda")
 
     # -------------------------------------------------------------- weights
@@ -534,9 +626,11 @@ class Engine:
         kt = n_fft // ds
         # w_logical[m][p][kk] = dft[m][kk*hop + p]
         wl = dft.reshape(2 * nfreq, kt, ds).transpose(0, 2, 1)
-        self.c_stft = make_conv(ConvSpec(wl, 1, ds, 0, 1, 1.0, None, shift=-self.mel_pl), dev)
+        # the STFT and the filterbank keep f32 operands: |STFT|^2 is unbounded
+        # (split-f16 staging needs |x| < 2^15)
+        self.c_stft = make_conv(ConvSpec(wl, 1, ds, 0, 1, 1.0, None, shift=-self.mel_pl), dev, prec=0)
         fb = dsp.melscale_fbanks(nfreq, 0.0, float(24000 // 2), self.mel_nmels, 24000)
-        self.c_fb = make_conv(ConvSpec(fb.T[:, :, None], nfreq, 1, 0, 1, 1.0, None), dev)
+        self.c_fb = make_conv(ConvSpec(fb.T[:, :, None], nfreq, 1, 0, 1, 1.0, None), dev, prec=0)
         self.c_melconv = prep_plain(sd, p + ".input_mel.conv", 3, dev)
         self.c_melblock = prep_block(sd, p + ".input_mel.conv_block", "none", None, False, dev)
         self.c_input = prep_plain(sd, p + ".input_conv", cfg.get("fb_kernel_size", 3), dev)

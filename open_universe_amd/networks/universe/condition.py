@@ -9,6 +9,7 @@ import math
 import torch
 from torch import nn
 
+from ... import _lib as L
 from ... import dsp
 from .blocks import ConvBlock, GRUParams, PReLU_Conv, conv_params
 
@@ -146,6 +147,7 @@ class ConditionerNetwork(nn.Module):
         self.precoding = None
         self._engine = None
         self._plans = {}
+        self._conv_prec = None   # None: OUHIP_CONV_PREC; 0 after a split-f16 range error
 
     def _get_engine(self):
         from ...engine import Engine
@@ -154,7 +156,7 @@ class ConditionerNetwork(nn.Module):
         if self._engine is None or self._engine.device != dev:
             cfg = {"score_model": None, "condition_model": self.config, "diffusion": None}
             sd = {"condition_model." + k: v for k, v in self.state_dict().items()}
-            self._engine = Engine(cfg, sd, dev, parts=("cond",))
+            self._engine = Engine(cfg, sd, dev, parts=("cond",), conv_prec=self._conv_prec)
             self._plans = {}
         return self._engine
 
@@ -174,7 +176,11 @@ class ConditionerNetwork(nn.Module):
         key = (B, T)
         if key not in self._plans:
             self._plans[key] = CondPlan(eng, B, T, need_aux=True)
-        conds, y, h = self._plans[key](x)
+        try:
+            conds, y, h = self._plans[key](x)
+        except L.OuRangeError:   # activations left the split-f16 range: f32 operands from now on
+            self._conv_prec, self._engine, self._plans = 0, None, {}
+            return self.forward(x, x_wav, train)
         conds = [c.clone() for c in conds]
         if train:
             return conds, y.clone(), h.clone()

@@ -9,6 +9,7 @@ import copy
 import torch
 from torch import nn
 
+from ... import _lib as L
 from .blocks import ConvBlock, GRUParams, PReLU, PReLU_Conv, conv_params, linear_params
 from .sigma_block import SigmaBlock, SimpleTimeEmbedding
 
@@ -101,6 +102,7 @@ class ScoreNetwork(nn.Module):
         self.precoding = None
         self._engine = None
         self._plans = {}
+        self._conv_prec = None   # None: OUHIP_CONV_PREC; 0 after a split-f16 range error
 
     def _get_engine(self):
         from ...engine import Engine
@@ -109,7 +111,7 @@ class ScoreNetwork(nn.Module):
         if self._engine is None or self._engine.device != dev:
             cfg = {"score_model": self.config, "condition_model": None, "diffusion": None}
             sd = {"score_model." + k: v for k, v in self.state_dict().items()}
-            self._engine = Engine(cfg, sd, dev, parts=("score",))
+            self._engine = Engine(cfg, sd, dev, parts=("score",), conv_prec=self._conv_prec)
             self._plans = {}
         return self._engine
 
@@ -127,4 +129,8 @@ class ScoreNetwork(nn.Module):
         key = (B, T)
         if key not in self._plans:
             self._plans[key] = ScorePlan(eng, B, T)
-        return self._plans[key](x, sigma, cond).clone()
+        try:
+            return self._plans[key](x, sigma, cond).clone()
+        except L.OuRangeError:   # activations left the split-f16 range: f32 operands from now on
+            self._conv_prec, self._engine, self._plans = 0, None, {}
+            return self.forward(x, sigma, cond)

@@ -23,6 +23,7 @@ from typing import Optional
 import torch
 from torch import nn
 
+from ... import _lib as L
 from .blocks import PReLU_Conv
 from .condition import ConditionerNetwork
 from .score import ScoreNetwork
@@ -81,6 +82,7 @@ class Universe(nn.Module):
         self.ema = None  # EMA weights are applied at load time (inference only)
         self._engine = None
         self._plans = {}
+        self._conv_prec = None   # None: OUHIP_CONV_PREC; 0 after a split-f16 range error
 
     def init_losses(self, score_model, condition_model, losses, training):
         """Training losses are out of scope; nothing to build for Universe."""
@@ -111,7 +113,7 @@ class Universe(nn.Module):
 
         dev = next(self.parameters()).device
         if self._engine is None or self._engine.device != dev:
-            self._engine = Engine(self._model_cfg(), self.state_dict(), dev)
+            self._engine = Engine(self._model_cfg(), self.state_dict(), dev, conv_prec=self._conv_prec)
             self._plans = {}
         return self._engine
 
@@ -198,14 +200,25 @@ class Universe(nn.Module):
             ens_mode = {"mean": 0, "median": 1}.get(ensemble_stat) if ensemble is not None else None
             key = (B, T, int(n_steps), float(epsilon), bool(keep_rms), bool(use_aux_signal),
                    warm_start, ensemble, ens_mode)
-            plan = self._plans.get(key)
-            if plan is None:
-                plan = EnhancePlan(eng, B, T, int(n_steps), float(epsilon), keep_rms=bool(keep_rms),
+            def make_plan(eng):
+                return EnhancePlan(eng, B, T, int(n_steps), float(epsilon), keep_rms=bool(keep_rms),
                                    use_aux_signal=bool(use_aux_signal), warm_start=warm_start,
                                    diff=dict(self.diff_kwargs), ensemble=ensemble,
                                    ensemble_mode=ens_mode)
-                self._plans[key] = plan
-            x = plan(mix, rng).clone()[:, None, :]
+
+            plan = self._plans.get(key)
+            if plan is None:
+                plan = self._plans[key] = make_plan(eng)
+            try:
+                x = plan(mix, rng).clone()[:, None, :]
+            except L.OuRangeError:
+                # a split-f16 conv input left its range (|x| >= 2^21): switch
+                # this model to f32 operands and rerun on the same noise
+                nz = plan.NZ.clone()
+                self._conv_prec = 0
+                self.invalidate()
+                plan = self._plans[key] = make_plan(self._get_engine())
+                x = plan.run_with_noise(mix, nz).clone()[:, None, :]
             if ensemble is not None and ens_mode is None:
                 x = self._ensemble_reduce(x.view((-1,) + tuple(mix_shape)), ensemble_stat)
         if x_ndim == 1:

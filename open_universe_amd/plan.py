@@ -16,6 +16,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from . import engine as E
 from .engine import Act, new_act
 
 f32 = np.float32
@@ -51,6 +52,27 @@ class _PlanBase:
         self.eng = eng
         self.dev = eng.device
         self.prog = L.Program()
+        # split-f16 input exponents (engine.begin_record): slot rows zeroed
+        # by the first op of every launch
+        self.amax = None
+        if eng.conv_prec == 1 and E.split_amax_enabled():
+            self.amax = torch.zeros((E.AMAX_SLOTS, 64), dtype=torch.float32, device=self.dev)
+            self.prog.add(L.OP_MEMSET, L.MemsetArgs(ptr=self.amax.data_ptr(), bytes=self.amax.numel() * 4))
+        E.begin_record(self.amax, eng.conv_prec)
+
+    def __init_subclass__(cls, **kw):
+        # every subclass records in its __init__: close the recording context
+        # when it returns (or raises)
+        super().__init_subclass__(**kw)
+        init = cls.__init__
+
+        def wrapped(self, *a, **k):
+            try:
+                init(self, *a, **k)
+            finally:
+                E.end_record()
+
+        cls.__init__ = wrapped
 
     def _launch(self, stream, use_graph):
         if use_graph:
@@ -62,9 +84,12 @@ class _PlanBase:
 
     def check(self):
         st = self.eng.status
-        if int(st.max().item()) != 0:
+        flags = st.tolist()
+        if any(flags):
             st.zero_()
-            raise L.OuHipError("GRU recurrence timed out (workgroup hand-off never completed)")
+            if flags[0]:
+                raise L.OuHipError("GRU recurrence timed out (workgroup hand-off never completed)")
+            raise L.OuRangeError("split-f16 conv input out of range (|x| >= 2^21)")
 
 
 class EnhancePlan(_PlanBase):
@@ -202,6 +227,14 @@ class EnhancePlan(_PlanBase):
         self.draw_noise(rng)
         stream = torch.cuda.current_stream(self.dev).cuda_stream
         self._launch(stream, use_graph)
+        self.check()
+        return self.OUT if self.RED is None else self.RED
+
+    def run_with_noise(self, mix, nz):
+        """Rerun on noise drawn earlier (NZ of a plan of the same shape)."""
+        self.MIX.copy_(mix)
+        self.NZ.copy_(nz)
+        self._launch(torch.cuda.current_stream(self.dev).cuda_stream, True)
         self.check()
         return self.OUT if self.RED is None else self.RED
 

@@ -42,8 +42,10 @@ int main(int argc, char** argv)
             r1((size_t)g.B * g.cout * out_len), r2(r1.size()), fm((size_t)g.B * 2 * g.cout), sc(g.B);
         for (auto* v : {&wl, &x, &bias, &r1, &r2, &fm, &sc})
             for (auto& e : *v) e = rnd();
-        std::vector<float> packed(ou_conv_packed_size(m, cin_eff, g.kt, 0));
+        std::vector<float> packed(ou_conv_packed_size(m, cin_eff, g.kt, 0)), packed_s(packed.size());
         ou_conv_pack(wl.data(), m, cin_eff, g.kt, 0, packed.data());
+        float unscale = 0.f;
+        ou_conv_pack_split(wl.data(), m, cin_eff, g.kt, packed_s.data(), &unscale);
         // reference
         std::vector<double> ref((size_t)g.B * g.cout * out_len, 0.0);
         for (int b = 0; b < g.B; ++b)
@@ -76,9 +78,9 @@ int main(int argc, char** argv)
         for (double v : ref) rn += v * v;
         for (int t = 0; t < ou_conv_num_tiles(); ++t) {
             if (!ou_conv_tile_ok(g.kt, t)) continue;
-            for (int tpw = 0; tpw < 4; ++tpw) {
+            for (int tpw = 0; tpw < 5; ++tpw) {   // 3: warp-specialised, 4: split-f16
                 if (tpw == 3 && g.rout != 1) continue;   // warp-specialised: plain convs only
-                if (!ou_conv_tile_ok(g.kt, t | (tpw == 3 ? 1024 : tpw << 8))) continue;
+                if (!ou_conv_tile_ok(g.kt, t | (tpw == 4 ? 2048 : tpw == 3 ? 1024 : tpw << 8))) continue;
                 std::vector<float> y(ref.size(), 1e30f);
                 ou_conv_desc d{};
                 d.x = x.data(); d.x_bstride = (int64_t)g.cin * g.T; d.x_cstride = g.T;
@@ -90,7 +92,12 @@ int main(int argc, char** argv)
                 d.res1 = g.res1 ? r1.data() : nullptr; d.r1_bstride = d.y_bstride; d.r1_cstride = out_len; d.s1 = 0.7f;
                 d.film = g.film ? fm.data() : nullptr; d.film_bstride = 2 * g.cout;
                 d.res2 = g.res2 ? r2.data() : nullptr; d.r2_bstride = d.y_bstride; d.r2_cstride = out_len; d.s2 = 0.5f;
-                d.tile = t | (tpw == 3 ? 1024 : tpw << 8);
+                d.tile = t | (tpw == 4 ? 0 : tpw == 3 ? 1024 : tpw << 8);
+                if (tpw == 4) {
+                    d.prec = 1;
+                    d.w = packed_s.data();
+                    d.w_unscale = unscale;
+                }
                 const int rc_ = ou_conv(&d, nullptr);
                 if (rc_ == -2 && tpw == 3) continue;   // warp-specialised form refused for this geometry
                 if (rc_ != 0) {

@@ -78,6 +78,12 @@ template <typename K>
 inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* n, K, int, size_t) { *n = 1; return hipSuccess; }
 inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return hipSuccess; }
 #define HIP_SYMBOL(x) (&(x))
+// wave vote / atomics: lanes run one after another here, so a vote sees only
+// the calling lane (used by the split-f16 range flag, never taken in tests)
+inline bool __any(bool p) { return p; }
+inline int atomicOr(int* p, int v) { const int o = *p; *p |= v; return o; }
+inline unsigned atomicMax(unsigned* p, unsigned v) { const unsigned o = *p; *p = o > v ? o : v; return o; }
+inline float __shfl_xor(float v, int) { return v; }
 
 // ---- buffer resources ----------------------------------------------------
 struct emu_rsrc {
@@ -139,6 +145,13 @@ emu_f16v emu_mfma(float a, float b, emu_f16v c, int, int, int);
 inline emu_f16v emu_mfma(float, float, emu_f16v c, int, int, int) { return c; }
 #endif
 #define __builtin_amdgcn_mfma_f32_32x32x2f32 emu_mfma
+typedef _Float16 emu_h8 __attribute__((ext_vector_type(8)));
+#ifdef OU_EMU_FIBERS
+emu_f16v emu_mfma16(emu_h8 a, emu_h8 b, emu_f16v c, int, int, int);
+#else
+inline emu_f16v emu_mfma16(emu_h8, emu_h8, emu_f16v c, int, int, int) { return c; }
+#endif
+#define __builtin_amdgcn_mfma_f32_32x32x16_f16 emu_mfma16
 
 // ---- dynamic LDS: an exact-size heap block per workgroup ------------------
 inline void* emu_lds_ptr = nullptr;
@@ -189,6 +202,8 @@ struct emu_fiber {
     std::vector<char> stack;
     int state = 0;   // 0 runnable, 1 at barrier, 2 at mfma, 3 done, 4 at a wave-level wait
     float a = 0, b = 0;
+    float a8[8] = {}, b8[8] = {};   // v_mfma_f32_32x32x16_f16 operands
+    int k16 = 0;
     emu_f16v c;
 };
 struct emu_block_state {
@@ -226,6 +241,22 @@ inline emu_f16v emu_mfma(float a, float b, emu_f16v c, int, int, int)
     me.a = a;
     me.b = b;
     me.c = c;
+    me.k16 = 0;
+    me.state = 2;
+    swapcontext(&me.ctx, &emu_bs->sched);
+    return me.c;
+}
+// v_mfma_f32_32x32x16_f16: lane l supplies A[l&31][8(l>>5) + j] and
+// B[8(l>>5) + j][l&31] in element j; f16 products are exact in f32
+inline emu_f16v emu_mfma16(emu_h8 a, emu_h8 b, emu_f16v c, int, int, int)
+{
+    emu_fiber& me = emu_bs->f[emu_bs->cur];
+    for (int j = 0; j < 8; ++j) {
+        me.a8[j] = (float)a[j];
+        me.b8[j] = (float)b[j];
+    }
+    me.c = c;
+    me.k16 = 1;
     me.state = 2;
     swapcontext(&me.ctx, &emu_bs->sched);
     return me.c;
@@ -233,6 +264,26 @@ inline emu_f16v emu_mfma(float a, float b, emu_f16v c, int, int, int)
 inline void emu_do_mfma(int wave)
 {
     emu_fiber* L = &emu_bs->f[wave * 64];
+    if (L[0].k16) {
+        float A16[32][16], B16[16][32];
+        for (int l = 0; l < 64; ++l)
+            for (int j = 0; j < 8; ++j) {
+                A16[l & 31][8 * (l >> 5) + j] = L[l].a8[j];
+                B16[8 * (l >> 5) + j][l & 31] = L[l].b8[j];
+            }
+        for (int l = 0; l < 64; ++l) {
+            emu_f16v d = L[l].c;
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), col = l & 31;
+                float acc = d[r];
+                for (int k = 0; k < 16; ++k) acc = std::fma(A16[row][k], B16[k][col], acc);
+                d[r] = acc;
+            }
+            L[l].c = d;
+            L[l].state = 0;
+        }
+        return;
+    }
     float A[32][2], B[2][32];
     for (int l = 0; l < 64; ++l) {
         A[l & 31][l >> 5] = L[l].a;

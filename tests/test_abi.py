@@ -85,3 +85,29 @@ def test_conv_tiles_fit_lds():
     assert n >= 6
     for kt in (1, 3, 4, 5):
         assert any(lib.ou_conv_tile_ok(kt, t) for t in range(n))
+
+
+def test_conv_pack_split_layout():
+    """Split-f16 order [mtile][pair // 8][hi | lo][tap][lane][pair % 8] of
+    a = w * 2^e (max|a| in [2^9, 2^10)): hi + lo * 2^-11 restores a to ~2^-22;
+    w_unscale = 2^(6 - e) (the kernel stages its input as x * 2^-6)."""
+    rng = np.random.default_rng(1)
+    m, cin, kt = 40, 20, 3
+    w = (rng.standard_normal((m, cin, kt)) * 0.03).astype(np.float32)
+    packed, unscale = L.conv_pack_split(w)
+    assert packed.size == L.load().ou_conv_packed_size(m, cin, kt, 0)
+    e = 6 - int(np.log2(unscale))
+    assert 2.0**9 <= np.abs(w).max() * 2.0**e < 2.0**10
+    h = packed.view(np.float16).astype(np.float64).reshape(2, 64 // 16, 2, kt, 64, 8)
+    a = h[:, :, 0] + h[:, :, 1] / 2048.0
+    ref = np.zeros((2, 4, kt, 64, 8))
+    for mt in range(2):
+        for g in range(4):
+            for k in range(kt):
+                for lane in range(64):
+                    for j in range(8):
+                        row, c = mt * 32 + (lane & 31), 2 * (8 * g + j) + (lane >> 5)
+                        if row < m and c < cin:
+                            ref[mt, g, k, lane, j] = float(w[row, c, k]) * 2.0**e
+    assert np.abs(a - ref).max() <= 2.0**-21 * np.abs(ref).max()
+    assert np.count_nonzero(ref) == np.count_nonzero(h[:, :, 0])

@@ -1,5 +1,5 @@
 """Every ou_conv tile shape x kernel variant (one tile per workgroup,
-persistent, warp-specialised persistent) against a torch fp32
+persistent, warp-specialised persistent; f32 and split-f16 operands) against a torch fp32
 reference of the same convolution (ragged lengths, batch 2, residual epilogue,
 frame view).  A tile the autotuner might pick must be exact up to fp32
 summation order."""
@@ -52,7 +52,7 @@ def test_conv_every_tile(geom):
     w = torch.randn(cout, cin * frame, kt, generator=g) * 0.1
     bias = torch.randn(cout, generator=g) * 0.1
     spec = E.ConvSpec(w.numpy(), cin, frame, (kt - 1) // 2, 1, 0.25, bias.numpy())
-    cw = E.make_conv(spec, DEV)
+    cws = {0: E.make_conv(spec, DEV, prec=0), 1: E.make_conv(spec, DEV, prec=1)}
     x = torch.randn(B, cin, T, generator=g)
     U = -(-T // frame)
     res = torch.randn(B, cout, U, generator=g) if with_res else None
@@ -64,13 +64,14 @@ def test_conv_every_tile(geom):
     for t in range(lib.ou_conv_num_tiles()):
         if not lib.ou_conv_tile_ok(kt, t):
             continue
-        for v in (0, 1 << 8, 2 << 8, 1 << 10):   # one-tile, persistent x2 / x4, warp-specialised
+        # one-tile, persistent x2 / x4, warp-specialised; split-f16 (query bit 11)
+        for v in (0, 1 << 8, 2 << 8, 1 << 10, 1 << 11):
             if not lib.ou_conv_tile_ok(kt, t | v):
                 continue
             y = E.new_act(B, cout, U, DEV)
             ra = E.Act(res.to(DEV)) if with_res else None
-            d = E.conv_desc(cw, xa, y, res1=ra, s1=0.7, n_frames=U)
-            d.tile = t | v
+            d = E.conv_desc(cws[1 if v == 1 << 11 else 0], xa, y, res1=ra, s1=0.7, n_frames=U)
+            d.tile = t | (v & ~(1 << 11))
             rc = lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
             if rc == -2 and v == 1 << 10:
                 continue   # warp-specialised form refused for this geometry (single K chunk, rout > 1)
@@ -91,7 +92,7 @@ def test_conv_full_epilogue_every_tile(geom):
     w = torch.randn(cout, cin * frame, kt, generator=g) * 0.1
     bias = torch.randn(cout, generator=g) * 0.1
     spec = E.ConvSpec(w.numpy(), cin, frame, (kt - 1) // 2, 1, 0.25, bias.numpy())
-    cw = E.make_conv(spec, DEV)
+    cws = {0: E.make_conv(spec, DEV, prec=0), 1: E.make_conv(spec, DEV, prec=1)}
     x = torch.randn(B, cin, T, generator=g)
     U = -(-T // frame)
     r1 = torch.randn(B, cout, U, generator=g)
@@ -109,13 +110,13 @@ def test_conv_full_epilogue_every_tile(geom):
     stream = torch.cuda.current_stream().cuda_stream
     bad = []
     for t in range(lib.ou_conv_num_tiles()):
-        for v in (0, 1 << 8, 2 << 8, 1 << 10):
+        for v in (0, 1 << 8, 2 << 8, 1 << 10, 1 << 11):
             if not lib.ou_conv_tile_ok(kt, t | v):
                 continue
             y = E.new_act(B, cout, U, DEV)
-            d = E.conv_desc(cw, xa, y, res1=r1a, s1=0.7, film=fd.data_ptr(), film_bs=2 * cout,
-                            res2=r2a, s2=0.5, n_frames=U, valid_len=valid)
-            d.tile = t | v
+            d = E.conv_desc(cws[1 if v == 1 << 11 else 0], xa, y, res1=r1a, s1=0.7, film=fd.data_ptr(),
+                            film_bs=2 * cout, res2=r2a, s2=0.5, n_frames=U, valid_len=valid)
+            d.tile = t | (v & ~(1 << 11))
             rc = lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
             if rc == -2 and v == 1 << 10:
                 continue   # warp-specialised form refused for this geometry (single K chunk, rout > 1)
@@ -125,3 +126,29 @@ def test_conv_full_epilogue_every_tile(geom):
             if not err < 1e-5:
                 bad.append((t, v, err))
     assert not bad, bad
+
+
+def test_split_range_flag():
+    """split-f16: an input at or above 2^21 sets the status word (the host then
+    reruns with f32 operands); inputs inside the range leave it clear and
+    match the f32 form."""
+    g = torch.Generator().manual_seed(5)
+    cout, cin, kt, T = 64, 64, 3, 900
+    w = torch.randn(cout, cin, kt, generator=g) * 0.1
+    spec = E.ConvSpec(w.numpy(), cin, 1, 1, 1, 0.25, None)
+    cw = E.make_conv(spec, DEV, prec=1)
+    status = torch.zeros(4, dtype=torch.int32, device=DEV)
+    stream = torch.cuda.current_stream().cuda_stream
+    for scale, want in ((1.5e6, 0), (3.0e6, 1)):
+        x = torch.randn(1, cin, T, generator=g)
+        x[0, 5, 17] = scale
+        y = E.new_act(1, cout, T, DEV)
+        d = E.conv_desc(cw, E.Act(x.to(DEV)), y)
+        d.status = status.data_ptr() + 4
+        L.run_now(L.OP_CONV, d, stream)
+        torch.cuda.synchronize()
+        assert int(status[1]) == want, (scale, status.tolist())
+        if want == 0:
+            ref = _ref(w, None, x, 1, kt, 0.25, None, 1.0)
+            assert ((y.t.cpu() - ref).norm() / ref.norm()).item() < 1e-5
+        status.zero_()

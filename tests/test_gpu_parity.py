@@ -216,3 +216,48 @@ def test_enhance_full_size_properties(pp16):
         torch.cuda.synchronize()
         # different batch sizes may autotune to different tiles (summation order)
         assert rel_rms(p1.OUT[0].cpu(), a[1].cpu()) < 1e-4
+
+
+# ------------------------------------------------------- operand precision
+def test_enhance_f32_operands_vs_reference(monkeypatch):
+    """The f32-operand ou_conv build (OUHIP_CONV_PREC=f32) against the
+    reference at the same bar as the default split-f16 build above."""
+    monkeypatch.setenv("OUHIP_CONV_PREC", "f32")
+    d, cfg, m = _model("pp16", "pp16", None)
+    assert m._get_engine().conv_prec == 0
+    mix = _dev(d["enh_mix"])
+    with torch.no_grad():
+        out = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
+    assert rel_rms(out, d["enh_out"]) < 1e-3
+    assert si_sdr(out, d["enh_out"]) > 60
+
+
+def test_split_and_f32_operands_agree_full_size(pp16, monkeypatch):
+    """BASELINE C2 size (8 s, 16 kHz, B = 1): the split-f16 and the f32 operand
+    builds of the whole enhance() agree to f32 summation-order level."""
+    d, cfg, m = pp16
+    assert m._get_engine().conv_prec == 1
+    T = 128000
+    mix = (0.1 * torch.randn(1, T, generator=torch.Generator().manual_seed(3))).to(DEV)
+    monkeypatch.setenv("OUHIP_CONV_PREC", "f32")
+    d32, _, m32 = _model("pp16", "pp16", None)
+    with torch.no_grad():
+        a = m.enhance(mix, rng=torch.Generator(device=DEV).manual_seed(2)).cpu()
+        b = m32.enhance(mix, rng=torch.Generator(device=DEV).manual_seed(2)).cpu()
+    assert torch.isfinite(a).all()
+    assert rel_rms(a, b) < 1e-3 and si_sdr(a, b) > 60
+
+
+def test_enhance_split_amax_exponents_vs_reference(monkeypatch):
+    """OUHIP_SPLIT_AMAX=1: split-f16 convs take their staging exponent from the
+    running max their producer recorded (ConvDesc.amax_in/amax_out)."""
+    monkeypatch.setenv("OUHIP_SPLIT_AMAX", "1")
+    d, cfg, m = _model("pp16_c4", "pp16", 4)
+    mix = _dev(d["enh_mix"])
+    with torch.no_grad():
+        out = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
+    plan = next(iter(m._plans.values()))
+    assert plan.amax is not None and float(plan.amax.max()) > 0
+    assert m._get_engine().conv_prec == 1
+    assert rel_rms(out, d["enh_out"]) < 1e-3
+    assert si_sdr(out, d["enh_out"]) > 60

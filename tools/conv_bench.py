@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--stamps", action="store_true", help="diag library: per-phase cycles")
     ap.add_argument("--wstamps", action="store_true", help="diag library: warp-specialised kernel phases")
+    ap.add_argument("--amax", action="store_true",
+                    help="split-f16: re-time the best tile with amax_out, then amax_in + amax_out")
     a = ap.parse_args()
     dev = "cuda:0"
     stream = torch.cuda.current_stream().cuda_stream
@@ -82,9 +84,13 @@ def main():
     names = [a.layer] if a.layer else list(LAYERS)
     for name in names:
         d, keep = make(name, dev)
-        tiles = [a.tile] if a.tile is not None else [t | v for t in range(lib.ou_conv_num_tiles())
-                                                      for v in (0, 1 << 8, 2 << 8, 1 << 10)
-                                                      if lib.ou_conv_tile_ok(d.kt, t | v)]
+        if d.prec == 1:
+            tiles = [a.tile] if a.tile is not None else [t for t in range(lib.ou_conv_num_tiles())
+                                                          if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))]
+        else:
+            tiles = [a.tile] if a.tile is not None else [t | v for t in range(lib.ou_conv_num_tiles())
+                                                          for v in (0, 1 << 8, 2 << 8, 1 << 10)
+                                                          if lib.ou_conv_tile_ok(d.kt, t | v)]
         res = []
         for t in tiles:
             ms = time_tile(d, t, a.reps, stream)
@@ -96,6 +102,16 @@ def main():
         line = "  ".join(f"{nm(t)}:{ms * 1e3:.1f}us" for ms, t in res[:12])
         print(f"{name:5s} {fl / 1e9:6.2f} GFLOP  best {nm(res[0][1])} {res[0][0] * 1e3:.1f} us "
               f"{fl / res[0][0] / 1e9:.1f} TF/s | {line}", flush=True)
+        if a.amax:
+            slots = torch.zeros(2, 64, device=dev)
+            slots[0] = 1.0
+            d.amax_out = slots[1].data_ptr()
+            t_out = time_tile(d, res[0][1], a.reps, stream)
+            d.amax_in = slots[0].data_ptr()
+            t_both = time_tile(d, res[0][1], a.reps, stream)
+            d.amax_out = d.amax_in = None
+            print(f"      amax: none {res[0][0] * 1e3:.1f} us, out {t_out * 1e3:.1f} us, in+out {t_both * 1e3:.1f} us",
+                  flush=True)
         if a.wstamps:
             import ctypes
 
