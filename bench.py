@@ -60,9 +60,9 @@ CONFIGS = {
     "c4": dict(arch="pp24", batch=32, seconds=10.0, n_steps=None, node_batch=True,
                workload="UNIVERSE++ 24 kHz enhance(), batch=32 per node sharded over the GPUs, 10 s clips, "
                         "8 diffusion steps (BASELINE.json configs[3])"),
-    "c5": dict(arch="pp16", batch=1, seconds=60.0, n_steps=None,
-               workload="UNIVERSE++ 16 kHz enhance(), batch=1, 60 s long-form clip, 8 diffusion steps, fp32 "
-                        "(BASELINE.json configs[4] names fp16; this build computes in fp32)"),
+    "c5": dict(arch="pp16", batch=1, seconds=60.0, n_steps=None, conv_prec="f16",
+               workload="UNIVERSE++ 16 kHz enhance(), batch=1, 60 s long-form clip, 8 diffusion steps, fp16 conv "
+                        "operands, whole sampler captured in one hipGraph (BASELINE.json configs[4])"),
 }
 
 
@@ -126,10 +126,11 @@ def profile_roofline(plan, stream, dump=None):
     flops = plan.prog.flops
     conv_ms = sum(t for t, k in zip(ms, kinds) if k == L.OP_CONV)
     conv_fl = sum(f for f, k in zip(flops, kinds) if k == L.OP_CONV)
+    conv_by = sum(b for b, k in zip(plan.prog.bytes, kinds) if k == L.OP_CONV)
     n_conv = sum(1 for k in kinds if k == L.OP_CONV)
     gru_ms = sum(t for t, k in zip(ms, kinds) if k == L.OP_GRU)
     return {
-        "conv_ms": conv_ms, "conv_flops": conv_fl, "n_conv": n_conv, "gru_ms": gru_ms,
+        "conv_ms": conv_ms, "conv_flops": conv_fl, "conv_bytes": conv_by, "n_conv": n_conv, "gru_ms": gru_ms,
         "total_ms": sum(ms), "total_flops": sum(flops), "n_ops": len(ms),
     }
 
@@ -164,6 +165,8 @@ def main():
     dev = torch.device("cuda", local)
 
     C = CONFIGS[args.config]
+    if C.get("conv_prec") and "OUHIP_CONV_PREC" not in os.environ:
+        os.environ["OUHIP_CONV_PREC"] = C["conv_prec"]
     if args.seconds is None:
         args.seconds = C["seconds"]
     B = C["batch"] // world if C.get("node_batch") else C["batch"]
@@ -208,6 +211,9 @@ def main():
     if prec == 1:
         dtype = "f32 (conv operands split into f16 hi/lo: 3 f16 MFMA passes, f32 accumulation)"
         peak, peak_basis = round(F16_PEAK_TF / 3, 1), "dense f16 MFMA peak / 3 passes per f32 MAC"
+    elif prec == 2:
+        dtype = "f16 (conv operands f16, f32 accumulation; GRU, sampler and STFT/mel in f32)"
+        peak, peak_basis = F16_PEAK_TF, "dense f16 MFMA peak"
     else:
         dtype, peak, peak_basis = "f32", FP32_PEAK_TF, "dense f32 MFMA peak"
     if rank == 0:
@@ -237,7 +243,12 @@ def main():
             "xrt_per_gpu": round(value / world, 3),
         }
         if prof is not None:
-            achieved = prof["conv_flops"] / (prof["conv_ms"] * 1e-3) / 1e12
+            # the roofline that binds ou_conv over one enhance: the larger of
+            # FLOPs / MFMA peak and algorithmic bytes / HBM peak
+            t_mfma = prof["conv_flops"] / (peak * 1e12)
+            t_hbm = prof["conv_bytes"] / (HBM_PEAK * 1e9)
+            sec = prof["conv_ms"] * 1e-3
+            tflops, gbps = prof["conv_flops"] / sec / 1e12, prof["conv_bytes"] / sec / 1e9
             traffic, tsrc = None, None
             if args.traffic_json and os.path.exists(args.traffic_json):
                 with open(args.traffic_json) as fh:
@@ -247,14 +258,24 @@ def main():
                     traffic = row["traffic_bytes_per_launch"]
                     tsrc = (f"{os.path.relpath(args.traffic_json, HERE)} ({pmc.get('tag', '')}): "
                             "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes per ou_conv launch")
+            if t_hbm > t_mfma:
+                rl = {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK, "peak_basis": "HBM3E",
+                      "unit": "GB/s", "frac": round(gbps / HBM_PEAK, 4),
+                      "mfma": {"achieved": round(tflops, 3), "peak": peak, "unit": "TFLOP/s",
+                               "frac": round(tflops / peak, 4), "peak_basis": peak_basis}}
+            else:
+                rl = {"bound": "mfma", "achieved": round(tflops, 3), "peak": peak, "peak_basis": peak_basis,
+                      "unit": "TFLOP/s", "frac": round(tflops / peak, 4),
+                      "hbm": {"achieved": round(gbps, 1), "peak": HBM_PEAK, "unit": "GB/s",
+                              "frac": round(gbps / HBM_PEAK, 4)}}
             out["roofline"] = {
-                "bound": "mfma", "achieved": round(achieved, 3), "peak": peak, "peak_basis": peak_basis,
-                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                **rl, "traffic": traffic,
                 "traffic_source": tsrc,
                 "kernel": "ou_conv (conv_kernel, all launches of one enhance)",
                 "launches": prof["n_conv"],
                 "avg_launch_ms": round(prof["conv_ms"] / prof["n_conv"], 5),
                 "flops_per_launch": round(prof["conv_flops"] / prof["n_conv"]),
+                "algorithmic_bytes_per_launch": round(prof["conv_bytes"] / prof["n_conv"]),
             }
             out["profile"] = {
                 "enhance_device_ms": round(prof["total_ms"], 3),

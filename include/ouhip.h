@@ -90,7 +90,9 @@ typedef struct ou_conv_desc {
                                /* ou_conv_tile_ok)                               */
     int32_t prec;              /* 0: f32 operands (weights from ou_conv_pack);   */
                                /* 1: split-f16 operands (ou_conv_pack_split),    */
-                               /*    f32-class accuracy, see ou_conv.hip         */
+                               /*    f32-class accuracy, see ou_conv.hip;        */
+                               /* 2: f16 operands (the hi halves of the same     */
+                               /*    packing), f32 accumulation                  */
     float w_unscale;           /* prec 1: power of two from ou_conv_pack_split   */
     int32_t _reserved;
     int32_t* status;           /* prec 1: set to 1 when a staged input exceeds   */

@@ -250,6 +250,7 @@ class Program:
         self.keep = []          # tensors whose memory the program references
         self.captured = False
         self.flops = []         # algorithmic FLOPs of the reference ops each op replaces
+        self.bytes = []         # algorithmic HBM bytes of each op (0 where not counted)
         self.info = []          # per-op geometry (profiling / reports)
 
     def add(self, op, desc):
@@ -259,6 +260,7 @@ class Program:
         check(self.lib.ou_program_add(self.h, op, ctypes.byref(desc), ctypes.sizeof(desc)),
               f"program_add(op={op})")
         self.flops.append(float(getattr(desc, "_flops", 0.0)))
+        self.bytes.append(float(getattr(desc, "_bytes", 0.0)))
         if op == OP_CONV:
             self.info.append({"m": desc.m, "cin": desc.cin, "frame": desc.frame, "kt": desc.kt,
                               "n": desc.n_frames, "b": desc.batch, "rout": desc.rout,

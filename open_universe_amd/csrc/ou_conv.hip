@@ -55,6 +55,7 @@ constexpr int kCinAlign = 64;   // packed weights pad the channel axis to this
 // (register blocking) over its share (1/WK) of every K chunk.
 // P = 0: f32 operands (v_mfma_f32_32x32x2_f32).  P = 1: split-f16 operands
 // (v_mfma_f32_32x32x16_f16, three passes per k-step, see conv_kernel).
+// P = 2: plain f16 operands (the hi halves only, one pass; f32 accumulation).
 template <int KT, int CC, int WM, int WN, int WK, int MR, int NR, int P = 0>
 struct Cfg {
     static constexpr int BM = 32 * WM * MR;
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
                     lo_[j] = (_Float16)((v_ - (float)hi_[j]) * 2048.f);                        \
                 }                                                                              \
                 *(half4_t*)(xh_ + xdst[e]) = hi_;                                              \
-                *(half4_t*)(xh_ + C::W * C::SX + xdst[e]) = lo_;                               \
+                if constexpr (P == 1) *(half4_t*)(xh_ + C::W * C::SX + xdst[e]) = lo_;         \
             }                                                                                  \
         } else {                                                                               \
             _Pragma("unroll") for (int e = 0; e < C::XE; ++e) if (xdst[e] >= 0)                \
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     }
 
     floatx16 acc[MR][NR];
-    floatx16 accx[P ? MR : 1][P ? NR : 1];   // split-f16 cross terms
+    floatx16 accx[P == 1 ? MR : 1][P == 1 ? NR : 1];   // split-f16 cross terms
     bool ovf = false;                        // split-f16: staged input out of range
 #pragma unroll
     for (int i = 0; i < MR; ++i)
@@ -362,12 +363,13 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 #pragma unroll
                 for (int mr = 0; mr < MR; ++mr) {
                     a[mr] = ap[(mr * C::HQ * KT + (c8 * 2) * KT + k) * 64];
-                    al[mr] = ap[(mr * C::HQ * KT + (c8 * 2 + 1) * KT + k) * 64];
+                    if constexpr (P == 1) al[mr] = ap[(mr * C::HQ * KT + (c8 * 2 + 1) * KT + k) * 64];
                 }
 #pragma unroll
                 for (int nr = 0; nr < NR; ++nr) {
                     bq[nr] = *(const half8_t*)(xp + (nr * 32 + k) * C::SX + 8 * c8);
-                    bl[nr] = *(const half8_t*)(xp + C::W * C::SX + (nr * 32 + k) * C::SX + 8 * c8);
+                    if constexpr (P == 1)
+                        bl[nr] = *(const half8_t*)(xp + C::W * C::SX + (nr * 32 + k) * C::SX + 8 * c8);
                 }
             };
             frag(0, fa[0], fal[0], fb[0], fbl[0]);
@@ -380,8 +382,10 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 #pragma unroll
                     for (int nr = 0; nr < NR; ++nr) {
                         acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[c][mr], fb[c][nr], acc[mr][nr], 0, 0, 0);
-                        accx[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[c][mr], fbl[c][nr], accx[mr][nr], 0, 0, 0);
-                        accx[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[c][mr], fb[c][nr], accx[mr][nr], 0, 0, 0);
+                        if constexpr (P == 1) {
+                            accx[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[c][mr], fbl[c][nr], accx[mr][nr], 0, 0, 0);
+                            accx[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[c][mr], fb[c][nr], accx[mr][nr], 0, 0, 0);
+                        }
                     }
             }
         } else {
@@ -432,7 +436,8 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 #pragma unroll
             for (int j = 0; j < NR; ++j)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = fmaf(accx[i][j][r], sx, acc[i][j][r] * su);
+                for (int r = 0; r < 16; ++r)
+                    acc[i][j][r] = P == 1 ? fmaf(accx[i][j][r], sx, acc[i][j][r] * su) : acc[i][j][r] * su;
     }
 
     // ---- intra-workgroup split-K reduction (fixed order: deterministic) ----
@@ -1544,6 +1549,14 @@ int launch_kt(const ou_conv_desc& d, int tile, int tpw, bool ws, hipStream_t s)
         }
         return ou_fail(-2, "conv: bad tile %d", tile);
     }
+    if (d.prec == 2) {   // plain f16 (same layout and tiles as split-f16)
+        switch (tile) {
+#define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) case id: return launch_t<KT, wm, wn, wk, mr, nr, big, 2>(d, 1, s);
+            OU_TILES(OU_TILE_CASE)
+#undef OU_TILE_CASE
+        }
+        return ou_fail(-2, "conv: bad tile %d", tile);
+    }
     if (ws) {
         switch (tile) {
 #define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) \
@@ -1633,7 +1646,7 @@ int lds_bytes(int kt, int tile)
 int pick_tile_for(const ou_conv_desc& d)
 {
     const int t = pick_tile(d);
-    if (d.prec != 1 || lds_bytes(d.kt, t | kSplitBit) > 0) return t;
+    if (d.prec == 0 || lds_bytes(d.kt, t | kSplitBit) > 0) return t;
     for (int c : {11, 3, 6, 5, 1, 0, 10, 8, 2, 4, 7, 12})
         if (lds_bytes(d.kt, c | kSplitBit) > 0) return c;
     return t;
@@ -1732,14 +1745,14 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     const bool ws = d.tile >= 0 && (d.tile & kWsBit);
     const int tpw = d.tile >= 0 && !ws ? 1 << ((d.tile >> 8) & 3) : 1;
     if (ws && d.rout != 1) return ou_fail(-2, "conv: the warp-specialised kernel has no transposed (rout %d) form", d.rout);
-    if (d.prec != 0 && d.prec != 1) return ou_fail(-1, "conv: bad precision %d", d.prec);
+    if (d.prec < 0 || d.prec > 2) return ou_fail(-1, "conv: bad precision %d", d.prec);
     if (d.amax_out && (ws || tpw > 1))
         return ou_fail(-2, "conv: amax_out needs the one-tile kernel (tile 0x%x)", d.tile);
-    if (d.prec == 1 && (ws || tpw > 1))
+    if (d.prec != 0 && (ws || tpw > 1))
         return ou_fail(-2, "conv: the split-f16 form has one-tile workgroups only (tile 0x%x)", d.tile);
-    if (d.prec == 1 && !(d.w_unscale > 0.f))
+    if (d.prec != 0 && !(d.w_unscale > 0.f))
         return ou_fail(-1, "conv: split-f16 needs the w_unscale of ou_conv_pack_split");
-    const int lb = lds_bytes(d.kt, tile | (ws ? kWsBit : 0) | (d.prec == 1 ? kSplitBit : 0));
+    const int lb = lds_bytes(d.kt, tile | (ws ? kWsBit : 0) | (d.prec != 0 ? kSplitBit : 0));
     if (lb <= 0 || lb > kMaxLds)
         return ou_fail(-2, "conv: tile %d (ws %d) needs %d B of LDS for kt=%d", tile, (int)ws, lb, d.kt);
     hipStream_t s = (hipStream_t)stream;

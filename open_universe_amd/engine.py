@@ -26,9 +26,10 @@ NF2 = np.float32(1.0 / math.sqrt(2.0))
 
 # Operand precision of ou_conv (ConvDesc.prec): 1 = split-f16 (three f16 MFMA
 # passes on hi/lo operand halves, f32 accumulation, f32-class accuracy: see
-# csrc/ou_conv.hip), 0 = f32 MFMA.  OUHIP_CONV_PREC=f32|split picks the default
+# csrc/ou_conv.hip), 0 = f32 MFMA, 2 = plain f16 operands (f32 accumulation;
+# BASELINE configs[4] "fp16").  OUHIP_CONV_PREC=f32|split|f16 picks the default
 # of every Engine; Engine(conv_prec=...) overrides it per model.
-_PREC_NAMES = {"f32": 0, "fp32": 0, "0": 0, "split": 1, "split16": 1, "1": 1}
+_PREC_NAMES = {"f32": 0, "fp32": 0, "0": 0, "split": 1, "split16": 1, "1": 1, "f16": 2, "fp16": 2, "2": 2}
 
 
 def default_conv_prec():
@@ -36,7 +37,7 @@ def default_conv_prec():
 
     v = os.environ.get("OUHIP_CONV_PREC", "split").strip().lower()
     if v not in _PREC_NAMES:
-        raise ValueError(f"OUHIP_CONV_PREC={v!r}: expected f32 or split")
+        raise ValueError(f"OUHIP_CONV_PREC={v!r}: expected f32, split or f16")
     return _PREC_NAMES[v]
 
 
@@ -137,7 +138,7 @@ class ConvSpec:
 
 
 def make_conv(spec, device, prec=None):
-    """prec: 0 f32 operands, 1 split-f16; None = the packing Engine's choice
+    """prec: 0 f32 operands, 1 split-f16, 2 f16; None = the packing Engine's choice
     (or OUHIP_CONV_PREC outside an Engine)."""
     if prec is None:
         prec = _PREP_PREC if _PREP_PREC is not None else default_conv_prec()
@@ -149,14 +150,14 @@ def make_conv(spec, device, prec=None):
         w_logical = np.ascontiguousarray(
             w_logical.reshape(m, spec.cin, spec.frame, kt).transpose(0, 2, 1, 3).reshape(m, cin_eff, kt))
     cc = L.conv_chunk(kt, spec.frame)
-    if prec == 1:
+    if prec in (1, 2):   # f16 uses the hi halves of the split packing
         packed_np, unscale = L.conv_pack_split(w_logical)
     else:
         packed_np, unscale = L.conv_pack(w_logical, cc), 1.0
     packed = torch.from_numpy(packed_np).to(device)
     b = None if spec.bias is None else torch.from_numpy(np.ascontiguousarray(spec.bias, np.float32)).to(device)
     return ConvW(m, spec.cin, kt, spec.frame, spec.pad, spec.rout, float(spec.slope), cc, packed, b,
-                 spec.shift, spec.ref_macs, int(prec), float(unscale), _PREP_STATUS if prec == 1 else 0)
+                 spec.shift, spec.ref_macs, int(prec), float(unscale), _PREP_STATUS if prec else 0)
 
 
 def _slope(sd, p):
@@ -338,6 +339,10 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
         d.res2, d.r2_bstride, d.r2_cstride, d.s2 = res2.ptr, res2.bs, res2.cs, s2
     d.tile = -1
     d._flops = 2.0 * cw.ref_macs * n_frames * d.batch
+    # algorithmic HBM bytes: input, output and residuals once each (f32), plus
+    # the logical f32 weights -- no halo or tile re-reads
+    act = cw.cin * d.in_len + cw.cout * d.out_len * (1 + (res1 is not None) + (res2 is not None))
+    d._bytes = 4.0 * (act * d.batch + cw.m * cw.cin * cw.frame * cw.kt)
     # shape guards: the kernel trusts these (an out-of-bounds store faults the GPU)
     assert x.C == cw.cin, ("conv input channels", x.C, cw.cin)
     assert y.C == cw.cout, ("conv output channels", y.C, cw.cout)
@@ -444,7 +449,7 @@ class ConvTuner:
         # tile shape x log2(output tiles per workgroup); > 0 = persistent kernel
         # (bit 10: the warp-specialised persistent kernel)
         # (split-f16, bit 11 in the query only, and amax tracking: one-tile workgroups)
-        if d.prec == 1:
+        if d.prec in (1, 2):
             cands = [t for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))]
         elif d.amax_out:
             cands = [t for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t)]

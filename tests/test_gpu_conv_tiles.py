@@ -152,3 +152,35 @@ def test_split_range_flag():
             ref = _ref(w, None, x, 1, kt, 0.25, None, 1.0)
             assert ((y.t.cpu() - ref).norm() / ref.norm()).item() < 1e-5
         status.zero_()
+
+
+@pytest.mark.parametrize("geom", GEOMS[:5], ids=[str(g) for g in GEOMS[:5]])
+def test_conv_f16_every_tile(geom):
+    """f16 operands (ConvDesc.prec = 2): every tile within f16 rounding of the
+    f32 reference (operands rounded to 11 bits, f32 accumulation)."""
+    cout, cin, frame, kt, T, B, with_res = geom
+    g = torch.Generator().manual_seed(hash(geom) % 1000)
+    w = torch.randn(cout, cin * frame, kt, generator=g) * 0.1
+    bias = torch.randn(cout, generator=g) * 0.1
+    spec = E.ConvSpec(w.numpy(), cin, frame, (kt - 1) // 2, 1, 0.25, bias.numpy())
+    cw = E.make_conv(spec, DEV, prec=2)
+    x = torch.randn(B, cin, T, generator=g)
+    U = -(-T // frame)
+    ref = _ref(w, bias, x, frame, kt, 0.25, None, 1.0)
+    xa = E.Act(x.to(DEV))
+    lib = L.load()
+    stream = torch.cuda.current_stream().cuda_stream
+    bad, n = [], 0
+    for t in range(lib.ou_conv_num_tiles()):
+        if not lib.ou_conv_tile_ok(kt, t | (1 << 11)):
+            continue
+        y = E.new_act(B, cout, U, DEV)
+        d = E.conv_desc(cw, xa, y, n_frames=U)
+        d.tile = t
+        assert lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream)) == 0
+        torch.cuda.synchronize()
+        err = ((y.t.cpu() - ref).norm() / ref.norm()).item()
+        n += 1
+        if not (1e-5 < err < 2e-3):   # f16-rounded, not f32-exact, and not wrong
+            bad.append((t, err))
+    assert n and not bad, bad

@@ -261,3 +261,16 @@ def test_enhance_split_amax_exponents_vs_reference(monkeypatch):
     assert m._get_engine().conv_prec == 1
     assert rel_rms(out, d["enh_out"]) < 1e-3
     assert si_sdr(out, d["enh_out"]) > 60
+
+
+def test_enhance_f16_operands_vs_reference(monkeypatch):
+    """OUHIP_CONV_PREC=f16 (BASELINE configs[4]): f16 conv operands with f32
+    accumulation, against the f32 reference: SI-SDR >= 30 dB."""
+    monkeypatch.setenv("OUHIP_CONV_PREC", "f16")
+    d, cfg, m = _model("pp16", "pp16", None)
+    assert m._get_engine().conv_prec == 2
+    mix = _dev(d["enh_mix"])
+    with torch.no_grad():
+        out = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
+    assert torch.isfinite(out).all()
+    assert si_sdr(out, d["enh_out"]) > 30
