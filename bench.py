@@ -12,10 +12,13 @@ GPUs with no collective on the data path -- so scaling is weak; ``value`` is
 the whole-job audio-seconds per second: N * K * 8 s / max-over-ranks time.
 
 Extra fields:
-  roofline      the dominant kernel (ou_conv, every launch of one enhance),
-                algorithmic FLOPs of the reference ops it replaces / its device
-                time, measured with HIP events per launch in an instrumented
-                eager replay of the same enhance on the same stream.
+  roofline      the dominant kernel (ou_conv, every launch of one enhance):
+                algorithmic FLOPs of the reference ops it replaces and
+                algorithmic bytes (activations once, f32 weights) over its
+                device time, measured with HIP events per launch in an
+                instrumented eager replay of the same enhance on the same
+                stream; the bound is whichever of FLOPs/MFMA peak and
+                bytes/HBM peak is larger.
   cpu_baseline  the CPU restatement of the reference op sequence (oracle/,
                 plain PyTorch) on this host's cores, bounded sample.
 Weights are synthetic (no trained checkpoint offline); timing does not depend
