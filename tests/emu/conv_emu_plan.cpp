@@ -33,8 +33,11 @@ int main(int argc, char** argv)
     }
     auto ptr = [&](long b, long off) -> float* { return b < 0 ? nullptr : (float*)(bufs[b] + off); };
     const int only = argc > 2 ? std::atoi(argv[2]) : -1;
+    int shard = 0, nshards = 1;   // OUHIP_EMU_SHARD="i/n": descriptors ci % n == i
+    if (const char* s = std::getenv("OUHIP_EMU_SHARD")) std::sscanf(s, "%d/%d", &shard, &nshards);
     for (size_t ci = 0; ci < convs.size(); ++ci) {
         if (only >= 0 && (int)ci != only) continue;
+        if ((int)(ci % nshards) != shard) continue;
         std::istringstream ss(convs[ci]);
         long xb, xo, ib, io, wb, wo, yb, yo, bb, bo, r1b, r1o, fb, fo, r2b, r2o;
         ou_conv_desc d{};
@@ -51,13 +54,16 @@ int main(int argc, char** argv)
         if (std::getenv("OUHIP_EMU_FRAMED") && d.frame == 1) continue;
         for (int t = 0; t < ou_conv_num_tiles(); ++t) {
             if (!ou_conv_tile_ok(d.kt, t)) continue;
-            for (int tpw = 0; tpw < 4; ++tpw) {
+            for (int tpw = 0; tpw < 5; ++tpw) {   // 3: warp-specialised, 4: split-f16 (same weight bytes)
                 if (tpw == 3 && d.rout != 1) continue;   // warp-specialised: plain convs only
-                if (!ou_conv_tile_ok(d.kt, t | (tpw == 3 ? 1024 : tpw << 8))) continue;
+                const int v = tpw == 4 ? 2048 : tpw == 3 ? 1024 : tpw << 8;
+                if (!ou_conv_tile_ok(d.kt, t | v)) continue;
                 if (std::getenv("OUHIP_EMU_VERBOSE"))
                     std::fprintf(stderr, "conv %zu (m %d cin %d frame %d kt %d n %d rout %d) tile %d tpw %d\n", ci, d.m,
                                  d.cin, d.frame, d.kt, d.n_frames, d.rout, t, tpw);
-                d.tile = t | (tpw == 3 ? 1024 : tpw << 8);
+                d.tile = t | (tpw == 4 ? 0 : v);
+                d.prec = tpw == 4 ? 1 : 0;
+                d.w_unscale = 1.f;
                 const int rc_ = ou_conv(&d, nullptr);
                 if (rc_ == -2 && tpw == 3) continue;   // warp-specialised form refused for this geometry
                 if (rc_ != 0) {

@@ -48,14 +48,27 @@ def test_recorded_plan_convs_in_bounds(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     exe = str(tmp_path / "conv_emu_plan")
     _build("conv_emu_plan.cpp", exe, *ASAN)
-    assert "ok:" in _run([exe, plan], env={"OUHIP_EMU_BLOCKS": "2"})
+    n = 4   # descriptor shards, one process each, run side by side
+    procs = [subprocess.Popen([exe, plan], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                              env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0", OUHIP_EMU_BLOCKS="2",
+                                       OUHIP_EMU_SHARD=f"{i}/{n}"))
+             for i in range(n)]
+    for p in procs:
+        out, err = p.communicate(timeout=900)
+        assert p.returncode == 0 and "ok:" in out, (out[-2000:], err[-4000:])
 
 
 def test_conv_values_match_reference(tmp_path):
     """Fiber emulation: every tile configuration against a double-precision
     evaluation of the ou_conv_desc formula (include/ouhip.h)."""
     exe = str(tmp_path / "conv_emu_values")
-    _build("conv_emu_values.cpp", exe, "-O1", "-DOU_EMU_FIBERS")
-    for g in ("0", "4", "7"):   # plain k3 batch 2; frame view; transposed conv
-        out = _run([exe, g])
-        assert "ok:" in out, out
+    # -O0: -O1 spends minutes compiling every kernel instantiation for the host
+    _build("conv_emu_values.cpp", exe, "-O0", "-DOU_EMU_FIBERS")
+    # plain k3 batch 2; 1x1 with FiLM and two residuals; transposed conv -- one
+    # process each, run side by side
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    procs = [subprocess.Popen([exe, g], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+             for g in ("0", "4", "7")]
+    for p in procs:
+        out, err = p.communicate(timeout=900)
+        assert p.returncode == 0 and "ok:" in out, (out[-2000:], err[-2000:])
