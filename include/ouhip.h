@@ -102,6 +102,9 @@ typedef struct ou_conv_desc {
                                /* id mod 64; zeroed by the caller per enhance)   */
     const float* amax_in;      /* prec 1: [64] amax_out of x's producer, sets    */
                                /* the staging exponent; NULL: fixed 2^-6         */
+    float* ks_ws;              /* K-slice workspace (tile bits 12-13 = log2 S,   */
+    int64_t ks_ws_bytes;       /* S > 1): S partial sums per output tile, then   */
+                               /* a reduce + epilogue launch; NULL if unused     */
 } ou_conv_desc;
 
 /* Default channel chunk of the kernel for a tap count (informational: the

@@ -37,7 +37,7 @@ class ConvDesc(ctypes.Structure):
         ("film", fp), ("film_bstride", c_int64),
         ("res2", fp), ("r2_bstride", c_int64), ("r2_cstride", c_int64), ("s2", c_float),
         ("tile", c_int32), ("prec", c_int32), ("w_unscale", c_float), ("_reserved", c_int32),
-        ("status", fp), ("amax_out", fp), ("amax_in", fp),
+        ("status", fp), ("amax_out", fp), ("amax_in", fp), ("ks_ws", fp), ("ks_ws_bytes", c_int64),
     ]
 
 

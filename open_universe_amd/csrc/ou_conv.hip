@@ -153,9 +153,15 @@ constexpr int kSplitShift = 6;
 typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
 typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
 
+//
+// K slices (tile bits 12-13, S = 2..8; for grids too small to fill the chip):
+// ksmode 1 runs the workgroups of slice ks = blockIdx.z % S over chunks
+// [ks n / S, (ks + 1) n / S) and stores their sums to d.ks_ws; ksmode 2 (a
+// second launch, so the kernel boundary orders the two) adds the S partial
+// sums in slice order -- deterministic -- and runs the epilogue.
 template <int KT, int CC, int WM, int WN, int WK, int MR, int NR, int P = 0>
 __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, int mtiles,
-                                                   int64_t a_mt_stride)
+                                                   int64_t a_mt_stride, int ksmode)
 {
     using C = Cfg<KT, CC, WM, WN, WK, MR, NR, P>;
     static_assert(CC % 8 == 0 && C::HQ % WK == 0, "chunk must split into 4-pair groups per wave");
@@ -172,7 +178,11 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const int wn = wave % WN;
     const int wm = (wave / WN) % WM;
     const int wk = wave / (WN * WM);
-    const int b = blockIdx.z;
+    const int nks = ksmode ? 1 << ((d.tile >> 12) & 3) : 1;   // K slices per output tile
+    const int b = ksmode == 1 ? (int)blockIdx.z / nks : (int)blockIdx.z;
+    const int ks = ksmode == 1 ? (int)blockIdx.z - b * nks : 0;
+    const int q0 = ksmode == 1 ? ks * nchunks / nks : 0;
+    const int q1 = ksmode == 1 ? (ks + 1) * nchunks / nks : nchunks;
     const int n0 = blockIdx.x * C::BN;
     const int mt0 = blockIdx.y * (WM * MR);       // first m-tile of the workgroup
     const int h = lane >> 5;
@@ -341,13 +351,14 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     }
 
     OU_CSTAMP_INIT
-    OU_LOAD_CHUNK(0);
+    if (ksmode != 2) {
+    OU_LOAD_CHUNK(q0);
     OU_STORE_CHUNK(0);
     __syncthreads();
     OU_CSTAMP(0);
-    for (int q = 0; q < nchunks; ++q) {
-        const int cur = q & 1;
-        if (q + 1 < nchunks) OU_LOAD_CHUNK(q + 1);
+    for (int q = q0; q < q1; ++q) {
+        const int cur = (q - q0) & 1;
+        if (q + 1 < q1) OU_LOAD_CHUNK(q + 1);
         OU_CSTAMP(1);
         if constexpr (P) {
             // one step = 8 channel pairs (16 k) at one tap: 3 f16 MFMAs per
@@ -420,7 +431,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
             }
         }
         OU_CSTAMP(2);
-        if (q + 1 < nchunks) OU_STORE_CHUNK(cur ^ 1);
+        if (q + 1 < q1) OU_STORE_CHUNK(cur ^ 1);
         OU_CSTAMP(3);
         __syncthreads();
         OU_CSTAMP(4);
@@ -466,6 +477,36 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
                     for (int r = 0; r < 16; ++r)
                         acc[mr][nr][r] +=
                             red[(((((j - 1) * WM * WN + sub) * MR + mr) * NR + nr) * 16 + r) * 64 + lane];
+    }
+
+    if (ksmode == 1) {   // this slice's sums -> d.ks_ws, [tile][slice][sub-tile][acc][lane]
+        const int64_t tl = ((int64_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        float* pw = d.ks_ws + ((tl * nks + ks) * (WM * WN) + wm * WN + wn) * (MR * NR * 16 * 64) + lane;
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+            for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) pw[((mr * NR + nr) * 16 + r) * 64] = acc[mr][nr][r];
+        return;
+    }
+    } else {   // ksmode 2: add the slices' sums in slice order
+        if (wk > 0) return;
+        const int S = 1 << ((d.tile >> 12) & 3);
+        const int64_t tl = ((int64_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        const float* pr = d.ks_ws + (tl * S * (WM * WN) + wm * WN + wn) * (MR * NR * 16 * 64) + lane;
+        for (int k = 0; k < S; ++k) {
+            const float* pk = pr + (int64_t)k * (WM * WN) * (MR * NR * 16 * 64);
+#pragma unroll
+            for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float v = pk[((mr * NR + nr) * 16 + r) * 64];
+                        acc[mr][nr][r] = k == 0 ? v : acc[mr][nr][r] + v;
+                    }
+        }
     }
 
     // ---- epilogue ----
@@ -1396,8 +1437,17 @@ int launch_t(const ou_conv_desc& d, int tpw, hipStream_t s)
     const int nchunks = (cin_eff + CC - 1) / CC;
     const int64_t a_mt_stride = (int64_t)cin_pad * KT * 32;
     (void)tpw;   // one output tile per workgroup
+    const int S = d.tile >= 0 ? 1 << ((d.tile >> 12) & 3) : 1;   // K slices
     dim3 grid((d.n_frames + C::BN - 1) / C::BN, (mtiles + WM * MR - 1) / (WM * MR), d.batch);
-    const int lds = (nchunks > 1 ? C::LDS2 : C::LDS1) * (int)sizeof(float);
+    if (S > 1) {
+        const int64_t need = (int64_t)grid.x * grid.y * grid.z * S * C::BM * C::BN * 4;
+        if (S > nchunks) return ou_fail(-2, "conv: %d K slices > %d chunks", S, nchunks);
+        if (!d.ks_ws || d.ks_ws_bytes < need)
+            return ou_fail(-2, "conv: K slices need %lld B of workspace (have %lld)", (long long)need,
+                           (long long)d.ks_ws_bytes);
+    }
+    const int slice_chunks = S > 1 ? (nchunks + S - 1) / S : nchunks;
+    const int lds = (slice_chunks > 1 ? C::LDS2 : C::LDS1) * (int)sizeof(float);
     auto kern = conv_kernel<KT, CC, WM, WN, WK, MR, NR, P>;
     static bool attr = false;   // opt in to more than 64 KiB of dynamic LDS, once
     if (!attr && C::LDS2 * 4 > 64 * 1024) {
@@ -1406,7 +1456,14 @@ int launch_t(const ou_conv_desc& d, int tpw, hipStream_t s)
                      "conv: LDS attribute");
         attr = true;
     }
-    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, d, nchunks, mtiles, a_mt_stride);
+    if (S == 1) {
+        hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, d, nchunks, mtiles, a_mt_stride, 0);
+        return ou_check_launch("conv");
+    }
+    hipLaunchKernelGGL(kern, dim3(grid.x, grid.y, grid.z * S), dim3(256), lds, s, d, nchunks, mtiles, a_mt_stride, 1);
+    const int rc = ou_check_launch("conv");
+    if (rc) return rc;
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, d, nchunks, mtiles, a_mt_stride, 2);
     return ou_check_launch("conv");
     }
 }
@@ -1744,6 +1801,9 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     const int tile = d.tile >= 0 && (d.tile & 0xff) < kNumTiles ? (d.tile & 0xff) : pick_tile_for(d);
     const bool ws = d.tile >= 0 && (d.tile & kWsBit);
     const int tpw = d.tile >= 0 && !ws ? 1 << ((d.tile >> 8) & 3) : 1;
+    const int kslices = d.tile >= 0 ? 1 << ((d.tile >> 12) & 3) : 1;
+    if (kslices > 1 && (ws || tpw > 1))
+        return ou_fail(-2, "conv: K slices need the one-tile kernel (tile 0x%x)", d.tile);
     if (ws && d.rout != 1) return ou_fail(-2, "conv: the warp-specialised kernel has no transposed (rout %d) form", d.rout);
     if (d.prec < 0 || d.prec > 2) return ou_fail(-1, "conv: bad precision %d", d.prec);
     if (d.amax_out && (ws || tpw > 1))

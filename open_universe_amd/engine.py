@@ -43,6 +43,8 @@ def default_conv_prec():
 
 _PREP_PREC = None     # set by Engine while it packs its weights
 _PREP_STATUS = 0      # device int32* the split-f16 convs flag range errors into
+_PREP_KSWS = (0, 0)   # (device float*, bytes): the engine's K-slice workspace
+KSWS_BYTES = 64 << 20
 
 # Optional per-tensor input exponents for split-f16 (OUHIP_SPLIT_AMAX=1): every
 # conv of a split engine records max |y| of what it stores (ConvDesc.amax_out,
@@ -116,6 +118,7 @@ class ConvW:
     prec: int = 0            # ConvDesc.prec the weights were packed for
     w_unscale: float = 1.0   # split-f16 weight scale (ou_conv_pack_split)
     status: int = 0          # device int32* for the split-f16 range flag (0 = none)
+    ks_ws: tuple = (0, 0)    # K-slice workspace (ptr, bytes) shared by the engine's convs
 
     @property
     def cout(self):
@@ -157,7 +160,8 @@ def make_conv(spec, device, prec=None):
     packed = torch.from_numpy(packed_np).to(device)
     b = None if spec.bias is None else torch.from_numpy(np.ascontiguousarray(spec.bias, np.float32)).to(device)
     return ConvW(m, spec.cin, kt, spec.frame, spec.pad, spec.rout, float(spec.slope), cc, packed, b,
-                 spec.shift, spec.ref_macs, int(prec), float(unscale), _PREP_STATUS if prec else 0)
+                 spec.shift, spec.ref_macs, int(prec), float(unscale), _PREP_STATUS if prec else 0,
+                 _PREP_KSWS)
 
 
 def _slope(sd, p):
@@ -319,6 +323,7 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
     d.in_scale, d.slope = in_scale or 0, cw.slope
     d.w, d.m, d.kt, d.pad, d.cc = cw.w.data_ptr(), cw.m, cw.kt, cw.pad, cw.cc
     d.prec, d.w_unscale, d.status = cw.prec, cw.w_unscale, cw.status
+    d.ks_ws, d.ks_ws_bytes = cw.ks_ws
     if _REC is not None and _REC["prec"] == 1:
         if cw.prec == 1 and x.ptr in _REC["slots"]:
             d.amax_in = _amax_slot(x)
@@ -449,13 +454,19 @@ class ConvTuner:
         # tile shape x log2(output tiles per workgroup); > 0 = persistent kernel
         # (bit 10: the warp-specialised persistent kernel)
         # (split-f16, bit 11 in the query only, and amax tracking: one-tile workgroups)
+        # K slices (bits 12-13) for one-tile shapes when the engine has a
+        # workspace; ou_conv refuses slices beyond the chunk count or workspace
+        ksl = (0, 1 << 12, 2 << 12, 3 << 12) if d.ks_ws else (0,)
         if d.prec in (1, 2):
-            cands = [t for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))]
+            cands = [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))
+                     for k in ksl]
         elif d.amax_out:
-            cands = [t for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t)]
+            cands = [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t) for k in ksl]
         else:
             cands = [t | v for t in range(lib.ou_conv_num_tiles()) for v in (0, 1 << 8, 2 << 8, 1 << 10)
                      if lib.ou_conv_tile_ok(d.kt, t | v)]
+            cands += [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t)
+                      for k in ksl[1:]]
         log = os.environ.get("OUHIP_TUNE_LOG")
         # candidates run on whatever the buffers hold at record time: keep
         # their split-f16 range flags out of the engine's status word
@@ -514,7 +525,7 @@ def enable_autotune(flag=True):
 class Engine:
     def __init__(self, model_cfg, sd, device, parts=("score", "cond", "sdl"), _record_only=False,
                  conv_prec=None):
-        global _PREP_PREC, _PREP_STATUS
+        global _PREP_PREC, _PREP_STATUS, _PREP_KSWS
         self.device = torch.device(device)
         self.conv_prec = default_conv_prec() if conv_prec is None else int(conv_prec)
         if self.device.type != "cuda" and not _record_only:
@@ -537,8 +548,12 @@ class Engine:
         self.has_sdl = False
         # [0] GRU hand-off timeout, [1] split-f16 conv range error (plan.check)
         self.status = torch.zeros(4, dtype=torch.int32, device=dev)
-        saved = _PREP_PREC, _PREP_STATUS
+        # K-slice partial sums (ou_conv tile bits 12-13): ops run one after
+        # another on the stream, so every conv of this engine shares one buffer
+        self.ks_ws = torch.empty(KSWS_BYTES // 4, dtype=torch.float32, device=dev)
+        saved = _PREP_PREC, _PREP_STATUS, _PREP_KSWS
         _PREP_PREC, _PREP_STATUS = self.conv_prec, self.status.data_ptr() + 4
+        _PREP_KSWS = (self.ks_ws.data_ptr(), KSWS_BYTES)
         try:
             with torch.no_grad():
                 if "score" in parts:
@@ -548,7 +563,7 @@ class Engine:
                 if "sdl" in parts:
                     self._prep_sdl(sd, "signal_decoupling_layer", dev)
         finally:
-            _PREP_PREC, _PREP_STATUS = saved
+            _PREP_PREC, _PREP_STATUS, _PREP_KSWS = saved
         enable_autotune(self.device.type == "cuda")
 
     # -------------------------------------------------------------- weights

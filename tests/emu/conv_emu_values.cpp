@@ -43,6 +43,7 @@ int main(int argc, char** argv)
         for (auto* v : {&wl, &x, &bias, &r1, &r2, &fm, &sc})
             for (auto& e : *v) e = rnd();
         std::vector<float> packed(ou_conv_packed_size(m, cin_eff, g.kt, 0)), packed_s(packed.size());
+        std::vector<float> ksws(4 << 20);   // K-slice partial sums
         ou_conv_pack(wl.data(), m, cin_eff, g.kt, 0, packed.data());
         float unscale = 0.f;
         ou_conv_pack_split(wl.data(), m, cin_eff, g.kt, packed_s.data(), &unscale);
@@ -78,9 +79,11 @@ int main(int argc, char** argv)
         for (double v : ref) rn += v * v;
         for (int t = 0; t < ou_conv_num_tiles(); ++t) {
             if (!ou_conv_tile_ok(g.kt, t)) continue;
-            for (int tpw = 0; tpw < 5; ++tpw) {   // 3: warp-specialised, 4: split-f16
+            // 3: warp-specialised, 4: split-f16, 5: f32 in 2 K slices, 6: split-f16 in 4 K slices
+            for (int tpw = 0; tpw < 7; ++tpw) {
                 if (tpw == 3 && g.rout != 1) continue;   // warp-specialised: plain convs only
-                if (!ou_conv_tile_ok(g.kt, t | (tpw == 4 ? 2048 : tpw == 3 ? 1024 : tpw << 8))) continue;
+                if (!ou_conv_tile_ok(g.kt, t | (tpw == 4 || tpw == 6 ? 2048 : tpw == 3 ? 1024 : tpw == 5 ? 0 : tpw << 8)))
+                    continue;
                 std::vector<float> y(ref.size(), 1e30f);
                 ou_conv_desc d{};
                 d.x = x.data(); d.x_bstride = (int64_t)g.cin * g.T; d.x_cstride = g.T;
@@ -92,13 +95,16 @@ int main(int argc, char** argv)
                 d.res1 = g.res1 ? r1.data() : nullptr; d.r1_bstride = d.y_bstride; d.r1_cstride = out_len; d.s1 = 0.7f;
                 d.film = g.film ? fm.data() : nullptr; d.film_bstride = 2 * g.cout;
                 d.res2 = g.res2 ? r2.data() : nullptr; d.r2_bstride = d.y_bstride; d.r2_cstride = out_len; d.s2 = 0.5f;
-                d.tile = t | (tpw == 4 ? 0 : tpw == 3 ? 1024 : tpw << 8);
-                if (tpw == 4) {
+                d.tile = t | (tpw == 4 ? 0 : tpw == 5 ? 1 << 12 : tpw == 6 ? 2 << 12 : tpw == 3 ? 1024 : tpw << 8);
+                if (tpw == 4 || tpw == 6) {
                     d.prec = 1;
                     d.w = packed_s.data();
                     d.w_unscale = unscale;
                 }
+                d.ks_ws = ksws.data();
+                d.ks_ws_bytes = (int64_t)ksws.size() * 4;
                 const int rc_ = ou_conv(&d, nullptr);
+                if (rc_ == -2 && tpw >= 5) continue;   // more K slices than chunks
                 if (rc_ == -2 && tpw == 3) continue;   // warp-specialised form refused for this geometry
                 if (rc_ != 0) {
                     std::printf("geom %d tile %d tpw %d: launch error\n", gi, t, tpw);

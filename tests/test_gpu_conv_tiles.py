@@ -15,6 +15,14 @@ from open_universe_amd import engine as E
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
+_KSWS = []
+
+
+def _ksws():
+    """K-slice workspace (64 MB, as an Engine holds)."""
+    if not _KSWS:
+        _KSWS.append(torch.empty(64 << 20 >> 2, dtype=torch.float32, device=DEV))
+    return _KSWS[0]
 
 # (cout, cin, frame, kt, T, batch, residual)
 GEOMS = [
@@ -80,6 +88,23 @@ def test_conv_every_tile(geom):
             err = ((y.t.cpu() - ref).norm() / ref.norm()).item()
             if not err < 1e-5:
                 bad.append((t, v, err))
+        # K slices (two launches: partial sums, then reduce + epilogue), both precisions
+        for prec, sl in ((0, 1), (1, 2), (1, 3)):
+            if not lib.ou_conv_tile_ok(kt, t | (prec << 11)):
+                continue
+            y = E.new_act(B, cout, U, DEV)
+            ra = E.Act(res.to(DEV)) if with_res else None
+            d = E.conv_desc(cws[prec], xa, y, res1=ra, s1=0.7, n_frames=U)
+            d.ks_ws, d.ks_ws_bytes = _ksws().data_ptr(), _ksws().numel() * 4
+            d.tile = t | (sl << 12)
+            rc = lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
+            if rc == -2:
+                continue   # more K slices than chunks, or workspace too small
+            assert rc == 0
+            torch.cuda.synchronize()
+            err = ((y.t.cpu() - ref).norm() / ref.norm()).item()
+            if not err < 1e-5:
+                bad.append((t, "ks", prec, sl, err))
     assert not bad, bad
 
 
