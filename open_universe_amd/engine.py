@@ -456,7 +456,10 @@ class ConvTuner:
         # (split-f16, bit 11 in the query only, and amax tracking: one-tile workgroups)
         # K slices (bits 12-13) for one-tile shapes when the engine has a
         # workspace; ou_conv refuses slices beyond the chunk count or workspace
-        ksl = (0, 1 << 12, 2 << 12, 3 << 12) if d.ks_ws else (0,)
+        # only where the grid is small (about 64 x 64 output tiles: under ~4
+        # workgroups per CU); elsewhere slices only add traffic
+        small = -(-d.n_frames // 64) * -(-d.m // 64) * d.batch <= 1024
+        ksl = (0, 1 << 12, 2 << 12, 3 << 12) if d.ks_ws and small else (0,)
         if d.prec in (1, 2):
             cands = [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))
                      for k in ksl]
@@ -500,6 +503,12 @@ class ConvTuner:
         d.tile = -1
         d.status = status
         self.cache[k] = best
+        if os.environ.get("OUHIP_TUNE_VERBOSE", "1") != "0":   # progress (long plan builds)
+            import sys
+
+            print(f"[ou tune] m={d.m} cin={d.cin} frame={d.frame} kt={d.kt} n={d.n_frames} b={d.batch} "
+                  f"rout={d.rout} prec={d.prec}: tile 0x{best:x} {best_ms * 1e3:.1f} us ({len(cands)} candidates)",
+                  file=sys.stderr, flush=True)
         self._save()
         return best
 

@@ -51,11 +51,19 @@ def main():
     from open_universe_amd.configs import get_config
     from open_universe_amd.networks.universe import UniverseGAN
 
-    d = load_golden("pp16")
-    cfg = get_config("pp16", None)
-    m = UniverseGAN(**{k: v for k, v in cfg.items() if k != "_target_"})
-    m.load_state_dict(golden_state_dict(d), strict=False)
-    m = m.to("cuda:0").eval()
+    import os
+
+    arch = os.environ.get("ARCH", "pp16")
+    if arch == "pp16":
+        d = load_golden("pp16")
+        cfg = get_config("pp16", None)
+        m = UniverseGAN(**{k: v for k, v in cfg.items() if k != "_target_"})
+        m.load_state_dict(golden_state_dict(d), strict=False)
+        m = m.to("cuda:0").eval()
+    else:   # bench.py's synthetic model of that architecture
+        import bench
+
+        cfg, m = bench.build_model("cuda:0", arch=arch)
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 128000
     mix = (0.1 * torch.randn(1, T, generator=torch.Generator().manual_seed(3))).to("cuda:0")
     from open_universe_amd.plan import EnhancePlan
