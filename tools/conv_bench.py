@@ -47,7 +47,9 @@ def make(name, dev, seed=0):
     y = E.new_act(1, m // rout, n * rout, dev)
     r = E.Act(torch.randn(1, m // rout, n * rout, device=dev)) if res else None
     d = E.conv_desc(cw, x, y, res1=r, s1=0.7, n_frames=n)
-    return d, (cw, x, y, r)
+    ws = torch.empty(E.KSWS_BYTES // 4, dtype=torch.float32, device=dev)   # K-slice workspace
+    d.ks_ws, d.ks_ws_bytes = ws.data_ptr(), E.KSWS_BYTES
+    return d, (cw, x, y, r, ws)
 
 
 def time_tile(d, tile, reps, stream):
@@ -85,8 +87,9 @@ def main():
     for name in names:
         d, keep = make(name, dev)
         if d.prec == 1:
-            tiles = [a.tile] if a.tile is not None else [t for t in range(lib.ou_conv_num_tiles())
-                                                          if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))]
+            tiles = [a.tile] if a.tile is not None else [t | k for t in range(lib.ou_conv_num_tiles())
+                                                          if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))
+                                                          for k in (0, 1 << 12, 2 << 12, 3 << 12)]
         else:
             tiles = [a.tile] if a.tile is not None else [t | v for t in range(lib.ou_conv_num_tiles())
                                                           for v in (0, 1 << 8, 2 << 8, 1 << 10)
@@ -98,7 +101,8 @@ def main():
                 res.append((ms, t))
         res.sort()
         fl = d._flops
-        nm = lambda t: f"t{t & 0xff}" + ("w" if t >> 10 else (f"p{1 << (t >> 8)}" if t >> 8 else ""))
+        nm = lambda t: (f"t{t & 0xff}" + ("w" if (t >> 10) & 1 else (f"p{1 << ((t >> 8) & 3)}" if (t >> 8) & 3 else ""))
+                        + (f"k{1 << (t >> 12)}" if t >> 12 else ""))
         line = "  ".join(f"{nm(t)}:{ms * 1e3:.1f}us" for ms, t in res[:12])
         print(f"{name:5s} {fl / 1e9:6.2f} GFLOP  best {nm(res[0][1])} {res[0][0] * 1e3:.1f} us "
               f"{fl / res[0][0] / 1e9:.1f} TF/s | {line}", flush=True)
