@@ -259,8 +259,13 @@ def main():
                 row = pmc.get("kernels", {}).get("conv_kernel")
                 if row:
                     traffic = row["traffic_bytes_per_launch"]
+                    per = "kernel dispatch"
+                    if pmc.get("enhances_profiled"):
+                        # per recorded conv op (K-slice ops dispatch twice)
+                        traffic = round(traffic * row["dispatches"] / pmc["enhances_profiled"] / prof["n_conv"])
+                        per = "ou_conv op (both launches of K-slice ops)"
                     tsrc = (f"{os.path.relpath(args.traffic_json, HERE)} ({pmc.get('tag', '')}): "
-                            "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes per ou_conv launch")
+                            f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes per {per}")
             if t_hbm > t_mfma:
                 rl = {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK, "peak_basis": "HBM3E",
                       "unit": "GB/s", "frac": round(gbps / HBM_PEAK, 4),
