@@ -72,7 +72,8 @@ struct Cfg {
     static constexpr int XG = W * CC / 4;            // float4 groups of X per chunk
     static constexpr int XE = (XG + 255) / 256;      // per thread
     static constexpr int AG = WM * MR * HQ * KT * 64;  // float4 of A per chunk
-    static constexpr int AE = (AG + 255) / 256;
+    static constexpr int AGL = P == 2 ? AG / 2 : AG;  // float4 of A staged (f16: hi halves only)
+    static constexpr int AE = (AGL + 255) / 256;
     static constexpr int XBUF = W * SX;
     static constexpr int STAGE = XBUF + AG * 4;
     static constexpr int RED = (WK - 1) * WM * WN * MR * NR * 16 * 64;
@@ -236,14 +237,23 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     }
     // packed weights: (mtiles * a_mt_stride) floats; one buffer resource
     const __amdgpu_buffer_rsrc_t wrs = ou_rsrc(d.w, (int64_t)mtiles * a_mt_stride * 4);
-    int aoff[C::AE];
+    int aoff[C::AE], adst[C::AE];   // global float offset and LDS float4 slot of each staged float4
 #pragma unroll
     for (int e = 0; e < C::AE; ++e) {
-        const int f = min(tid + e * 256, C::AG - 1);
-        const int ml = f / (C::HQ * KT * 64);
-        const int r = f - ml * (C::HQ * KT * 64);
+        const int f = min(tid + e * 256, C::AGL - 1);
+        int ml, r;
+        if constexpr (P == 2) {   // hi blocks only: [g8][hi][tap][lane] of each m-tile
+            ml = f / (C::HQ8 * KT * 64);
+            const int rh = f - ml * (C::HQ8 * KT * 64);
+            const int g8 = rh / (KT * 64);
+            r = g8 * 2 * KT * 64 + (rh - g8 * KT * 64);
+        } else {
+            ml = f / (C::HQ * KT * 64);
+            r = f - ml * (C::HQ * KT * 64);
+        }
         const int mtg = min(mt0 + ml, mtiles - 1);   // rows past M are computed, never stored
         aoff[e] = (int)(mtg * a_mt_stride) + r * 4;
+        adst[e] = ml * (C::HQ * KT * 64) + r;
     }
 
     float xr[4 * C::XE];   // plain float arrays: float4 arrays end up in scratch
@@ -328,8 +338,8 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
                                                         OU_PRELU(xr[4 * e + 2]), OU_PRELU(xr[4 * e + 3])); \
         }                                                                                      \
         float4* as_ = (float4*)(xs_ + C::XBUF);                                                \
-        _Pragma("unroll") for (int e = 0; e < C::AE; ++e) if (C::AG % 256 == 0 || tid + e * 256 < C::AG) \
-            as_[tid + e * 256] = make_float4(ar[4 * e], ar[4 * e + 1], ar[4 * e + 2], ar[4 * e + 3]); \
+        _Pragma("unroll") for (int e = 0; e < C::AE; ++e) if (C::AGL % 256 == 0 || tid + e * 256 < C::AGL) \
+            as_[adst[e]] = make_float4(ar[4 * e], ar[4 * e + 1], ar[4 * e + 2], ar[4 * e + 3]); \
     }
 
     floatx16 acc[MR][NR];
@@ -341,7 +351,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
         for (int j = 0; j < NR; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    if constexpr (P) {
+    if constexpr (P == 1) {
 #pragma unroll
         for (int i = 0; i < MR; ++i)
 #pragma unroll

@@ -28,7 +28,7 @@ static int run(const Geom& g, int tile)
     const int64_t np = ou_conv_packed_size(m, cin_eff, g.kt, 0);
     float* w = alloc(np);
     float unscale = 1.f;
-    const bool split = tile & 2048;   // split-f16 form (d.prec = 1)
+    const bool split = tile & 2048;   // split-f16 form (d.prec = 1; 2 with bit 12: f16)
     if (split)
         ou_conv_pack_split(wl.data(), m, cin_eff, g.kt, w, &unscale);
     else
@@ -51,8 +51,8 @@ static int run(const Geom& g, int tile)
     d.res1 = r1; d.r1_bstride = d.y_bstride; d.r1_cstride = d.y_cstride; d.s1 = 0.7f;
     d.film = fm; d.film_bstride = 2 * g.cout;
     d.res2 = r2; d.r2_bstride = d.y_bstride; d.r2_cstride = d.y_cstride; d.s2 = 0.5f;
-    d.tile = tile & ~2048;
-    d.prec = split ? 1 : 0;
+    d.tile = tile & ~(2048 | 4096);
+    d.prec = split ? ((tile & 4096) ? 2 : 1) : 0;
     d.w_unscale = unscale;
     const int rc = ou_conv(&d, nullptr);
     for (float* p : {w, x, y, bias, r1, r2, fm, sc}) std::free(p);
@@ -80,12 +80,12 @@ int main(int argc, char** argv)
         const Geom& g = geoms[gi];
         for (int t = 0; t < ou_conv_num_tiles(); ++t) {
             if (!ou_conv_tile_ok(g.kt, t)) continue;
-            for (int tpw = 0; tpw < 5; ++tpw) {   // 3: warp-specialised, 4: split-f16
+            for (int tpw = 0; tpw < 6; ++tpw) {   // 3: warp-specialised, 4: split-f16, 5: f16
                 if (tpw == 3 && g.rout != 1) continue;   // warp-specialised: plain convs only
-                const int v = tpw == 4 ? 2048 : tpw == 3 ? 1024 : tpw << 8;
+                const int v = tpw >= 4 ? 2048 : tpw == 3 ? 1024 : tpw << 8;
                 if (!ou_conv_tile_ok(g.kt, t | v)) continue;
                 if (std::getenv("OUHIP_EMU_VERBOSE")) std::fprintf(stderr, "geom %d tile %d tpw %d\n", gi, t, tpw);
-                const int rc = run(g, t | v);
+                const int rc = run(g, t | v | (tpw == 5 ? 4096 : 0));
                 if (rc == -2 && tpw == 3) continue;   // warp-specialised form refused for this geometry
                 if (rc != 0) {
                     std::fprintf(stderr, "geom %d tile %d tpw %d: ou_conv returned %d\n", gi, t, tpw, rc);
