@@ -7,9 +7,14 @@ One step = one ``model.enhance()`` of one synthetic 8 s clip at batch 1
 (BASELINE.json configs[1]: "UNIVERSE++ 16 kHz, batch=1, 8 s clips"), run as
 the production path does it: one hipGraph replay of the recorded sampler
 (conditioner + 8 score-network passes + sampler updates).  Every rank (one
-process per GPU, torchrun) enhances its own clips -- utterances shard across
-GPUs with no collective on the data path -- so scaling is weak; ``value`` is
-the whole-job audio-seconds per second: N * K * 8 s / max-over-ranks time.
+process per GPU) enhances its own clips -- utterances shard across GPUs with
+no collective on the data path -- so scaling is weak; ``value`` is the
+whole-job audio-seconds per second: N * K * 8 s / max-over-ranks time
+(``value_per_gpu`` = value / N, the per-GPU figure the metric names).
+
+Ranks: under torchrun (WORLD_SIZE set) this process is one rank.  Without it,
+``--gpus N`` (N > 1) starts the N rank processes itself before touching the
+GPU (``launch_ranks``), each with the torchrun environment, and waits for them.
 
 Extra fields:
   roofline      the dominant kernel (ou_conv, every launch of one enhance):
@@ -20,7 +25,10 @@ Extra fields:
                 stream; the bound is whichever of FLOPs/MFMA peak and
                 bytes/HBM peak is larger.
   cpu_baseline  the CPU restatement of the reference op sequence (oracle/,
-                plain PyTorch) on this host's cores, bounded sample.
+                plain PyTorch) on this host's cores, bounded sample, B = 1
+                and the config's B.
+  f32_value     (c2) a second timed pass with f32 conv operands, beside the
+                default split-f16 operand build.
 Weights are synthetic (no trained checkpoint offline); timing does not depend
 on weight values.
 """
@@ -84,33 +92,74 @@ def build_model(device, nch=None, seed=0, arch="pp16"):
     return cfg, m.to(device).eval()
 
 
-def cpu_baseline(model, cfg, seconds):
-    """Oracle (CPU restatement of the reference ops) on a bounded sample:
-    one 8 s clip, 1 warm-up + best of 3."""
+def available_cpus():
+    """CPUs this process may use: os.cpu_count(),
+    bounded by the affinity mask and the cgroup CPU quota when either is
+    smaller (a GPU box shares its host: os.cpu_count() shows the whole
+    machine, the quota is this job's share)."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, period = fh.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    if quota:
+        n = min(n, max(1, int(math.ceil(quota))))
+    return n, quota
+
+
+# CPU sample per config: (clip seconds at B=1, clip seconds at the config's B).
+# Bounded so each leg is a few seconds of oracle work (c2: the full 8 s clip).
+CPU_SAMPLE = {"c2": (8.0, 8.0), "c3": (1.0, 0.25), "c4": (2.0, 0.1), "c5": (8.0, 8.0)}
+
+
+def cpu_baseline(model, cfg, C, config_name):
+    """The oracle (CPU restatement of the reference ops, oracle/ou_oracle.py)
+    on a bounded sample of the workload: B=1 and the config's B, one warm-up
+    then best of 3.  The headline ``value`` is the
+    config-B leg (the B=1 leg is reported beside it)."""
     import numpy as np
     import torch
 
     from oracle import ou_oracle
     from open_universe_amd.utils.synthetic import synth_audio
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    threads, quota = available_cpus()
     torch.set_num_threads(threads)
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     orc = ou_oracle.Oracle(sd, cfg)
-    T = int(seconds * FS)
-    mix = torch.from_numpy(synth_audio(T, FS, 99)[0])[None]
-    best = float("inf")
-    with torch.no_grad():
-        for i in range(4):
-            t0 = time.perf_counter()
-            orc.enhance(mix, rng=torch.Generator().manual_seed(1028282))
-            dt = time.perf_counter() - t0
-            if i > 0:
-                best = min(best, dt)
-    return {"value": round(seconds / best, 4), "unit": "audio-s/s", "cores": threads,
-            "kind": "port",
-            "sample": f"oracle/ou_oracle.py Oracle.enhance, UNIVERSE++ 16 kHz, one {seconds:g} s clip, "
-                      f"B=1, 8 steps, fp32, best of 3 after 1 warm-up ({best:.3f} s), {cpu_model()}"}
+    fs = int(cfg["fs"])
+    ekw = {"n_steps": C["n_steps"]} if C["n_steps"] else {}
+    legs = {}
+    s1, sB = CPU_SAMPLE[config_name]
+    Bc = C["batch"]
+    for B, secs in ((1, s1), (Bc, sB)):
+        if B in legs:
+            continue
+        T = int(secs * fs)
+        mix = torch.from_numpy(np.stack([synth_audio(T, fs, 99 + j)[0] for j in range(B)]))
+        best = float("inf")
+        with torch.no_grad():
+            for i in range(4):
+                t0 = time.perf_counter()
+                orc.enhance(mix, rng=torch.Generator().manual_seed(1028282), **ekw)
+                dt = time.perf_counter() - t0
+                if i > 0:
+                    best = min(best, dt)
+        legs[B] = {"value": round(B * secs / best, 4), "batch": B, "clip_s": secs, "best_s": round(best, 3)}
+    head = legs[Bc]
+    return {"value": head["value"], "unit": "audio-s/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_quota": quota, "legs": list(legs.values()),
+            "sample": f"oracle/ou_oracle.py Oracle.enhance ({C['arch']}, {C['n_steps'] or 8} steps, fp32), "
+                      f"torch.set_num_threads({threads}); value = the B={Bc} leg ({head['clip_s']:g} s clips), "
+                      f"B=1 leg in legs; 1 warm-up + best of 3 per leg; {cpu_model()}"}
 
 
 def profile_roofline(plan, stream, dump=None):
@@ -138,6 +187,75 @@ def profile_roofline(plan, stream, dump=None):
     }
 
 
+def launch_ranks(n, argv):
+    """``bench.py --gpus N`` without an outer torchrun: start N rank processes
+    (one per GPU) before anything in this parent touches the GPU, wait for
+    them and return the worst exit code.  Each child gets the torchrun
+    environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1,
+    MASTER_PORT) and joins the gloo barrier / max-over-ranks like a torchrun
+    rank; rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    try:
+        for p in procs:
+            rc = max(rc, p.wait())
+            if rc:
+                break
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+    return rc
+
+
+def rank_batch(C, world):
+    """Clips per rank: the config's batch per GPU, or (node_batch configs, C4)
+    the whole-node batch split into equal contiguous shards (equal-length clips;
+    sharding.shard_utterances gives the same split)."""
+    if not C.get("node_batch"):
+        return C["batch"]
+    if C["batch"] % world:
+        raise ValueError(f"{C['batch']} clips do not shard evenly over {world} ranks")
+    return C["batch"] // world
+
+
+def timed_loop(step, warmup, steps, world, sync):
+    """W untimed steps, then K steps bracketed by barrier + device sync; the
+    elapsed time is the max over ranks."""
+    import torch.distributed as dist
+
+    from open_universe_amd.sharding import max_over_ranks
+
+    for i in range(warmup):
+        step(i)
+    sync()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i)
+    sync()
+    if world > 1:
+        dist.barrier()
+    return max_over_ranks(time.perf_counter() - t0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,32 +266,51 @@ def main():
     ap.add_argument("--seconds", type=float, default=None, help="override the config's clip length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-f32-pass", action="store_true",
+                    help="skip the second timed pass with f32 conv operands (f32_value)")
     ap.add_argument("--dump-ops", default=None, help="write per-op profile rows (JSON)")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "pmc_latest.json"),
                     help="per-kernel HBM traffic from tools/pmc_summary.py (rocprofv3 PMC passes)")
+    ap.add_argument("--stub-ms", type=float, default=None, help=argparse.SUPPRESS)  # CPU test of the launcher
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import numpy as np
     import torch
     import torch.distributed as dist
 
+    from open_universe_amd.sharding import dist_env
     from open_universe_amd.utils.synthetic import synth_audio
-
-    from open_universe_amd.sharding import dist_env, max_over_ranks
 
     rank, local, world = dist_env()
     if world > 1:
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
+    if world != args.gpus and rank == 0:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: reporting {world}", file=sys.stderr)
     C = CONFIGS[args.config]
-    if C.get("conv_prec") and "OUHIP_CONV_PREC" not in os.environ:
-        os.environ["OUHIP_CONV_PREC"] = C["conv_prec"]
     if args.seconds is None:
         args.seconds = C["seconds"]
-    B = C["batch"] // world if C.get("node_batch") else C["batch"]
-    assert B >= 1, "c4 shards 32 clips over at most 32 ranks"
+    B = rank_batch(C, world)
+
+    if args.stub_ms is not None:
+        # launcher/control-plane test without a GPU: a step is a sleep
+        elapsed = timed_loop(lambda i: time.sleep(args.stub_ms * 1e-3), args.warmup, args.steps, world,
+                             lambda: None)
+        if rank == 0:
+            print(json.dumps({"metric": "stub", "value": world * B * args.steps * args.seconds / elapsed,
+                              "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                              "ms_per_step": 1000.0 * elapsed / args.steps,
+                              "config": {"global_batch": world * B, "batch_per_gpu": B}}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if C.get("conv_prec") and "OUHIP_CONV_PREC" not in os.environ:
+        os.environ["OUHIP_CONV_PREC"] = C["conv_prec"]
     cfg, model = build_model(dev, arch=C["arch"])
     fs = int(cfg["fs"])
     T = int(args.seconds * fs)
@@ -182,21 +319,11 @@ def main():
              .to(dev) for i in range(min(n_clips, 4))]
     rng = torch.Generator(device=dev).manual_seed(1028282 + rank)
     ekw = {"n_steps": C["n_steps"]} if C["n_steps"] else {}
+    sync = lambda: torch.cuda.synchronize(dev)
 
     with torch.no_grad():
-        for i in range(args.warmup):
-            model.enhance(clips[i % len(clips)], rng=rng, **ekw)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            model.enhance(clips[(args.warmup + i) % len(clips)], rng=rng, **ekw)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed)
+        elapsed = timed_loop(lambda i: model.enhance(clips[i % len(clips)], rng=rng, **ekw),
+                             args.warmup, args.steps, world, sync)
 
     prof = None
     if not args.no_profile:
@@ -206,11 +333,24 @@ def main():
             plan.draw_noise(rng)
             prof = profile_roofline(plan, torch.cuda.current_stream(dev).cuda_stream, args.dump_ops)
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
-        cpu = cpu_baseline(model, cfg, args.seconds)
-
     prec = model._get_engine().conv_prec
+    # the strictly-f32 figure: a second timed pass with f32 conv operands
+    f32 = None
+    if prec != 0 and not args.no_f32_pass and args.config == "c2":
+        _, m32 = build_model(dev, arch=C["arch"])
+        m32._conv_prec = 0
+        with torch.no_grad():
+            e32 = timed_loop(lambda i: m32.enhance(clips[i % len(clips)], rng=rng, **ekw),
+                             args.warmup, args.steps, world, sync)
+        assert m32._get_engine().conv_prec == 0
+        f32 = {"value": round(world * B * args.steps * args.seconds / e32, 3),
+               "ms_per_step": round(1000.0 * e32 / args.steps, 3)}
+        del m32
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(model, cfg, C, args.config)
+
     if prec == 1:
         dtype = "f32 (conv operands split into f16 hi/lo: 3 f16 MFMA passes, f32 accumulation)"
         peak, peak_basis = round(F16_PEAK_TF / 3, 1), "dense f16 MFMA peak / 3 passes per f32 MAC"
@@ -228,6 +368,9 @@ def main():
             "bench_config": args.config,
             "value": round(value, 3),
             "unit": "audio-s/s",
+            "value_semantics": "whole job: audio-seconds enhanced by all n_gpus ranks / max-over-ranks wall "
+                               "time (bench contract); the per-GPU figure the metric names is value_per_gpu",
+            "value_per_gpu": round(value / world, 3),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -245,6 +388,10 @@ def main():
                        "parallelism": f"utterance-shard x{world}"},
             "xrt_per_gpu": round(value / world, 3),
         }
+        if f32 is not None:
+            out["f32_value"] = f32["value"]
+            out["f32_pass"] = {**f32, "dtype": "f32 (v_mfma_f32_32x32x2_f32 conv operands)",
+                               "steps": args.steps, "warmup": args.warmup}
         if prof is not None:
             # the roofline that binds ou_conv over one enhance: the larger of
             # FLOPs / MFMA peak and algorithmic bytes / HBM peak
@@ -257,7 +404,7 @@ def main():
                 with open(args.traffic_json) as fh:
                     pmc = json.load(fh)
                 row = pmc.get("kernels", {}).get("conv_kernel")
-                if row:
+                if row and pmc.get("config", "c2") == args.config:
                     traffic = row["traffic_bytes_per_launch"]
                     per = "kernel dispatch"
                     if pmc.get("enhances_profiled"):
