@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define OUHIP_ABI_VERSION 2
+#define OUHIP_ABI_VERSION 3
 
 int ou_abi_version(void);
 const char* ou_last_error(void);
@@ -256,9 +256,16 @@ int ou_scale(const float* z, float* y, int64_t n, float scale, const float* add,
  * peak when it exceeds 1.                                                 */
 int ou_finish(const float* x, int64_t x_bstride, int left, float* y, int batch,
               int len, const float* mix_rms, void* stream);
-/* Elementwise median / mean over an ensemble of E results, [E][n] -> [n]. */
+/* Elementwise median / mean over an ensemble of E results, [E][n] -> [n]
+ * (universe.py:359-366: x.mean(dim=0) / x.median(dim=0).values, lower median). */
 int ou_ensemble_reduce(const float* x, float* y, int ensemble, int64_t n,
                        int mode /* 0 mean, 1 median */, void* stream);
+/* Ensemble signal_median (universe.py:366-367 -> utils/stats.py:22-66):
+ * x [E][batch][n] -> y [batch][n] = the member selected by the reference's
+ * per-sample rank vote.  counts: device int32 workspace [batch][32] (zeroed
+ * here).  E <= 32. */
+int ou_signal_median(const float* x, float* y, int ensemble, int batch, int64_t n, int* counts,
+                     void* stream);
 
 /* Audio-rate resampling around enhance(): replaces
  * torchaudio.functional.resample(x, orig, new) with its defaults
@@ -349,8 +356,10 @@ typedef struct ou_finish_args {
 typedef struct ou_ensemble_args {
     const float* x;
     float* y;
-    int32_t ensemble, mode;
-    int64_t n;
+    int32_t ensemble, mode;    /* mode 0 mean, 1 median, 2 signal_median   */
+    int64_t n;                 /* batch * samples                          */
+    int32_t batch, _pad;       /* signal_median: batch items (n / batch each) */
+    int32_t* counts;           /* signal_median: [batch][32] int32 workspace */
 } ou_ensemble_args;
 
 ou_program* ou_program_create(void);

@@ -12,7 +12,7 @@ from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OUHIP_LIB", os.path.join(_HERE, "libouhip.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 fp = c_void_p  # device pointers are passed as integers
 
@@ -116,7 +116,8 @@ class FinishArgs(ctypes.Structure):
 
 
 class EnsembleArgs(ctypes.Structure):
-    _fields_ = [("x", fp), ("y", fp), ("ensemble", c_int32), ("mode", c_int32), ("n", c_int64)]
+    _fields_ = [("x", fp), ("y", fp), ("ensemble", c_int32), ("mode", c_int32), ("n", c_int64),
+                ("batch", c_int32), ("_pad", c_int32), ("counts", c_void_p)]
 
 
 OP_STRUCT = {
@@ -152,6 +153,7 @@ EXPORTS = {
     "ou_scale": (c_int, [fp, fp, c_int64, c_float, fp, c_void_p]),
     "ou_finish": (c_int, [fp, c_int64, c_int, fp, c_int, c_int, fp, c_void_p]),
     "ou_ensemble_reduce": (c_int, [fp, fp, c_int, c_int64, c_int, c_void_p]),
+    "ou_signal_median": (c_int, [fp, fp, c_int, c_int, c_int64, c_void_p, c_void_p]),
     "ou_snake_aa": (c_int, [POINTER(SnakeDesc), c_void_p]),
     "ou_resample": (c_int, [fp, c_int64, fp, c_int64, c_int, c_int, c_int, fp, c_int, c_int, c_int, c_int,
                             c_void_p]),

@@ -10,12 +10,14 @@
 //                 (universe.py:259,352-357)
 //  * ou_snake_aa  alias-free Snake of the signal-decoupling layer
 //                 (bigvgan/snake.py:131-157, alias_free_act.py:8-30)
-//  * small elementwise helpers (pad, scale, |STFT|^2, ensemble reduce)
+//  * small elementwise helpers (pad, scale, |STFT|^2, ensemble mean/median)
+//  * ou_signal_median  ensemble signal_median (utils/stats.py:22-66)
 //
 // All of these are HBM- or latency-bound and tiny next to the conv stack; they
 // exist so that no op of the sampler leaves the device or touches ATen.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "../../include/ouhip.h"
@@ -301,6 +303,67 @@ __global__ void ensemble_kernel(const float* x, float* y, int E, int64_t n, int 
     y[i] = v[(E - 1) / 2];   // torch.median: lower median
 }
 
+// ---------------------------------------------------------------- signal median
+// utils/stats.py:22-66 (signal_median) over x[E][B][n]: at every sample the
+// reference sorts the E members, takes the rank position k at which the member
+// whose INDEX is closest to E/2 sits (argmin over the sorted index list, first
+// occurrence), histograms k over the samples of each batch item, and returns
+// the member whose index equals the most frequent k (argmax, first
+// occurrence).  Rank of member j: #{i : x_i < x_j} + #{i < j : x_i == x_j}
+// (the sort order of a stable sort).  Candidates: j = E/2 for even E; for odd
+// E the two members (E-1)/2 and (E+1)/2 tie at distance 1/2 and the one
+// sorted first wins.
+__device__ __forceinline__ int member_rank(const float* x, int64_t estride, int E, int j)
+{
+    const float v = x[(int64_t)j * estride];
+    int r = 0;
+    for (int i = 0; i < E; ++i) {
+        const float u = x[(int64_t)i * estride];
+        r += (u < v) || (u == v && i < j);
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(256) void sigmed_vote_kernel(const float* x, int E, int B, int64_t n,
+                                                          int* counts)
+{
+    __shared__ int hist[32];
+    const int b = blockIdx.y;
+    if (threadIdx.x < 32) hist[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t es = (int64_t)B * n;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float* xs = x + (int64_t)b * n + i;
+        int k;
+        if ((E & 1) == 0) {
+            k = member_rank(xs, es, E, E / 2);
+        } else {
+            k = member_rank(xs, es, E, (E - 1) / 2);
+            if (E > 1) k = min(k, member_rank(xs, es, E, (E + 1) / 2));
+        }
+        atomicAdd(&hist[k], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < E && hist[threadIdx.x]) atomicAdd(&counts[b * 32 + threadIdx.x], hist[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void sigmed_pick_kernel(const float* x, float* y, int E, int B, int64_t n,
+                                                          const int* counts)
+{
+    const int b = blockIdx.y;
+    int sel = 0, best = counts[b * 32];
+    for (int e = 1; e < E; ++e) {
+        const int c = counts[b * 32 + e];
+        if (c > best) best = c, sel = e;
+    }
+    const float* xs = x + ((int64_t)sel * B + b) * n;
+    float* ys = y + (int64_t)b * n;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        ys[i] = xs[i];
+}
+
 // ---------------------------------------------------------------- alias-free snake
 // y[b][c][t] = down2( snake( up2(h[b][c][:]) ) )[t]
 //   up2:   u[2s + i] = sum_k ku[i][k] * h[s + k - wu]       (torchaudio Resample 1->2)
@@ -454,6 +517,22 @@ extern "C" int ou_ensemble_reduce(const float* x, float* y, int ensemble, int64_
     hipLaunchKernelGGL(ensemble_kernel, dim3(blocks_for(n, 256)), dim3(256), 0,
                        (hipStream_t)stream, x, y, ensemble, n, mode);
     return ou_check_launch("ensemble");
+}
+
+extern "C" int ou_signal_median(const float* x, float* y, int ensemble, int batch, int64_t n, int* counts,
+                                void* stream)
+{
+    if (!x || !y || !counts || ensemble <= 0 || ensemble > 32 || batch <= 0 || n <= 0)
+        return ou_fail(-1, "signal_median: bad args (ensemble <= 32)");
+    hipStream_t s = (hipStream_t)stream;
+    OU_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int) * 32 * (size_t)batch, s), "signal_median counts");
+    const unsigned gx = (unsigned)std::min<int64_t>(blocks_for(n, 256), 1024);
+    hipLaunchKernelGGL(sigmed_vote_kernel, dim3(gx, batch), dim3(256), 0, s, x, ensemble, batch, n, counts);
+    int rc = ou_check_launch("signal_median vote");
+    if (rc) return rc;
+    hipLaunchKernelGGL(sigmed_pick_kernel, dim3(gx, batch), dim3(256), 0, s, x, y, ensemble, batch, n,
+                       (const int*)counts);
+    return ou_check_launch("signal_median pick");
 }
 
 extern "C" int ou_snake_aa(const ou_snake_desc* d, void* stream)

@@ -89,6 +89,10 @@ static int run_op(int kind, const void* p, hipStream_t s)
     }
     case OU_OP_ENSEMBLE: {
         auto a = (const ou_ensemble_args*)p;
+        if (a->mode == 2) {
+            if (a->batch <= 0 || a->n % a->batch) return ou_fail(-1, "ensemble: bad batch");
+            return ou_signal_median(a->x, a->y, a->ensemble, a->batch, a->n / a->batch, a->counts, s);
+        }
         return ou_ensemble_reduce(a->x, a->y, a->ensemble, a->n, a->mode, s);
     }
     }

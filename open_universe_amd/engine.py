@@ -437,9 +437,10 @@ class ConvTuner:
 
     @staticmethod
     def key(d):
+        # bool(ks_ws): K-slice tiles are only valid with a workspace
         return (d.m, d.cin, d.frame, d.kt, d.pad, d.n_frames, d.batch, d.rout, d.in_len,
                 d.out_len, bool(d.res1), bool(d.film), bool(d.res2), bool(d.in_scale), d.prec,
-                bool(d.amax_out))
+                bool(d.amax_out), bool(d.ks_ws))
 
     def __call__(self, d):
         import ctypes

@@ -5,7 +5,9 @@ Reads the reference's checkpoint layout unchanged:
     ``../../../.hydra/`` (model_loader.py:33-51); hydra ``_target_`` strings of
     ``open_universe.networks.universe{,_orig}.*`` resolve to this package's
     classes, ``${a.b.c}`` interpolations are resolved without omegaconf;
-  * ``torch.load(...)["state_dict"]``; discriminator / MDN loss keys
+  * ``torch.load(..., weights_only=True)["state_dict"]`` (Lightning's
+    pickled ``hyper_parameters`` etc. load as inert stand-ins, see
+    ``load_checkpoint``); discriminator / MDN loss keys
     (``loss_*``) are training-only and skipped;
   * the torch_ema block ``ckpt["ema"]["shadow_params"]``, a positional list in
     ``model.model_parameters()`` order, which ``Universe.eval()`` copies over
@@ -85,6 +87,51 @@ def instantiate(cfg):
     return _TARGETS[name](**{k: v for k, v in cfg.items() if k != "_target_"})
 
 
+class _Inert:
+    """Stand-in for one of the hyper-parameter classes listed below
+    (omegaconf ``DictConfig`` / node / metadata objects and the typing and
+    builtins globals their metadata names).  Constructing it and setting its
+    state run no code from the file; the loader never reads these objects."""
+
+    def __init__(self, *args, **kwargs):
+        pass
+
+    def __setstate__(self, state):
+        self.__dict__["_state"] = state
+
+
+# The non-tensor globals a checkpoint of the reference's Lightning trainer
+# names (save_hyperparameters(), universe.py:66, pickles omegaconf containers
+# into ``hyper_parameters``): each is allow-listed for the weights-only
+# unpickler as an inert ``_Inert`` stand-in, never as the real class.
+_HPARAM_GLOBALS = (
+    ["omegaconf.dictconfig.DictConfig", "omegaconf.listconfig.ListConfig",
+     "omegaconf.base.ContainerMetadata", "omegaconf.base.Metadata", "omegaconf.base.Node",
+     "omegaconf.base.Container", "omegaconf.basecontainer.BaseContainer"]
+    + [f"omegaconf.nodes.{n}" for n in ("AnyNode", "ValueNode", "StringNode", "IntegerNode", "FloatNode",
+                                         "BooleanNode", "BytesNode", "PathNode", "EnumNode")]
+    + ["typing.Any"]
+    + [f"builtins.{n}" for n in ("dict", "list", "int", "float", "str", "bool")]
+    + ["pytorch_lightning.utilities.parsing.AttributeDict", "lightning_fabric.utilities.data.AttributeDict"]
+)
+
+
+def load_checkpoint(path):
+    """``torch.load(path, weights_only=True)`` that also accepts a checkpoint
+    the reference's Lightning trainer wrote: the fixed list of
+    hyper-parameter globals above loads as inert stand-ins.  Anything else the
+    weights-only unpickler refuses still raises.  Only ``state_dict`` and
+    ``ema`` are read from the result."""
+    stubs = []
+    for name in _HPARAM_GLOBALS:
+        stub = type(name.rsplit(".", 1)[-1], (_Inert,), {})
+        stubs.append((stub, name))
+        if name.startswith("builtins."):   # the unpickler may name builtins bare
+            stubs.append((stub, name[len("builtins."):]))
+    with torch.serialization.safe_globals(stubs):
+        return torch.load(path, map_location="cpu", weights_only=True)
+
+
 def load_model(ckpt_path, device=None, strict=True, return_config=False, hf_token=None):
     """Load a model from a checkpoint file (or a Hugging Face id when the hub is
     reachable) -- model_loader.py:65-140."""
@@ -107,7 +154,7 @@ def load_model(ckpt_path, device=None, strict=True, return_config=False, hf_toke
 
     config = open_update_config(config_path)
     model = instantiate(config["model"])
-    data = torch.load(ckpt_path, map_location="cpu", weights_only=True)
+    data = load_checkpoint(ckpt_path)
     state = {k: v for k, v in data["state_dict"].items() if not k.startswith("loss_")}
     if "ema" in data and data["ema"] is not None:
         model.load_state_dict(state, strict=False)

@@ -1,5 +1,12 @@
 """``add_enhance_arguments`` (mirrors inference_utils/signature_to_parser.py:26-66):
-argparse options generated from ``typing.get_type_hints(model.enhance)``."""
+argparse options generated from ``typing.get_type_hints(model.enhance)``.
+
+This function follows the reference's own implementation closely because the
+CLI contract is the function itself (the argument names, types and defaults
+the reference CLI derives from the type hints).  That implementation is
+Copyright 2024 LY Corporation, licensed under the Apache License, Version 2.0
+(http://www.apache.org/licenses/LICENSE-2.0).
+"""
 import typing
 
 

@@ -195,9 +195,8 @@ class Universe(nn.Module):
             mix = mix.to(torch.float32).contiguous()
             eng = self._get_engine()
             B, _, T = mix.shape
-            # mean / median reduce on the device inside the plan; signal_median
-            # needs the whole ensemble (tensor ops below)
-            ens_mode = {"mean": 0, "median": 1}.get(ensemble_stat) if ensemble is not None else None
+            # mean / median / signal_median reduce on the device inside the plan
+            ens_mode = {"mean": 0, "median": 1, "signal_median": 2}[ensemble_stat] if ensemble is not None else None
             key = (B, T, int(n_steps), float(epsilon), bool(keep_rms), bool(use_aux_signal),
                    warm_start, ensemble, ens_mode)
             def make_plan(eng):
@@ -219,8 +218,6 @@ class Universe(nn.Module):
                 self.invalidate()
                 plan = self._plans[key] = make_plan(self._get_engine())
                 x = plan.run_with_noise(mix, nz).clone()[:, None, :]
-            if ensemble is not None and ens_mode is None:
-                x = self._ensemble_reduce(x.view((-1,) + tuple(mix_shape)), ensemble_stat)
         if x_ndim == 1:
             x = x[0, 0]
         elif x_ndim == 2:
@@ -229,16 +226,12 @@ class Universe(nn.Module):
 
     @staticmethod
     def _ensemble_reduce(x, stat):
-        """universe.py:359-368 (x: (E, B, 1, T))."""
-        from ...utils.stats import signal_median
+        """universe.py:359-368 for the known-answer mode (x: (E, B, 1, T) on
+        the device): the same ou_ensemble_reduce / ou_signal_median kernels
+        the recorded plans use."""
+        from ...utils.stats import ensemble_reduce
 
-        if stat == "mean":
-            return x.mean(dim=0)
-        if stat == "median":
-            return x.median(dim=0).values
-        if stat == "signal_median":
-            return signal_median(x)
-        raise NotImplementedError()
+        return ensemble_reduce(x, stat)
 
     def _enhance_fake_score(self, mix, n_steps, epsilon, target, fake_score_snr, rng, keep_rms,
                             ensemble, ensemble_stat):

@@ -201,14 +201,18 @@ class EnhancePlan(_PlanBase):
         p.add(L.OP_FINISH, L.FinishArgs(x=x_final.ptr, x_bstride=Tp, left=self.pad // 2,
                                         batch=B, len=mix_len, y=self.OUT.data_ptr(),
                                         mix_rms=self.MIXRMS.data_ptr() if keep_rms else 0))
-        # ensemble reduction (universe.py:359-366): B = E x B0 results -> B0
+        # ensemble reduction (universe.py:359-368): B = E x B0 results -> B0
+        # (mode 0 mean, 1 median, 2 signal_median)
         self.RED = None
         if ensemble is not None and ensemble_mode is not None:
             assert B % ensemble == 0
-            self.RED = torch.empty((B // ensemble, mix_len), dtype=torch.float32, device=dev)
+            B0 = B // ensemble
+            self.RED = torch.empty((B0, mix_len), dtype=torch.float32, device=dev)
+            # signal_median (mode 2): per-batch-item vote counts
+            self.CNT = torch.zeros((B0, 32), dtype=torch.int32, device=dev)
             p.add(L.OP_ENSEMBLE, L.EnsembleArgs(x=self.OUT.data_ptr(), y=self.RED.data_ptr(),
                                                 ensemble=ensemble, mode=ensemble_mode,
-                                                n=(B // ensemble) * mix_len))
+                                                n=B0 * mix_len, batch=B0, counts=self.CNT.data_ptr()))
 
     def draw_noise(self, rng):
         """Noise in the reference's draw order (universe.py:39-41,326,338):

@@ -1,52 +1,39 @@
-"""Amplitude normalisation (mirrors utils/norm.py:22-91).
+"""Batch level normalisation (reference utils/norm.py:47-91, ``norm=2``).
 
-On the enhance() path this runs as the ``ou_normalize`` kernel; this tensor
-version serves the sampler known-answer mode and API parity.
+On the enhance() path this is the ``ou_normalize`` kernel.  This tensor form
+serves only the sampler known-answer mode (``enhance(target=...)``), whose
+arithmetic is tensor ops by design; ``Universe`` accepts ``norm=2`` only, so
+the ``"max"`` / ``"2-max"`` norms are not restated.
 """
 import torch
 
 
-def _norm2(signal, eps=1e-5):
-    return signal.std(dim=(1, 2), keepdim=True).clamp(min=eps)
-
-
-def _norm_max(signal, eps=1e-5):
-    std = abs(signal.view((signal.shape[0], -1))).max(dim=1).values
-    return std[:, None, None].clamp(min=eps)
-
-
-def _compute_gain(signal, norm, level, eps=1e-5):
-    if norm == 2 or norm == "2":
-        return level / _norm2(signal)
-    if norm == "max":
-        return level / _norm_max(signal)
-    if norm == "2-max":
-        return torch.minimum(level / _norm2(signal, eps=eps), 1.0 / _norm_max(signal, eps=eps))
-    raise NotImplementedError(f"Norm {norm} is not implemented for batch normalization")
+def _centre_and_gain(x, level, eps, zero_mean):
+    """Per item over (channels, samples): the mean that is removed and the gain
+    level / max(std, eps), with torch's unbiased std of the centred signal."""
+    mu = x.mean(dim=(1, 2), keepdim=True) if zero_mean else torch.zeros_like(x[:, :1, :1])
+    gain = level / (x - mu).std(dim=(1, 2), keepdim=True).clamp(min=eps)
+    return mu, gain
 
 
 def normalize_batch(batch, norm=2, level_db=0.0, ref="noisy", eps=1e-5, zero_mean=True):
-    assert ref in ["noisy", "both"]
-    level = 10 ** (level_db / 20.0)
-    mix, *others = batch
-    if zero_mean:
-        mean = mix.mean(dim=(1, 2), keepdim=True)
-        mix = mix - mean
-    else:
-        mean = 0.0
-    gain = _compute_gain(mix, norm, level, eps=eps)
-    mix = mix * gain
-    out = [mix]
-    for tgt in others:
-        if tgt is not None:
-            if ref == "both":
-                if zero_mean:
-                    tgt = tgt - tgt.mean(dim=(1, 2), keepdim=True)
-                tgt = tgt * _compute_gain(tgt, norm, level, eps=eps)
-            else:
-                tgt = (tgt - mean) * gain
-        out.append(tgt)
-    return out, mean, 1.0 / gain
+    """Normalise ``batch = (mix, *targets)`` to ``level_db``.  ``ref="both"``
+    normalises every target on its own statistics, ``ref="noisy"`` applies the
+    mixture's.  Returns ``([mix, *targets], mean, 1 / gain)``."""
+    if str(norm) != "2":
+        raise NotImplementedError(f"Norm {norm} is not implemented for batch normalization")
+    if ref not in ("noisy", "both"):
+        raise ValueError(f"ref must be 'noisy' or 'both', got {ref!r}")
+    level = 10.0 ** (level_db / 20.0)
+    mix, *targets = batch
+    mu, gain = _centre_and_gain(mix, level, eps, zero_mean)
+    out = [(mix - mu) * gain]
+    for t in targets:
+        if t is not None:
+            tm, tg = _centre_and_gain(t, level, eps, zero_mean) if ref == "both" else (mu, gain)
+            t = (t - tm) * tg
+        out.append(t)
+    return out, (mu if zero_mean else 0.0), 1.0 / gain
 
 
 def denormalize_batch(x, mean, std):

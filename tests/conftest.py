@@ -12,6 +12,13 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+    # under pytest-xdist, share the cores between workers (the oracle's torch
+    # ops oversubscribe badly otherwise)
+    n = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "0") or 0)
+    if n > 1:
+        import torch
+
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // n))
 
 
 def load_golden(tag):

@@ -80,8 +80,8 @@ int main(int argc, char** argv)
         for (int t = 0; t < ou_conv_num_tiles(); ++t) {
             if (!ou_conv_tile_ok(g.kt, t)) continue;
             // 3: warp-specialised, 4: split-f16, 5: f32 in 2 K slices, 6: split-f16 in 4 K slices,
-            // 7: f16 operands
-            for (int tpw = 0; tpw < 8; ++tpw) {
+            // 7: f16 operands, 8: f16 in 2 K slices, 9: f16 in 4 K slices
+            for (int tpw = 0; tpw < 10; ++tpw) {
                 if (tpw == 3 && g.rout != 1) continue;   // warp-specialised: plain convs only
                 if (!ou_conv_tile_ok(g.kt, t | (tpw >= 6 || tpw == 4 ? 2048 : tpw == 3 ? 1024 : tpw == 5 ? 0 : tpw << 8)))
                     continue;
@@ -96,9 +96,11 @@ int main(int argc, char** argv)
                 d.res1 = g.res1 ? r1.data() : nullptr; d.r1_bstride = d.y_bstride; d.r1_cstride = out_len; d.s1 = 0.7f;
                 d.film = g.film ? fm.data() : nullptr; d.film_bstride = 2 * g.cout;
                 d.res2 = g.res2 ? r2.data() : nullptr; d.r2_bstride = d.y_bstride; d.r2_cstride = out_len; d.s2 = 0.5f;
-                d.tile = t | (tpw == 4 || tpw == 7 ? 0 : tpw == 5 ? 1 << 12 : tpw == 6 ? 2 << 12 : tpw == 3 ? 1024 : tpw << 8);
-                if (tpw == 4 || tpw == 6 || tpw == 7) {
-                    d.prec = tpw == 7 ? 2 : 1;
+                d.tile = t | (tpw == 4 || tpw == 7 ? 0 : tpw == 5 || tpw == 8 ? 1 << 12
+                                                    : tpw == 6 || tpw == 9 ? 2 << 12 : tpw == 3 ? 1024 : tpw << 8);
+                const bool f16 = tpw >= 7;
+                if (tpw == 4 || tpw == 6 || f16) {
+                    d.prec = f16 ? 2 : 1;
                     d.w = packed_s.data();
                     d.w_unscale = unscale;
                 }
@@ -117,7 +119,7 @@ int main(int argc, char** argv)
                 const double rel = std::sqrt(en / rn);
                 ++n;
                 // f16 operands: rounded to 11 bits, so neither f32-exact nor wrong
-                if (tpw == 7 ? !(rel > 1e-6 && rel < 3e-3) : !(rel < 1e-5)) {
+                if (f16 ? !(rel > 1e-6 && rel < 3e-3) : !(rel < 1e-5)) {
                     std::printf("geom %d tile %d tpw %d: rel err %.3g\n", gi, t, tpw, rel);
                     if (std::getenv("OUHIP_EMU_VERBOSE")) {
                         int shown = 0;

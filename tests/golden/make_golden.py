@@ -16,7 +16,7 @@ resampler is therefore pinned to that restatement, not to torchaudio bytes.
 Weights: ``open_universe_amd.utils.synthetic.synth_tensor`` keyed by parameter
 name (the trained HF checkpoint is unavailable offline).
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [tag ...]   (tags: CASES, gru, manifests; none = all)
 """
 import importlib.util
 import math
@@ -250,77 +250,142 @@ def tensors(d):
             for k, v in d.items()}
 
 
+# (model, n_channels, samples, tag): reduced-width variants and full width.
+# Full-width ORIG16 / PP24 at short T cover the real channel widths (48..768,
+# GRU H = 384) and, for ORIG16, the 60-step sampler of BASELINE configs[2].
+CASES = (("pp16", None, 3360, "pp16"),
+         ("pp16", 4, 4000, "pp16_c4"),
+         ("orig16", 4, 3360, "orig16_c4"),
+         ("pp24", 4, 5040, "pp24_c4"),
+         ("orig16", None, 3360, "orig16"),
+         ("pp24", None, 5040, "pp24"))
+
+# Standalone torch.nn.GRU layers, the module the reference calls
+# (score.py:84-90 one layer, condition.py:173-179 two layers), at the hidden
+# sizes and batches the configs run: (tag, hidden, layers, batch, frames).
+GRU_CASES = (("h384_b8", 384, 1, 8, 33), ("h384_b32", 384, 1, 32, 17),
+             ("h128_b32", 128, 1, 32, 21), ("h64_b8_l2", 64, 2, 8, 50))
+
+
+def make_model_case(name, nch, T, tag):
+    model = build_ref_model(name, nch)
+    names, shapes, order = manifest(model)
+    fs = model.fs
+    d = {}
+    d["manifest_names"] = np.array(names)
+    d["manifest_shapes"] = np.array([",".join(map(str, s)) for s in shapes])
+    d["param_order"] = np.array(order)
+
+    B = 2
+    mix = torch.stack([torch.from_numpy(synth_audio(T, fs, i)[0]) for i in range(B)])[:, None]
+    tgt = torch.stack([torch.from_numpy(synth_audio(T, fs, i)[1]) for i in range(B)])[:, None]
+    peak = {}
+
+    def track(mod, inp, out, nm=None):
+        o = out[0] if isinstance(out, tuple) else out
+        if torch.is_tensor(o):
+            peak[nm] = max(peak.get(nm, 0.0), float(o.abs().max()))
+
+    hooks = [m.register_forward_hook(lambda m_, i_, o_, nm=n: track(m_, i_, o_, nm))
+             for n, m in model.named_modules() if n and n.count(".") <= 3]
+    with torch.no_grad():
+        # conditioner on a padded, normalized input (what enhance feeds it)
+        xpad, _ = model.pad(mix)
+        (xn, _), *_ = model.normalize_batch((xpad, None))
+        conds, y_hat, hlat = model.condition_model(xn, x_wav=xn, train=True)
+        d["cond_in"] = xn
+        for i, c in enumerate(conds):
+            d[f"cond_out{i}"] = c
+        d["cond_yhat"] = y_hat
+        d["cond_h"] = hlat
+        # score network forward at two noise levels
+        sigma = torch.tensor([0.7, 0.02])
+        g = torch.Generator().manual_seed(5)
+        xs = torch.randn(xn.shape, generator=g) * 0.3
+        net = model.get_score_model()
+        d["score_x"] = xs
+        d["score_sigma"] = sigma
+        d["score_out"] = net(xs, sigma, conds)
+        # full enhance, default steps, seeded CPU generator
+        peak.clear()
+        rng = torch.Generator().manual_seed(1028282)
+        d["enh_mix"] = mix
+        d["enh_out"] = model.enhance(mix[:, 0], rng=rng)
+        # largest |activation| of any module during that enhance (synthetic
+        # weights drive PP24 to ~1e7: the reference diverges the same way)
+        d["enh_peak_activation"] = np.float64(max(peak.values()))
+        rng = torch.Generator().manual_seed(7)
+        d["enh2_out"] = model.enhance(mix, n_steps=3, rng=rng, keep_rms=True)
+        # sampler known-answer test: true score + noise at 20 dB
+        rng = torch.Generator().manual_seed(11)
+        d["enh_tgt"] = tgt
+        d["enh_fake_out"] = model.enhance(mix, target=tgt, fake_score_snr=20.0, rng=rng)
+        if tag in ("pp16_c4",):
+            rng = torch.Generator().manual_seed(3)
+            d["enh_ens_out"] = model.enhance(mix[0, 0], rng=rng, ensemble=3,
+                                             ensemble_stat="median")
+            rng = torch.Generator().manual_seed(3)
+            d["enh_ensmean_out"] = model.enhance(mix[0, 0], rng=rng, ensemble=3, ensemble_stat="mean")
+            # signal_median, odd and even ensembles, batch of 2
+            rng = torch.Generator().manual_seed(8)
+            d["enh_sigmed3_out"] = model.enhance(mix, rng=rng, ensemble=3, ensemble_stat="signal_median")
+            rng = torch.Generator().manual_seed(9)
+            d["enh_sigmed4_out"] = model.enhance(mix, rng=rng, ensemble=4, ensemble_stat="signal_median")
+            rng = torch.Generator().manual_seed(4)
+            d["enh_aux_out"] = model.enhance(mix, rng=rng, use_aux_signal=True)
+            rng = torch.Generator().manual_seed(6)
+            d["enh_warm_out"] = model.enhance(mix, rng=rng, warm_start=4)
+        if tag == "orig16":
+            # BASELINE configs[2]: the 60-step sampler
+            rng = torch.Generator().manual_seed(60)
+            d["enh60_out"] = model.enhance(mix[:, 0], n_steps=60, rng=rng)
+    for h in hooks:
+        h.remove()
+    print(tag, "params", sum(p.numel() for p in model.model_parameters()),
+          "score_out rms", float(d["score_out"].square().mean().sqrt()),
+          "enh rms", float(d["enh_out"].square().mean().sqrt()),
+          "peak activation", float(d["enh_peak_activation"]))
+    return tensors(d)
+
+
+def make_gru_cases():
+    from open_universe_amd.utils.synthetic import synth_tensor
+
+    d = {}
+    for tag, H, layers, B, T in GRU_CASES:
+        gru = torch.nn.GRU(2 * H, H, num_layers=layers, bidirectional=True, batch_first=True)
+        prefix = f"gru_{tag}"
+        with torch.no_grad():
+            for n, p in gru.named_parameters():
+                p.copy_(synth_tensor(f"{prefix}.{n}", p.shape))
+            x = 0.5 * torch.randn(B, 2 * H, T, generator=torch.Generator().manual_seed(H + B))
+            # the callers' layout: NCW in, (B, T, C) through the GRU, NCW out
+            y, _ = gru(x.transpose(-2, -1))
+        d[f"{tag}_x"] = x
+        d[f"{tag}_y"] = y.transpose(-2, -1)
+        d[f"{tag}_meta"] = np.array([H, layers, B, T])
+    return tensors(d)
+
+
 def main():
     torch.set_num_threads(8)
     load_reference()
-    out = {}
-
-    for name, nch, T, tag in (("pp16", None, 3360, "pp16"),
-                              ("pp16", 4, 4000, "pp16_c4"),
-                              ("orig16", 4, 3360, "orig16_c4"),
-                              ("pp24", 4, 5040, "pp24_c4")):
-        model = build_ref_model(name, nch)
-        names, shapes, order = manifest(model)
-        fs = model.fs
-        d = {}
-        d["manifest_names"] = np.array(names)
-        d["manifest_shapes"] = np.array([",".join(map(str, s)) for s in shapes])
-        d["param_order"] = np.array(order)
-
-        B = 2
-        mix = torch.stack([torch.from_numpy(synth_audio(T, fs, i)[0]) for i in range(B)])[:, None]
-        tgt = torch.stack([torch.from_numpy(synth_audio(T, fs, i)[1]) for i in range(B)])[:, None]
-        with torch.no_grad():
-            # conditioner on a padded, normalized input (what enhance feeds it)
-            xpad, _ = model.pad(mix)
-            (xn, _), *_ = model.normalize_batch((xpad, None))
-            conds, y_hat, hlat = model.condition_model(xn, x_wav=xn, train=True)
-            d["cond_in"] = xn
-            for i, c in enumerate(conds):
-                d[f"cond_out{i}"] = c
-            d["cond_yhat"] = y_hat
-            d["cond_h"] = hlat
-            # score network forward at two noise levels
-            sigma = torch.tensor([0.7, 0.02])
-            g = torch.Generator().manual_seed(5)
-            xs = torch.randn(xn.shape, generator=g) * 0.3
-            net = model.get_score_model()
-            d["score_x"] = xs
-            d["score_sigma"] = sigma
-            d["score_out"] = net(xs, sigma, conds)
-            # full enhance, default steps, seeded CPU generator
-            rng = torch.Generator().manual_seed(1028282)
-            d["enh_mix"] = mix
-            d["enh_out"] = model.enhance(mix[:, 0], rng=rng)
-            rng = torch.Generator().manual_seed(7)
-            d["enh2_out"] = model.enhance(mix, n_steps=3, rng=rng, keep_rms=True)
-            # sampler known-answer test: true score + noise at 20 dB
-            rng = torch.Generator().manual_seed(11)
-            d["enh_tgt"] = tgt
-            d["enh_fake_out"] = model.enhance(mix, target=tgt, fake_score_snr=20.0, rng=rng)
-            if tag in ("pp16_c4",):
-                rng = torch.Generator().manual_seed(3)
-                d["enh_ens_out"] = model.enhance(mix[0, 0], rng=rng, ensemble=3,
-                                                 ensemble_stat="median")
-                rng = torch.Generator().manual_seed(4)
-                d["enh_aux_out"] = model.enhance(mix, rng=rng, use_aux_signal=True)
-                rng = torch.Generator().manual_seed(6)
-                d["enh_warm_out"] = model.enhance(mix, rng=rng, warm_start=4)
-        out[tag] = tensors(d)
-        print(tag, "params", sum(p.numel() for p in model.model_parameters()),
-              "score_out rms", float(d["score_out"].square().mean().sqrt()),
-              "enh rms", float(d["enh_out"].square().mean().sqrt()))
-
-    for tag, d in out.items():
-        np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **d)
-    # PP24 full-width manifest only (too large to run cheaply)
-    for name in ("pp24", "orig16"):
-        model = build_ref_model(name)
-        names, shapes, order = manifest(model)
-        np.savez_compressed(os.path.join(HERE, f"{name}_manifest.npz"),
-                            manifest_names=np.array(names),
-                            manifest_shapes=np.array([",".join(map(str, s)) for s in shapes]),
-                            param_order=np.array(order))
+    want = set(sys.argv[1:])
+    for name, nch, T, tag in CASES:
+        if want and tag not in want:
+            continue
+        np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **make_model_case(name, nch, T, tag))
+    if not want or "gru" in want:
+        np.savez_compressed(os.path.join(HERE, "gru.npz"), **make_gru_cases())
+    # full-width manifests (state-dict names/shapes, EMA order)
+    if not want or "manifests" in want:
+        for name in ("pp24", "orig16"):
+            model = build_ref_model(name)
+            names, shapes, order = manifest(model)
+            np.savez_compressed(os.path.join(HERE, f"{name}_manifest.npz"),
+                                manifest_names=np.array(names),
+                                manifest_shapes=np.array([",".join(map(str, s)) for s in shapes]),
+                                param_order=np.array(order))
     print("written to", HERE)
 
 

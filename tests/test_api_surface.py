@@ -102,3 +102,43 @@ def test_add_enhance_arguments(tmp_path):
     assert args.n_steps == 4 and args.epsilon == 1.1 and args.keep_rms is None
     args = parser.parse_args([])
     assert args.n_steps == 8 and args.epsilon == 1.3
+
+
+_LIGHTNING_SAVER = r'''
+import sys, types, typing, torch
+# stand-ins shaped like omegaconf's pickled objects (the real package is absent)
+dc = types.ModuleType("omegaconf.dictconfig"); nodes = types.ModuleType("omegaconf.nodes")
+base = types.ModuleType("omegaconf.base")
+sys.modules["omegaconf"] = types.ModuleType("omegaconf")
+class ContainerMetadata:
+    def __init__(self): self.ref_type = typing.Any; self.object_type = dict; self.key_type = typing.Any
+class DictConfig:
+    def __init__(self, content): self._metadata = ContainerMetadata(); self._parent = None; self._content = content
+    def __getstate__(self): return {"_metadata": self._metadata, "_parent": self._parent, "_content": self._content}
+class AnyNode:
+    def __init__(self, v): self._val = v; self._metadata = ContainerMetadata()
+for cls, mod in ((DictConfig, dc), (AnyNode, nodes), (ContainerMetadata, base)):
+    cls.__module__ = mod.__name__; setattr(mod, cls.__name__, cls); sys.modules[mod.__name__] = mod
+data = torch.load(sys.argv[1], weights_only=True)
+data["hyper_parameters"] = {"fs": 16000, "score_model": DictConfig({"n_channels": AnyNode(4)})}
+data["optimizer_states"] = [{"state": {}, "param_groups": [{"lr": 1e-4}]}]
+data["callbacks"] = {"ModelCheckpoint": {"best_model_path": "x.ckpt"}}
+data["epoch"], data["global_step"], data["pytorch-lightning_version"] = 3, 1000, "2.1.0"
+torch.save(data, sys.argv[1])
+'''
+
+
+def test_load_model_lightning_checkpoint_with_pickled_hparams(tmp_path):
+    """A checkpoint as the reference's Lightning trainer writes it (ADVICE r1):
+    hyper_parameters hold pickled omegaconf objects, which the weights-only
+    loader reads as inert stand-ins; state_dict and ema still load."""
+    import subprocess
+    import sys
+
+    path, m, sd, ema = _write_ckpt(str(tmp_path), True)
+    subprocess.run([sys.executable, "-c", _LIGHTNING_SAVER, path], check=True, timeout=120)
+    with pytest.raises(Exception):
+        torch.load(path, weights_only=True)   # plain weights-only refuses it
+    model = load_model(path)
+    for p, e in zip(model.model_parameters(), ema):
+        torch.testing.assert_close(p.detach(), e)

@@ -181,8 +181,9 @@ def test_split_range_flag():
 
 @pytest.mark.parametrize("geom", GEOMS[:5], ids=[str(g) for g in GEOMS[:5]])
 def test_conv_f16_every_tile(geom):
-    """f16 operands (ConvDesc.prec = 2): every tile within f16 rounding of the
-    f32 reference (operands rounded to 11 bits, f32 accumulation)."""
+    """f16 operands (ConvDesc.prec = 2): every tile, alone and in 2 / 4 K
+    slices, within f16 rounding of the f32 reference (operands rounded to 11
+    bits, f32 accumulation)."""
     cout, cin, frame, kt, T, B, with_res = geom
     g = torch.Generator().manual_seed(hash(geom) % 1000)
     w = torch.randn(cout, cin * frame, kt, generator=g) * 0.1
@@ -195,17 +196,23 @@ def test_conv_f16_every_tile(geom):
     xa = E.Act(x.to(DEV))
     lib = L.load()
     stream = torch.cuda.current_stream().cuda_stream
+    ws = torch.empty(E.KSWS_BYTES // 4, dtype=torch.float32, device=DEV)   # K-slice partial sums
     bad, n = [], 0
     for t in range(lib.ou_conv_num_tiles()):
         if not lib.ou_conv_tile_ok(kt, t | (1 << 11)):
             continue
-        y = E.new_act(B, cout, U, DEV)
-        d = E.conv_desc(cw, xa, y, n_frames=U)
-        d.tile = t
-        assert lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream)) == 0
-        torch.cuda.synchronize()
-        err = ((y.t.cpu() - ref).norm() / ref.norm()).item()
-        n += 1
-        if not (1e-5 < err < 2e-3):   # f16-rounded, not f32-exact, and not wrong
-            bad.append((t, err))
+        for ks in (0, 1 << 12, 2 << 12):   # one workgroup per tile, 2 and 4 K slices
+            y = E.new_act(B, cout, U, DEV)
+            d = E.conv_desc(cw, xa, y, n_frames=U)
+            d.ks_ws, d.ks_ws_bytes = ws.data_ptr(), E.KSWS_BYTES
+            d.tile = t | ks
+            rc = lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
+            if rc == -2 and ks:
+                continue   # more K slices than K chunks
+            assert rc == 0
+            torch.cuda.synchronize()
+            err = ((y.t.cpu() - ref).norm() / ref.norm()).item()
+            n += 1
+            if not (1e-5 < err < 2e-3):   # f16-rounded, not f32-exact, and not wrong
+                bad.append((t, ks, err))
     assert n and not bad, bad
