@@ -310,7 +310,8 @@ __global__ void ensemble_kernel(const float* x, float* y, int E, int64_t n, int 
 // occurrence), histograms k over the samples of each batch item, and returns
 // the member whose index equals the most frequent k (argmax, first
 // occurrence).  Rank of member j: #{i : x_i < x_j} + #{i < j : x_i == x_j}
-// (the sort order of a stable sort).  Candidates: j = E/2 for even E; for odd
+// (the order of a stable sort; torch's CPU sort is stable up to 16 members,
+// unstable beyond, which only matters for exact ties).  Candidates: j = E/2 for even E; for odd
 // E the two members (E-1)/2 and (E+1)/2 tie at distance 1/2 and the one
 // sorted first wins.
 __device__ __forceinline__ int member_rank(const float* x, int64_t estride, int E, int j)

@@ -192,9 +192,10 @@ def test_graph_replay_equals_eager_and_is_deterministic(pp16_c4):
 
 
 def test_enhance_full_size_properties(pp16):
-    """BASELINE config C2 shape (8 s at 16 kHz, B = 1): no oracle at this size;
-    size-independent properties instead -- finite, bounded by the peak
-    normaliser, deterministic, and batch items independent of each other."""
+    """BASELINE config C2 shape (8 s at 16 kHz, B = 2): size-independent
+    properties -- finite, bounded by the peak normaliser, deterministic, and
+    batch items independent of each other.  (The value comparison against the
+    oracle at this size is test_gpu_parity_sizes.test_c2_size_enhance_vs_oracle.)"""
     d, cfg, m = pp16
     T = 128000
     g = torch.Generator().manual_seed(0)

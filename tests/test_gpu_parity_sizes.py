@@ -1,0 +1,223 @@
+"""GPU parity at the real sizes: full-width ORIG16 / PP24 against the
+reference's own fixtures, GRU layers at every hidden size / batch the configs
+run against torch.nn.GRU fixtures, the ensemble reductions against the
+reference, and the HIP enhance against the pinned CPU oracle at the BASELINE
+configs' shapes (C2 8 s, C3 60 steps B=8, C4 PP24 full width, C5 60 s f16)
+with the same injected noise (one seeded CPU generator, drawn in the
+reference's order on both sides).
+
+Tolerances: fp32 enhance rel-RMS <= 1e-3 and SI-SDR >= 60 dB
+against the reference / oracle; per network call rel-RMS <= 1e-4; GRU layer
+rel-RMS <= 1e-5; the fp16 config SI-SDR >= 30 dB against the fp32 oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_state_dict, load_golden, rel_rms, si_sdr
+from open_universe_amd import _lib as L
+from open_universe_amd import engine as E
+from open_universe_amd.configs import get_config
+from open_universe_amd.networks.universe import Universe, UniverseGAN
+from open_universe_amd.utils.synthetic import synth_audio, synth_state_dict, synth_tensor
+from oracle import ou_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+torch.set_num_threads(16)   # the oracle legs: the GPU box's host share
+
+
+def _t(a):
+    return torch.from_numpy(np.asarray(a))
+
+
+def _golden_model(tag, name, nch=None):
+    d = load_golden(tag)
+    cfg = get_config(name, nch)
+    cls = UniverseGAN if cfg["_target_"].endswith("UniverseGAN") else Universe
+    m = cls(**{k: v for k, v in cfg.items() if k != "_target_"})
+    m.load_state_dict(golden_state_dict(d), strict=False)
+    return d, cfg, m.to(DEV).eval()
+
+
+def _synth_model(name, seed=0):
+    cfg = get_config(name, None)
+    cls = UniverseGAN if cfg["_target_"].endswith("UniverseGAN") else Universe
+    m = cls(**{k: v for k, v in cfg.items() if k != "_target_"})
+    m.load_state_dict(synth_state_dict([(k, v.shape) for k, v in m.state_dict().items()], seed), strict=False)
+    return cfg, m.to(DEV).eval()
+
+
+def _oracle(m, cfg):
+    return O.Oracle({k: v.detach().cpu() for k, v in m.state_dict().items()}, cfg)
+
+
+def _clips(B, seconds, fs, base=0):
+    T = int(seconds * fs)
+    return torch.from_numpy(np.stack([synth_audio(T, fs, base + j)[0] for j in range(B)]))
+
+
+# ----------------------------------------------------------------- GRU layers
+@pytest.mark.parametrize("case", ["h384_b8", "h384_b32", "h128_b32", "h64_b8_l2"])
+def test_gru_layers_vs_torch_gru(case):
+    """ou_gru (with its ou_conv input projection) against torch.nn.GRU at
+    H = 384 (PP24, C4 batch 32), 128 and 64 (two layers, as the conditioner)."""
+    d = load_golden("gru")
+    H, layers, B, T = (int(v) for v in d[f"{case}_meta"])
+    p = f"gru_{case}"
+    sd = {}
+    for l in range(layers):
+        for sfx in ("", "_reverse"):
+            for kind, shape in (("weight_ih", (3 * H, 2 * H)), ("weight_hh", (3 * H, H)),
+                                ("bias_ih", (3 * H,)), ("bias_hh", (3 * H,))):
+                n = f"{p}.{kind}_l{l}{sfx}"
+                sd[n] = synth_tensor(n, shape)
+    for prec in (0, 1):   # f32 and split-f16 input projection
+        saved, E._PREP_PREC = E._PREP_PREC, prec
+        try:
+            gw = E.prep_gru(sd, p, layers, DEV)
+        finally:
+            E._PREP_PREC = saved
+        status = torch.zeros(4, dtype=torch.int32, device=DEV)
+        gran = torch.zeros(L.load().ou_gru_workspace_bytes(H, B) // 8, dtype=torch.int64, device=DEV)
+        x = E.Act(_t(d[f"{case}_x"]).to(DEV).contiguous())
+        gi = E.new_act(B, 6 * H, T, DEV)
+        prog = L.Program()
+        h = x
+        for l in range(layers):
+            y = E.new_act(B, 2 * H, T, DEV)
+            E.rec_gru(prog, gw, l, h, gi, y, gran, status)
+            h = y
+        prog.run(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert int(status.abs().sum()) == 0
+        assert rel_rms(h.t.cpu(), d[f"{case}_y"]) < 1e-5, prec
+
+
+# ----------------------------------------------------------------- ensembles
+@pytest.mark.parametrize("E_", [1, 2, 3, 4, 5, 8, 16, 17, 32])
+def test_signal_median_kernel_vs_oracle(E_):
+    """Bit-exact against the restated reference.  Batch item 1 has many exact
+    ties between members: the kernel ranks ties by member index (a stable
+    sort), which is what torch's CPU sort does for up to 16 members; beyond
+    that torch's sort is unstable, so item 1 is compared only for E <= 16."""
+    g = torch.Generator().manual_seed(E_)
+    x = torch.randn(E_, 3, 1, 5003, generator=g)
+    x[:, 1] = torch.round(x[:, 1] * 2) / 2   # many ties across members
+    from open_universe_amd.utils.stats import ensemble_reduce, signal_median
+
+    got = signal_median(x.to(DEV)).cpu()
+    want = O.signal_median(x)
+    items = [0, 1, 2] if E_ <= 16 else [0, 2]
+    assert torch.equal(got[items], want[items])
+    assert torch.allclose(ensemble_reduce(x.to(DEV), "mean").cpu(), x.mean(0), rtol=1e-6, atol=1e-7)
+    assert torch.equal(ensemble_reduce(x.to(DEV), "median").cpu(), x.median(0).values)
+
+
+def test_ensemble_mean_and_signal_median_vs_reference():
+    d, cfg, m = _golden_model("pp16_c4", "pp16", 4)
+    mix = _t(d["enh_mix"]).to(DEV)
+    with torch.no_grad():
+        mean = m.enhance(mix[0, 0], rng=torch.Generator().manual_seed(3), ensemble=3,
+                         ensemble_stat="mean").cpu()
+        assert mean.shape == d["enh_ensmean_out"].shape
+        assert rel_rms(mean, d["enh_ensmean_out"]) < 1e-3
+        for e, seed in ((3, 8), (4, 9)):
+            sm = m.enhance(mix, rng=torch.Generator().manual_seed(seed), ensemble=e,
+                           ensemble_stat="signal_median").cpu()
+            assert sm.shape == d[f"enh_sigmed{e}_out"].shape
+            assert rel_rms(sm, d[f"enh_sigmed{e}_out"]) < 1e-3
+        # the known-answer mode reduces through the same kernels (one item: the
+        # reference broadcasts target against the repeated mixture)
+        fk = m.enhance(mix[:1], target=_t(d["enh_tgt"])[:1].to(DEV), fake_score_snr=20.0,
+                       rng=torch.Generator().manual_seed(11), ensemble=3, ensemble_stat="signal_median")
+        assert fk.shape == mix[:1].shape and torch.isfinite(fk).all()
+
+
+# ------------------------------------------------------- full-width fixtures
+@pytest.mark.parametrize("tag,name", [("orig16", "orig16"), ("pp24", "pp24")])
+def test_full_width_networks_vs_reference(tag, name):
+    d, cfg, m = _golden_model(tag, name)
+    with torch.no_grad():
+        conds, y_hat, h = m.condition_model(_t(d["cond_in"]).to(DEV), train=True)
+        for i, c in enumerate(conds):
+            assert rel_rms(c.cpu(), d[f"cond_out{i}"]) < 1e-4, i
+        conds = [_t(d[f"cond_out{i}"]).to(DEV) for i in range(5)]
+        out = m.get_score_model()(_t(d["score_x"]).to(DEV), _t(d["score_sigma"]).to(DEV), conds)
+    assert rel_rms(out.cpu(), d["score_out"]) < 1e-4
+
+
+def test_full_width_orig16_enhance_8_and_60_steps():
+    """ORIG16 (BASELINE configs[2]'s model) at full width: the default sampler
+    and the 60-step sampler against the reference."""
+    d, cfg, m = _golden_model("orig16", "orig16")
+    mix = _t(d["enh_mix"]).to(DEV)
+    with torch.no_grad():
+        out = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
+        assert rel_rms(out, d["enh_out"]) < 1e-3 and si_sdr(out, d["enh_out"]) > 60
+        out60 = m.enhance(mix[:, 0], n_steps=60, rng=torch.Generator().manual_seed(60)).cpu()
+    assert rel_rms(out60, d["enh60_out"]) < 1e-3 and si_sdr(out60, d["enh60_out"]) > 60
+    assert m._get_engine().conv_prec == 1
+
+
+def test_full_width_pp24_enhance():
+    """PP24 at full width (48..768 channels, GRU H = 384).  With the seeded
+    synthetic weights the reference's activations reach ~8e6 (fixture
+    enh_peak_activation), beyond the split-f16 range: the range flag fires and
+    the model reruns the same enhance with f32 operands, which must match the
+    reference."""
+    d, cfg, m = _golden_model("pp24", "pp24")
+    assert float(d["enh_peak_activation"]) > 2.0**21
+    mix = _t(d["enh_mix"]).to(DEV)
+    with torch.no_grad():
+        out = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
+    assert m._get_engine().conv_prec == 0   # the f32 rerun happened
+    assert rel_rms(out, d["enh_out"]) < 1e-3 and si_sdr(out, d["enh_out"]) > 60
+
+
+# ------------------------------------------- BASELINE shapes vs the oracle
+def _vs_oracle(name, B, seconds, n_steps=None, seed=0, conv_prec=None):
+    cfg, m = _synth_model(name, seed)
+    if conv_prec is not None:
+        m._conv_prec = conv_prec
+    mix = _clips(B, seconds, cfg["fs"], base=11)
+    kw = {"n_steps": n_steps} if n_steps else {}
+    with torch.no_grad():
+        out = m.enhance(mix.to(DEV), rng=torch.Generator().manual_seed(20250614), **kw).cpu()
+        ref = _oracle(m, cfg).enhance(mix, rng=torch.Generator().manual_seed(20250614), **kw)
+    return m, out, ref
+
+
+def test_c2_size_enhance_vs_oracle():
+    """BASELINE configs[1]: PP16, one 8 s clip, 8 steps, default (split-f16)
+    operands, against the fp32 oracle on the same noise."""
+    m, out, ref = _vs_oracle("pp16", 1, 8.0)
+    assert m._get_engine().conv_prec == 1
+    assert out.shape == ref.shape == (1, 128000)
+    assert rel_rms(out, ref) < 1e-3 and si_sdr(out, ref) > 60
+
+
+def test_c3_shape_enhance_vs_oracle():
+    """BASELINE configs[2]: ORIG16 full width, batch 8, 60 steps (0.25 s clips
+    so the oracle finishes in seconds)."""
+    m, out, ref = _vs_oracle("orig16", 8, 0.25, n_steps=60)
+    assert out.shape == ref.shape == (8, 4000)
+    assert rel_rms(out, ref) < 1e-3 and si_sdr(out, ref) > 60
+
+
+def test_c4_shape_enhance_vs_oracle():
+    """BASELINE configs[3]: PP24 full width (GRU H = 384), batch 4, 0.5 s
+    clips, f32 operands (the synthetic weights leave the split range)."""
+    m, out, ref = _vs_oracle("pp24", 4, 0.5)
+    assert out.shape == ref.shape == (4, 12000)
+    assert rel_rms(out, ref) < 1e-3 and si_sdr(out, ref) > 60
+
+
+def test_c5_size_f16_enhance_vs_oracle():
+    """BASELINE configs[4]: PP16, one 60 s clip, f16 conv operands, against the
+    fp32 oracle: SI-SDR >= 30 dB, and the f16 path itself produced it."""
+    m, out, ref = _vs_oracle("pp16", 1, 60.0, conv_prec=2)
+    eng = m._get_engine()
+    assert eng.conv_prec == 2 and int(eng.status.abs().sum()) == 0
+    assert out.shape == ref.shape == (1, 960000)
+    assert torch.isfinite(out).all() and si_sdr(out, ref) > 30
