@@ -176,13 +176,17 @@ def profile_roofline(plan, stream, dump=None):
             json.dump(rows, fh)
     kinds = plan.prog.op_kinds()
     flops = plan.prog.flops
-    conv_ms = sum(t for t, k in zip(ms, kinds) if k == L.OP_CONV)
-    conv_fl = sum(f for f, k in zip(flops, kinds) if k == L.OP_CONV)
-    conv_by = sum(b for b, k in zip(plan.prog.bytes, kinds) if k == L.OP_CONV)
-    n_conv = sum(1 for k in kinds if k == L.OP_CONV)
+    # the conv stack: ou_conv launches and fused ConvBlock (ou_block) launches
+    cv = (L.OP_CONV, L.OP_BLOCK)
+    conv_ms = sum(t for t, k in zip(ms, kinds) if k in cv)
+    conv_fl = sum(f for f, k in zip(flops, kinds) if k in cv)
+    conv_by = sum(b for b, k in zip(plan.prog.bytes, kinds) if k in cv)
+    n_conv = sum(1 for k in kinds if k in cv)
+    n_block = sum(1 for k in kinds if k == L.OP_BLOCK)
     gru_ms = sum(t for t, k in zip(ms, kinds) if k == L.OP_GRU)
     return {
-        "conv_ms": conv_ms, "conv_flops": conv_fl, "conv_bytes": conv_by, "n_conv": n_conv, "gru_ms": gru_ms,
+        "conv_ms": conv_ms, "conv_flops": conv_fl, "conv_bytes": conv_by, "n_conv": n_conv, "n_block": n_block,
+        "gru_ms": gru_ms,
         "total_ms": sum(ms), "total_flops": sum(flops), "n_ops": len(ms),
     }
 
@@ -403,14 +407,13 @@ def main():
             if args.traffic_json and os.path.exists(args.traffic_json):
                 with open(args.traffic_json) as fh:
                     pmc = json.load(fh)
-                row = pmc.get("kernels", {}).get("conv_kernel")
-                if row and pmc.get("config", "c2") == args.config:
-                    traffic = row["traffic_bytes_per_launch"]
-                    per = "kernel dispatch"
-                    if pmc.get("enhances_profiled"):
-                        # per recorded conv op (K-slice ops dispatch twice)
-                        traffic = round(traffic * row["dispatches"] / pmc["enhances_profiled"] / prof["n_conv"])
-                        per = "ou_conv op (both launches of K-slice ops)"
+                rows = [r for k, r in pmc.get("kernels", {}).items() if k in ("conv_kernel", "block_kernel")]
+                if rows and pmc.get("config", "c2") == args.config and pmc.get("enhances_profiled"):
+                    # bytes of every conv-stack dispatch of one enhance, per
+                    # recorded conv op (K-slice ops dispatch twice)
+                    tot = sum(r["traffic_bytes_per_launch"] * r["dispatches"] for r in rows)
+                    traffic = round(tot / pmc["enhances_profiled"] / prof["n_conv"])
+                    per = "conv-stack op (ou_conv incl. both launches of K-slice ops, ou_block)"
                     tsrc = (f"{os.path.relpath(args.traffic_json, HERE)} ({pmc.get('tag', '')}): "
                             f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes per {per}")
             if t_hbm > t_mfma:
@@ -426,8 +429,10 @@ def main():
             out["roofline"] = {
                 **rl, "traffic": traffic,
                 "traffic_source": tsrc,
-                "kernel": "ou_conv (conv_kernel, all launches of one enhance)",
+                "kernel": "conv stack: ou_conv (conv_kernel) + fused ConvBlock ou_block (block_kernel), "
+                          "all launches of one enhance",
                 "launches": prof["n_conv"],
+                "fused_block_launches": prof["n_block"],
                 "avg_launch_ms": round(prof["conv_ms"] / prof["n_conv"], 5),
                 "flops_per_launch": round(prof["conv_flops"] / prof["n_conv"]),
                 "algorithmic_bytes_per_launch": round(prof["conv_bytes"] / prof["n_conv"]),

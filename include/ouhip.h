@@ -296,6 +296,54 @@ typedef struct ou_snake_desc {
 int ou_snake_aa(const ou_snake_desc* d, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Fused ConvBlock main path (ou_block.hip): the three PReLU_Conv calls of a
+ * ConvBlock and the arithmetic between them in one launch, for channel
+ * counts whose whole channel range fits one workgroup (32, 64, 128, 256) and
+ * split-f16 / f16 operands.  Replaces blocks.py:393-416:
+ *   c1 = conv1(h) (k5);  c1 = (c1 + sc) * s_sc;  c1 = film(c1);  cond_out = c1
+ *   y  = ((h + conv3(conv2(c1))) * s_res + res2) * s2        (k3, k3)
+ * Each conv applies its scalar PReLU slope to its input; frames outside
+ * [0, length) are zero padding.  sc / film / cond_out / res2 are optional
+ * (NULL).  y must not alias h, sc, cond_out or res2.
+ * ---------------------------------------------------------------------- */
+typedef struct ou_block_desc {
+    const float* h;            /* block input [B][C][T]                          */
+    int64_t h_bstride, h_cstride;
+    int32_t channels, length;  /* C, T                                           */
+    int32_t batch, prec;       /* prec 1 split-f16, 2 f16                        */
+    const void* w[3];          /* conv1 (k5), conv2, conv3 (k3): ou_block_pack   */
+    const float* bias[3];      /* [C] or NULL                                    */
+    float slope[3];            /* PReLU slope on each conv's input               */
+    float w_unscale[3];        /* from ou_block_pack                             */
+    const float* sc;           /* conv1 residual (input_cond) or NULL            */
+    int64_t sc_bstride, sc_cstride;
+    float s_sc;
+    int32_t dbg;               /* diagnostics only (tools/block_bench.py): 0     */
+    const float* film;         /* [B][2C] (gamma | beta) or NULL                 */
+    int64_t film_bstride;
+    float* cond_out;           /* conv1 result after sc / FiLM, or NULL          */
+    int64_t co_bstride, co_cstride;
+    float* y;
+    int64_t y_bstride, y_cstride;
+    float s_res, s2;
+    const float* res2;         /* or NULL                                        */
+    int64_t r2_bstride, r2_cstride;
+    int32_t* status;           /* split-f16 range flag (as ou_conv), or NULL     */
+} ou_block_desc;
+
+/* 1 when ou_block handles this channel count and operand precision. */
+int ou_block_supported(int channels, int prec);
+/* Output frames per workgroup (the grid is ceil(length / frames) x batch). */
+int ou_block_frames(int channels);
+/* Halves of one packed conv (C x C x kt, hi and lo planes). */
+int64_t ou_block_packed_halves(int channels, int kt);
+/* Pack w[C][C][kt] (f32, host) as [m-tile][tap][16-channel step][hi | lo]
+ * [lane][8 halves] of a = w * 2^e (max|a| in [2^9, 2^10)); *w_unscale =
+ * 2^(6 - e). */
+int ou_block_pack(const float* w, int channels, int kt, void* out, float* w_unscale);
+int ou_block(const ou_block_desc* d, void* stream);
+
+/* ------------------------------------------------------------------------
  * Program: a recorded list of the launches above, replayed natively (and
  * optionally as one hipGraph).  Built once per (shape, options) by the
  * Python host; replaces the Python-level loop of Universe.enhance.
@@ -306,7 +354,14 @@ enum {
     OU_OP_CONV = 1, OU_OP_GRU = 2, OU_OP_EMBED = 3, OU_OP_HEAD = 4,
     OU_OP_NORMALIZE = 5, OU_OP_INV_RMS = 6, OU_OP_POWER = 7, OU_OP_PAD = 8,
     OU_OP_SCALE = 9, OU_OP_FINISH = 10, OU_OP_RMS = 11, OU_OP_SNAKE = 12,
-    OU_OP_MEMSET = 13, OU_OP_ENSEMBLE = 14
+    OU_OP_MEMSET = 13, OU_OP_ENSEMBLE = 14, OU_OP_BLOCK = 15,
+    /* lanes: ops after OU_OP_LANE{id} run on stream `id` (0 = the caller's /
+     * capture stream, id > 0 = program-owned side streams); OU_OP_SIGNAL{id}
+     * records event id on the current lane, OU_OP_WAIT{id} makes the current
+     * lane wait for it.  A side lane must start with a WAIT and lane 0 must end
+     * after waiting for every side lane's last SIGNAL (checked: run and
+     * capture fail otherwise).  ou_program_profile runs the list serially. */
+    OU_OP_LANE = 16, OU_OP_SIGNAL = 17, OU_OP_WAIT = 18
 };
 
 /* Descriptors of the helper ops when recorded into a program. */
@@ -353,6 +408,10 @@ typedef struct ou_finish_args {
     float* y;
     const float* mix_rms;
 } ou_finish_args;
+typedef struct ou_sync_args {
+    int32_t id;                /* lane (OU_OP_LANE) or event (SIGNAL / WAIT), 0..63 */
+    int32_t _pad;
+} ou_sync_args;
 typedef struct ou_ensemble_args {
     const float* x;
     float* y;

@@ -20,7 +20,8 @@ fp = c_void_p  # device pointers are passed as integers
 OP_CONV, OP_GRU, OP_EMBED, OP_HEAD = 1, 2, 3, 4
 OP_NORMALIZE, OP_INV_RMS, OP_POWER, OP_PAD = 5, 6, 7, 8
 OP_SCALE, OP_FINISH, OP_RMS, OP_SNAKE = 9, 10, 11, 12
-OP_MEMSET, OP_ENSEMBLE = 13, 14
+OP_MEMSET, OP_ENSEMBLE, OP_BLOCK = 13, 14, 15
+OP_LANE, OP_SIGNAL, OP_WAIT = 16, 17, 18   # program lanes (side streams) and their events
 
 
 class ConvDesc(ctypes.Structure):
@@ -81,6 +82,10 @@ class SnakeDesc(ctypes.Structure):
     ]
 
 
+class SyncArgs(ctypes.Structure):
+    _fields_ = [("id", c_int32), ("_pad", c_int32)]
+
+
 class MemsetArgs(ctypes.Structure):
     _fields_ = [("ptr", fp), ("bytes", c_int64)]
 
@@ -120,11 +125,26 @@ class EnsembleArgs(ctypes.Structure):
                 ("batch", c_int32), ("_pad", c_int32), ("counts", c_void_p)]
 
 
+class BlockDesc(ctypes.Structure):
+    _fields_ = [
+        ("h", fp), ("h_bstride", c_int64), ("h_cstride", c_int64),
+        ("channels", c_int32), ("length", c_int32), ("batch", c_int32), ("prec", c_int32),
+        ("w", fp * 3), ("bias", fp * 3), ("slope", c_float * 3), ("w_unscale", c_float * 3),
+        ("sc", fp), ("sc_bstride", c_int64), ("sc_cstride", c_int64), ("s_sc", c_float), ("dbg", c_int32),
+        ("film", fp), ("film_bstride", c_int64),
+        ("cond_out", fp), ("co_bstride", c_int64), ("co_cstride", c_int64),
+        ("y", fp), ("y_bstride", c_int64), ("y_cstride", c_int64), ("s_res", c_float), ("s2", c_float),
+        ("res2", fp), ("r2_bstride", c_int64), ("r2_cstride", c_int64),
+        ("status", fp),
+    ]
+
+
 OP_STRUCT = {
     OP_CONV: ConvDesc, OP_GRU: GruDesc, OP_EMBED: EmbedDesc, OP_HEAD: HeadDesc,
     OP_NORMALIZE: NormArgs, OP_INV_RMS: RmsArgs, OP_RMS: RmsArgs, OP_POWER: PowerArgs,
     OP_PAD: PadArgs, OP_SCALE: ScaleArgs, OP_FINISH: FinishArgs, OP_SNAKE: SnakeDesc,
-    OP_MEMSET: MemsetArgs, OP_ENSEMBLE: EnsembleArgs,
+    OP_MEMSET: MemsetArgs, OP_ENSEMBLE: EnsembleArgs, OP_BLOCK: BlockDesc,
+    OP_LANE: SyncArgs, OP_SIGNAL: SyncArgs, OP_WAIT: SyncArgs,
 }
 
 # every symbol include/ouhip.h declares (checked by tests/test_abi.py)
@@ -155,6 +175,11 @@ EXPORTS = {
     "ou_ensemble_reduce": (c_int, [fp, fp, c_int, c_int64, c_int, c_void_p]),
     "ou_signal_median": (c_int, [fp, fp, c_int, c_int, c_int64, c_void_p, c_void_p]),
     "ou_snake_aa": (c_int, [POINTER(SnakeDesc), c_void_p]),
+    "ou_block_supported": (c_int, [c_int, c_int]),
+    "ou_block_frames": (c_int, [c_int]),
+    "ou_block_packed_halves": (c_int64, [c_int, c_int]),
+    "ou_block_pack": (c_int, [POINTER(c_float), c_int, c_int, c_void_p, POINTER(c_float)]),
+    "ou_block": (c_int, [POINTER(BlockDesc), c_void_p]),
     "ou_resample": (c_int, [fp, c_int64, fp, c_int64, c_int, c_int, c_int, fp, c_int, c_int, c_int, c_int,
                             c_void_p]),
     "ou_program_create": (c_void_p, []),
@@ -238,6 +263,21 @@ def conv_pack_split(w_logical):
     return out, float(un.value)
 
 
+def block_pack(w_logical):
+    """Fused-block packing of one C x C x kt conv: returns (packed f16 as an
+    int16 numpy array, w_unscale)."""
+    import numpy as np
+
+    w = np.ascontiguousarray(w_logical, dtype=np.float32)
+    c, c2, kt = w.shape
+    assert c == c2, w.shape
+    out = np.empty(load().ou_block_packed_halves(c, kt), dtype=np.int16)
+    un = c_float(0.0)
+    check(load().ou_block_pack(w.ctypes.data_as(POINTER(c_float)), c, kt, out.ctypes.data, ctypes.byref(un)),
+          "block_pack")
+    return out, float(un.value)
+
+
 # Optional per-layer tile autotuner for ou_conv (set by the engine on a GPU):
 # called with a ConvDesc whose tile is -1, returns the tile id to record.
 TUNER = None
@@ -250,6 +290,7 @@ class Program:
         self.lib = load()
         self.h = self.lib.ou_program_create()
         self.keep = []          # tensors whose memory the program references
+        self.cur_lane = 0
         self.captured = False
         self.flops = []         # algorithmic FLOPs of the reference ops each op replaces
         self.bytes = []         # algorithmic HBM bytes of each op (0 where not counted)
@@ -271,6 +312,24 @@ class Program:
             self.info.append({"H": desc.hidden, "T": desc.steps, "b": desc.batch})
         else:
             self.info.append({})
+
+    # ---- lanes: concurrent branches of the recorded program (side streams
+    # in eager replay, parallel branches of the captured hipGraph)
+    def lane(self, i):
+        self.add(OP_LANE, SyncArgs(id=i))
+        self.cur_lane = i
+
+    def new_event(self):
+        self.n_events = getattr(self, "n_events", 0) + 1
+        return self.n_events - 1
+
+    def signal(self, ev=None):
+        ev = self.new_event() if ev is None else ev
+        self.add(OP_SIGNAL, SyncArgs(id=ev))
+        return ev
+
+    def wait(self, ev):
+        self.add(OP_WAIT, SyncArgs(id=ev))
 
     def __len__(self):
         return self.lib.ou_program_size(self.h)
@@ -308,5 +367,5 @@ def run_now(op, desc, stream):
     """Launch one op immediately (used by layer-level tests)."""
     lib = load()
     fns = {OP_CONV: lib.ou_conv, OP_GRU: lib.ou_gru, OP_EMBED: lib.ou_embed,
-           OP_HEAD: lib.ou_head, OP_SNAKE: lib.ou_snake_aa}
+           OP_HEAD: lib.ou_head, OP_SNAKE: lib.ou_snake_aa, OP_BLOCK: lib.ou_block}
     check(fns[op](ctypes.byref(desc), c_void_p(stream)), f"op {op}")

@@ -17,7 +17,7 @@ cc() {   # cc <src> <obj> [extra flags...]
   /opt/rocm/bin/hipcc "${CFLAGS[@]}" ${OUHIP_CFLAGS:-} "$@" -c "$HERE/$src" -o "$OBJDIR/$obj" &
   pids+=($!)
 }
-for s in ou_gru.hip ou_misc.hip ou_program.hip ou_audio.hip; do
+for s in ou_gru.hip ou_misc.hip ou_program.hip ou_audio.hip ou_block.hip; do
   cc "$s" "${s%.hip}.o"
 done
 if [[ "${OUHIP_CFLAGS:-}" == *OU_CONV_STAMPS* ]]; then

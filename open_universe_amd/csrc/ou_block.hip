@@ -1,0 +1,526 @@
+// ou_block.hip -- fused ConvBlock main path for channel-complete workgroups
+// (gfx950 / MI355X).
+//
+// Replaces the three PReLU_Conv calls of one ConvBlock and the arithmetic
+// between them (networks/universe/blocks.py:393-416):
+//   c1 = conv1(h)                            k5, PReLU on its input
+//   c1 = (c1 + input_cond) * s_sc            (score decoder, optional)
+//   c1 = film(c1)                            (gamma * c1 + beta, optional)
+//   cond_out = c1                            (conditioner decoder, optional store)
+//   c2 = conv2(c1)                           k3
+//   c3 = conv3(c2)                           k3
+//   y  = ((h + c3) * s_res [+ res2]) * s2
+// in ONE launch instead of three.  A workgroup owns F = 32*NT - 4 output
+// frames of every channel: it stages PReLU(h) over its frames plus a 4-frame
+// halo on each side (2 + 1 + 1 taps of the three convs) in LDS, computes
+// conv1 over F + 4 frames, conv2 over F + 2 and conv3 over F, each into LDS,
+// and writes only y (and cond_out) to HBM.  The intermediates never leave
+// the CU: per block the HBM traffic drops from 3 reads + 3 writes (+ the
+// residual re-read) of a C x T tensor to 1 read + 1 write, and 3 kernel
+// latencies become 1.  Halo frames are recomputed by the neighbouring
+// workgroup (F = 124 / 60 / 28 frames at C = 32 / 64 / 128).
+//
+// Arithmetic is the split-f16 form of ou_conv (P = 1): every operand is
+// v = hi + lo * 2^-11 (f16 halves; weights packed by ou_block_pack with a
+// per-conv power-of-two scale, activations split while they are written to
+// LDS, staged as x * 2^-6) and a product is ha hb + (ha lb + la hb) 2^-11 on
+// v_mfma_f32_32x32x16_f16 with f32 accumulation -- f32-class accuracy.  P = 2
+// is plain f16 (hi halves only).  A staged |x| >= 2^21 sets *status (the
+// host reruns the enhance with f32 operands), exactly as ou_conv does.
+//
+// Frames outside [0, T) are the zero padding of each conv's input ('same'
+// convs pad their PReLU'd input with zeros), so the conv1/conv2 results are
+// zeroed there before they become the next conv's input.
+//
+// MFMA mapping: 4 waves as WM x WN; wave (wm, wn) owns MR x NR 32 x 32 output
+// tiles (rows = channels, columns = frames).  A fragments (weights) stream
+// from global memory (L2-resident: every workgroup reads the same weights)
+// through a 3-deep register ring; B fragments are one ds_read_b128 of 8
+// consecutive channels of one frame row.  LDS rows are [frame][channel] with
+// a stride of C + 8 halves (an odd number of 16-B slots: conflict-free).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "../../include/ouhip.h"
+#include "ou_common.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+
+namespace {
+
+constexpr int kStageShift = 6;   // activations are staged as x * 2^-6 (ou_conv's kSplitShift)
+#ifndef OU_BLOCK_NT32
+#define OU_BLOCK_NT32 4
+#endif
+#ifndef OU_BLOCK_NT64
+#define OU_BLOCK_NT64 2
+#endif
+#ifndef OU_BLOCK_NT128
+#define OU_BLOCK_NT128 1
+#endif
+
+template <int C, int NT, int P>
+struct BCfg {
+    static constexpr int MT = C / 32;              // 32-row M tiles (output channels)
+    static constexpr int WM = MT >= 4 ? 4 : MT;    // waves along M
+    static constexpr int WN = 4 / WM;              // waves along N (frames)
+    static constexpr int MR = MT / WM;             // M tiles per wave
+    static constexpr int NR = NT / WN;             // N tiles per wave
+    static constexpr int NF = 32 * NT;             // frames of one conv stage
+    static constexpr int F = NF - 4;               // output frames per workgroup
+    static constexpr int SX = C + 8;               // LDS row stride in halves
+    static constexpr int R1 = NF + 4;              // conv1 input rows (frames t0-4 ..)
+    static constexpr int R2 = NF + 2;              // conv2 / conv3 input rows
+    static constexpr int NPL = P == 1 ? 2 : 1;     // planes: hi (+ lo)
+    static constexpr int PA = R1 * SX;             // plane stride of region A (halves)
+    static constexpr int PB = R2 * SX;             // plane stride of region B
+    static constexpr int A_OFF = 0;                // region A: conv1 input, then conv3 input
+    static constexpr int B_OFF = NPL * PA;         // region B: conv2 input
+    static constexpr int LDS_BYTES = 2 * (NPL * PA + NPL * PB);
+    static constexpr int KS = C / 16;              // 16-channel k-steps per tap
+    static constexpr int RING = MR == 1 ? 6 : 4;   // weight-fragment ring depth (k-steps)
+    static_assert(C % 32 == 0 && WM * WN == 4 && MT % WM == 0 && NT % WN == 0, "block tiling");
+    static_assert((SX / 8) % 2 == 1, "LDS row stride must be an odd number of 16-B slots");
+};
+
+__device__ __forceinline__ float prelu(float v, float a) { return v >= 0.f ? v : a * v; }
+
+// One conv stage: acc[mr][nr] (+ accx for the split cross terms) over KT taps
+// x C channels.  xin: LDS base of the stage's input (hi plane; lo plane at
+// + pstride); wp: packed weights [mt][tap][ks][plane][lane][8].
+template <int KT, int C, int NT, int P>
+__device__ __forceinline__ void stage_mma(const half8_t* __restrict__ wp, const _Float16* xin, int pstride, int wm,
+                                          int wn, int lane, int dbg, floatx16 (&acc)[BCfg<C, NT, P>::MR][BCfg<C, NT, P>::NR],
+                                          floatx16 (&accx)[BCfg<C, NT, P>::MR][BCfg<C, NT, P>::NR])
+{
+    using K = BCfg<C, NT, P>;
+    constexpr int MR = K::MR, NR = K::NR, KS = K::KS, NS = KT * KS;
+    const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[mr][nr][r] = 0.f, accx[mr][nr][r] = 0.f;
+        }
+    // weight fragments stream from L2 through a D-deep register ring: the
+    // loads of step s + D - 1 are issued before the MFMAs of step s
+    if (dbg & 2) return;   // diagnostics (tools/block_bench.py --dbg): no MFMA stage
+    constexpr int D = NS < K::RING ? NS : K::RING;
+    half8_t ra[D][MR][2];
+    auto load_a = [&](int s, half8_t (&dst)[MR][2]) {
+        const int k = s / KS, ks = s - (s / KS) * KS;
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr) {
+            const half8_t* p = wp + ((((int64_t)(wm * MR + mr) * KT + k) * KS + ks) * 2) * 64 + lane;
+            dst[mr][0] = p[0];
+            if constexpr (P == 1) dst[mr][1] = p[64];
+        }
+    };
+#pragma unroll
+    for (int s = 0; s < D - 1; ++s) load_a(s, ra[s]);
+    const _Float16* xb = xin + (wn * NR * 32 + l32) * K::SX + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        if (s + D - 1 < NS) load_a(s + D - 1, ra[(s + D - 1) % D]);
+        const int k = s / KS, ks = s - (s / KS) * KS;
+        half8_t b[NR], bl[NR];
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+            const _Float16* q = xb + (nr * 32 + k) * K::SX + 16 * ks;
+            b[nr] = *(const half8_t*)q;
+            if constexpr (P == 1) bl[nr] = *(const half8_t*)(q + pstride);
+        }
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+            for (int nr = 0; nr < NR; ++nr) {
+                acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][mr][0], b[nr], acc[mr][nr], 0, 0, 0);
+                if constexpr (P == 1) {
+                    accx[mr][nr] =
+                        __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][mr][0], bl[nr], accx[mr][nr], 0, 0, 0);
+                    accx[mr][nr] =
+                        __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][mr][1], b[nr], accx[mr][nr], 0, 0, 0);
+                }
+            }
+    }
+}
+
+// Epilogue variants (template EPI bits, so the per-element code has no
+// run-time branches): the score encoder's FiLM, the score decoder's
+// input_cond residual + FiLM, the conditioner decoder's cond_out store.
+constexpr int kEpiFilm = 1, kEpiSc = 2, kEpiCond = 4, kEpiRes2 = 8;
+
+typedef float float2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+
+// x (already scaled by 2^-6) -> hi (+ lo) halves of 4 consecutive channels;
+// ovf |= any |x| >= 2^15
+template <int P>
+__device__ __forceinline__ void split4(float x0, float x1, float x2, float x3, half4_t& hi, half4_t& lo, bool& ovf)
+{
+    const float2_t a = {x0, x1}, b = {x2, x3};
+    const half2_t ha = __builtin_convertvector(a, half2_t), hb = __builtin_convertvector(b, half2_t);
+    hi = half4_t{ha[0], ha[1], hb[0], hb[1]};
+    if constexpr (P == 1) {
+        const half2_t la = __builtin_convertvector((a - __builtin_convertvector(ha, float2_t)) * 2048.f, half2_t);
+        const half2_t lb = __builtin_convertvector((b - __builtin_convertvector(hb, float2_t)) * 2048.f, half2_t);
+        lo = half4_t{la[0], la[1], lb[0], lb[1]};
+    }
+    const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(x0), __builtin_fabsf(x1)),
+                                    __builtin_fmaxf(__builtin_fabsf(x2), __builtin_fabsf(x3)));
+    ovf |= !(m < 32768.f);
+}
+
+template <int C, int NT, int P, int EPI>
+__global__ __launch_bounds__(256, 2) void block_kernel(ou_block_desc d)
+{
+    using K = BCfg<C, NT, P>;
+    constexpr int MR = K::MR, NR = K::NR, F = K::F, NF = K::NF, SX = K::SX;
+    constexpr float kIn = 1.f / (1 << kStageShift);
+    OU_DYNAMIC_LDS(half8_t, lds8);
+    _Float16* lds = (_Float16*)lds8;
+    _Float16* xa = lds + K::A_OFF;
+    _Float16* xbuf = lds + K::B_OFF;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave % K::WM, wn = wave / K::WM;
+    const int l32 = lane & 31, h = lane >> 5;
+    const int b = blockIdx.y;
+    const int T = d.length;
+    const int t0 = blockIdx.x * F;
+    const float* __restrict__ hb = d.h + (int64_t)b * d.h_bstride;
+    bool ovf = false;
+
+    // ---- stage 0: PReLU1(h) * 2^-6 over frames [t0 - 4, t0 + NF + 4) -> region A.
+    // A work item is (8-channel group, frame): 8 coalesced loads (consecutive
+    // lanes = consecutive frames), then one 16-B LDS write per plane.  All
+    // loads of a thread are issued before any arithmetic.
+    {
+        constexpr int NI = (C / 8) * K::R1;
+        constexpr int NIT = (NI + 255) / 256;
+        const float a1 = d.slope[0];
+        float v[NIT][8];
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            // out-of-range items / frames load a clamped (valid) address and
+            // are zeroed afterwards: no branches around the loads
+            const int item = min(tid + 256 * it, NI - 1);
+            const int g = item / K::R1, r = item - g * K::R1;
+            const int t = t0 - 4 + r;
+            const int tc = min(max(t, 0), T - 1);
+            const float* src = hb + (int64_t)(8 * g) * d.h_cstride + tc;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = src[(int64_t)i * d.h_cstride];
+            if (t != tc || (d.dbg & 1)) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[it][i] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int item = tid + 256 * it;
+            if (NIT * 256 > NI && item >= NI) break;
+            const int g = item / K::R1, r = item - g * K::R1;
+            float x[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = (v[it][i] >= 0.f ? kIn : a1 * kIn) * v[it][i];
+            half4_t h0, h1, l0, l1;
+            split4<P>(x[0], x[1], x[2], x[3], h0, l0, ovf);
+            split4<P>(x[4], x[5], x[6], x[7], h1, l1, ovf);
+            _Float16* dst = xa + r * SX + 8 * g;
+            *(half8_t*)dst = half8_t{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+            if constexpr (P == 1)
+                *(half8_t*)(dst + K::PA) = half8_t{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+        }
+    }
+    __syncthreads();
+
+    floatx16 acc[MR][NR], accx[MR][NR];
+    // per-row constants of this wave's output rows: m = row(mr, r)
+    auto row = [&](int mr, int r) { return (wm * MR + mr) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };
+
+    // ---- stage 1: conv1 (k5) over frames t0 - 2 + u, u in [0, NF) -> region B
+    stage_mma<5, C, NT, P>((const half8_t*)d.w[0], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
+    {
+        const float a2 = d.slope[1];
+        // operands of the epilogue, loaded before anything is stored
+        float bia[MR][16], gam[MR][16], bet[MR][16], scv[MR][NR][16];
+        const float* film = d.film + (int64_t)b * d.film_bstride;
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = row(mr, r);
+                bia[mr][r] = d.bias[0] ? d.bias[0][m] : 0.f;
+                if constexpr (EPI & kEpiFilm) {
+                    gam[mr][r] = film[m];
+                    bet[mr][r] = film[C + m];
+                }
+                if constexpr (EPI & kEpiSc) {
+#pragma unroll
+                    for (int nr = 0; nr < NR; ++nr) {   // frames outside [0, T) are zeroed below
+                        const int t = min(max(t0 - 2 + (wn * NR + nr) * 32 + l32, 0), T - 1);
+                        scv[mr][nr][r] = d.sc[(int64_t)b * d.sc_bstride + (int64_t)m * d.sc_cstride + t];
+                    }
+                }
+            }
+        const float un = d.w_unscale[0];
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+            for (int nr = 0; nr < NR; ++nr) {
+                const int u = (wn * NR + nr) * 32 + l32;
+                const int t = t0 - 2 + u;
+                const bool inside = t >= 0 && t < T;
+                float o[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float v = __builtin_fmaf(__builtin_fmaf(accx[mr][nr][r], 1.f / 2048.f, acc[mr][nr][r]), un,
+                                             bia[mr][r]);
+                    if constexpr (EPI & kEpiSc) v = (v + scv[mr][nr][r]) * d.s_sc;
+                    if constexpr (EPI & kEpiFilm) v = __builtin_fmaf(gam[mr][r], v, bet[mr][r]);
+                    o[r] = inside ? v : 0.f;
+                }
+                if constexpr (EPI & kEpiCond) {
+                    if (inside && t >= t0 && t < t0 + F) {
+                        float* co = d.cond_out + (int64_t)b * d.co_bstride + t;
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) co[(int64_t)row(mr, r) * d.co_cstride] = o[r];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float x[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float q = o[4 * j + i];
+                        x[i] = (q >= 0.f ? kIn : a2 * kIn) * q;
+                    }
+                    half4_t hi, lo;
+                    split4<P>(x[0], x[1], x[2], x[3], hi, lo, ovf);
+                    _Float16* dst = xbuf + u * SX + (wm * MR + mr) * 32 + 8 * j + 4 * h;
+                    *(half4_t*)dst = hi;
+                    if constexpr (P == 1) *(half4_t*)(dst + K::PB) = lo;
+                }
+            }
+        // rows NF, NF + 1 feed only discarded conv2 columns: keep them zero
+        for (int e = tid; e < 2 * (C / 8); e += 256) {
+            _Float16* dst = xbuf + (NF + e / (C / 8)) * SX + 8 * (e % (C / 8));
+            *(half8_t*)dst = half8_t{};
+            if constexpr (P == 1) *(half8_t*)(dst + K::PB) = half8_t{};
+        }
+    }
+    __syncthreads();
+
+    // ---- stage 2: conv2 (k3) over frames t0 - 1 + v -> region A
+    stage_mma<3, C, NT, P>((const half8_t*)d.w[1], xbuf, K::PB, wm, wn, lane, d.dbg, acc, accx);
+    {
+        const float a3 = d.slope[2], un = d.w_unscale[1];
+        float bia[MR][16];
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bia[mr][r] = d.bias[1] ? d.bias[1][row(mr, r)] : 0.f;
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+            for (int nr = 0; nr < NR; ++nr) {
+                const int v_ = (wn * NR + nr) * 32 + l32;
+                const int t = t0 - 1 + v_;
+                const float keep = (t >= 0 && t < T) ? kIn : 0.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float x[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = 4 * j + i;
+                        const float q = __builtin_fmaf(__builtin_fmaf(accx[mr][nr][r], 1.f / 2048.f, acc[mr][nr][r]),
+                                                       un, bia[mr][r]);
+                        x[i] = (q >= 0.f ? keep : a3 * keep) * q;
+                    }
+                    half4_t hi, lo;
+                    split4<P>(x[0], x[1], x[2], x[3], hi, lo, ovf);
+                    _Float16* dst = xa + v_ * SX + (wm * MR + mr) * 32 + 8 * j + 4 * h;
+                    *(half4_t*)dst = hi;
+                    if constexpr (P == 1) *(half4_t*)(dst + K::PA) = lo;
+                }
+            }
+        for (int e = tid; e < 2 * (C / 8); e += 256) {
+            _Float16* dst = xa + (NF + e / (C / 8)) * SX + 8 * (e % (C / 8));
+            *(half8_t*)dst = half8_t{};
+            if constexpr (P == 1) *(half8_t*)(dst + K::PA) = half8_t{};
+        }
+    }
+    __syncthreads();
+
+    // ---- stage 3: conv3 (k3) over frames t0 + w, w < F -> y
+    stage_mma<3, C, NT, P>((const half8_t*)d.w[2], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
+    {
+        const float un = d.w_unscale[2];
+        float bia[MR][16], hv[MR][NR][16], rv[MR][NR][16];
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = row(mr, r);
+                bia[mr][r] = d.bias[2] ? d.bias[2][m] : 0.f;
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr) {
+                    const int w = (wn * NR + nr) * 32 + l32;
+                    const int t = t0 + w;
+                    const int tc = min(t, T - 1);   // the stores below skip t >= T
+                    hv[mr][nr][r] = hb[(int64_t)m * d.h_cstride + tc];
+                    if constexpr (EPI & kEpiRes2)
+                        rv[mr][nr][r] = d.res2[(int64_t)b * d.r2_bstride + (int64_t)m * d.r2_cstride + tc];
+                }
+            }
+        float* yb = d.y + (int64_t)b * d.y_bstride;
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+            for (int nr = 0; nr < NR; ++nr) {
+                const int w = (wn * NR + nr) * 32 + l32;
+                const int t = t0 + w;
+                if (w >= F || t >= T || ((d.dbg & 4) && !(d.dbg & 1024))) continue;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float v = __builtin_fmaf(__builtin_fmaf(accx[mr][nr][r], 1.f / 2048.f, acc[mr][nr][r]), un,
+                                             bia[mr][r]);
+                    v = (v + hv[mr][nr][r]) * d.s_res;
+                    if constexpr (EPI & kEpiRes2) v = (v + rv[mr][nr][r]) * d.s2;
+                    yb[(int64_t)row(mr, r) * d.y_cstride + t] = v;
+                }
+            }
+    }
+    if (__any(ovf) && lane == 0 && d.status) atomicOr(d.status, 1);
+}
+
+template <int C, int NT, int P, int EPI>
+int launch(const ou_block_desc& d, hipStream_t s)
+{
+    using K = BCfg<C, NT, P>;
+    static bool attr = false;
+    if (!attr) {
+        OU_HIP_CHECK(hipFuncSetAttribute((const void*)block_kernel<C, NT, P, EPI>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS_BYTES),
+                     "block: LDS attribute");
+        attr = true;
+    }
+    dim3 grid((d.length + K::F - 1) / K::F, d.batch);
+    hipLaunchKernelGGL((block_kernel<C, NT, P, EPI>), grid, dim3(256), K::LDS_BYTES, s, d);
+    return ou_check_launch("block");
+}
+
+template <int C, int NT, int P>
+int launch_epi(const ou_block_desc& d, hipStream_t s)
+{
+    const int epi = (d.film ? kEpiFilm : 0) | (d.sc ? kEpiSc : 0) | (d.cond_out ? kEpiCond : 0) |
+                    (d.res2 ? kEpiRes2 : 0);
+    switch (epi) {
+    case 0: return launch<C, NT, P, 0>(d, s);
+    case kEpiFilm: return launch<C, NT, P, kEpiFilm>(d, s);
+    case kEpiFilm | kEpiSc: return launch<C, NT, P, kEpiFilm | kEpiSc>(d, s);
+    case kEpiCond: return launch<C, NT, P, kEpiCond>(d, s);
+    case kEpiRes2: return launch<C, NT, P, kEpiRes2>(d, s);
+    }
+    return ou_fail(-1, "block: unsupported epilogue combination %d", epi);
+}
+
+// 32-frame N tiles per workgroup, per channel count
+template <int C>
+constexpr int nt_for()
+{
+    return C == 32 ? OU_BLOCK_NT32 : C == 64 ? OU_BLOCK_NT64 : C == 128 ? OU_BLOCK_NT128 : 1;
+}
+
+template <int P>
+int launch_p(const ou_block_desc& d, hipStream_t s)
+{
+    switch (d.channels) {
+    case 32: return launch_epi<32, nt_for<32>(), P>(d, s);
+    case 64: return launch_epi<64, nt_for<64>(), P>(d, s);
+    case 128: return launch_epi<128, nt_for<128>(), P>(d, s);
+    case 256: return launch_epi<256, 1, P>(d, s);
+    }
+    return ou_fail(-1, "block: unsupported channel count %d", d.channels);
+}
+
+}  // namespace
+
+// C = 256 (and the 512-channel bottleneck) stay on ou_conv: with one
+// workgroup owning every channel, the fused form re-streams the whole
+// 256 x 256 x 11 weight set for every 28 frames and is weight-bandwidth bound
+// (127 us against 52 us for the three ou_conv launches at 4005 frames,
+// tools/block_bench.py); at 32 / 64 / 128 channels it is 2.0x / 1.4x / 1.2x
+// faster than the unfused launches.
+extern "C" int ou_block_supported(int channels, int prec)
+{
+    return (prec == 1 || prec == 2) && (channels == 32 || channels == 64 || channels == 128);
+}
+
+extern "C" int ou_block_frames(int channels)
+{
+    switch (channels) {
+    case 32: return BCfg<32, nt_for<32>(), 1>::F;
+    case 64: return BCfg<64, nt_for<64>(), 1>::F;
+    case 128: return BCfg<128, nt_for<128>(), 1>::F;
+    case 256: return BCfg<256, 1, 1>::F;
+    }
+    return 0;
+}
+
+extern "C" int64_t ou_block_packed_halves(int channels, int kt)
+{
+    return (int64_t)channels * channels * kt * 2;
+}
+
+extern "C" int ou_block_pack(const float* w, int channels, int kt, void* out, float* w_unscale)
+{
+    if (!w || !out || !w_unscale || channels <= 0 || channels % 32 || kt <= 0)
+        return ou_fail(-1, "block_pack: bad arguments");
+    const int C = channels, KS = C / 16, MT = C / 32;
+    const int64_t n = (int64_t)C * C * kt;
+    float mx = 0.f;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!std::isfinite(w[i])) return ou_fail(-1, "block_pack: non-finite weight at %lld", (long long)i);
+        mx = std::fmax(mx, std::fabs(w[i]));
+    }
+    int e = 0;
+    if (mx > 0.f) {
+        int ex = 0;
+        std::frexp(mx, &ex);                       // mx in [2^(ex-1), 2^ex)
+        e = std::min(100, std::max(-100, 10 - ex));   // max|a| in [2^9, 2^10)
+    }
+    const float sc = std::ldexp(1.f, e);
+    _Float16* o = (_Float16*)out;
+    for (int mt = 0; mt < MT; ++mt)
+        for (int k = 0; k < kt; ++k)
+            for (int ks = 0; ks < KS; ++ks)
+                for (int plane = 0; plane < 2; ++plane)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int i = 0; i < 8; ++i) {
+                            const int row = mt * 32 + (lane & 31);
+                            const int c = ks * 16 + 8 * (lane >> 5) + i;
+                            const float a = w[((int64_t)row * C + c) * kt + k] * sc;
+                            const _Float16 hi = (_Float16)a;
+                            *o++ = plane == 0 ? hi : (_Float16)((a - (float)hi) * 2048.f);
+                        }
+    *w_unscale = std::ldexp(1.f, kStageShift - e);
+    return 0;
+}
+
+extern "C" int ou_block(const ou_block_desc* dp, void* stream)
+{
+    if (!dp) return ou_fail(-1, "block: null descriptor");
+    const ou_block_desc& d = *dp;
+    if (!d.h || !d.y || !d.w[0] || !d.w[1] || !d.w[2] || d.length <= 0 || d.batch <= 0 || d.batch > 65535)
+        return ou_fail(-1, "block: invalid descriptor");
+    if (!ou_block_supported(d.channels, d.prec))
+        return ou_fail(-1, "block: channels %d / prec %d not supported", d.channels, d.prec);
+    hipStream_t s = (hipStream_t)stream;
+    return d.prec == 1 ? launch_p<1>(d, s) : launch_p<2>(d, s);
+}

@@ -8,6 +8,7 @@
 // one host call regardless of the ~500 kernels inside.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -23,6 +24,10 @@ struct ou_program {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     hipStream_t cap_stream = nullptr;
+    // lanes: lane 0 runs on the caller's (or the capture) stream, lane i > 0
+    // on side[i - 1]; SIGNAL / WAIT ops order them through events[]
+    std::vector<hipStream_t> side;
+    std::vector<hipEvent_t> events;
 };
 
 static size_t expected_size(int op)
@@ -42,6 +47,112 @@ static size_t expected_size(int op)
     case OU_OP_SNAKE: return sizeof(ou_snake_desc);
     case OU_OP_MEMSET: return sizeof(ou_memset_desc);
     case OU_OP_ENSEMBLE: return sizeof(ou_ensemble_args);
+    case OU_OP_BLOCK: return sizeof(ou_block_desc);
+    case OU_OP_LANE: case OU_OP_SIGNAL: case OU_OP_WAIT: return sizeof(ou_sync_args);
+    }
+    return 0;
+}
+
+static int run_op(int kind, const void* p, hipStream_t s);
+
+static bool is_sync(int kind) { return kind == OU_OP_LANE || kind == OU_OP_SIGNAL || kind == OU_OP_WAIT; }
+
+// Lane structure check: every lane > 0 starts with a WAIT (it joins the
+// caller's stream / the capture through an event recorded on another lane),
+// every SIGNAL'd event is recorded before it is waited on, and the program
+// ends on lane 0 after waiting for the last SIGNAL of every other lane that
+// ran ops (so the caller's stream, and a captured graph, end after all of it).
+static int validate_lanes(const ou_program* p, int* n_lanes, int* n_events)
+{
+    int lane = 0, nl = 1, ne = 0;
+    std::vector<int> seen(1, 1), last_sig(1, -1), ops_in(1, 0);
+    std::vector<int> recorded, ev_lane;
+    for (const auto& o : p->ops) {
+        if (!is_sync(o.kind)) {
+            ops_in[lane]++;
+            continue;
+        }
+        const int v = ((const ou_sync_args*)o.desc.data())->id;
+        if (v < 0 || v > 63) return ou_fail(-1, "program: sync id %d out of range", v);
+        if (o.kind == OU_OP_LANE) {
+            if (v >= nl) {
+                nl = v + 1;
+                seen.resize(nl, 0), last_sig.resize(nl, -1), ops_in.resize(nl, 0);
+            }
+            lane = v;
+            continue;
+        }
+        if ((int)recorded.size() <= v) recorded.resize(v + 1, 0), ev_lane.resize(v + 1, -1);
+        ne = std::max(ne, v + 1);
+        if (o.kind == OU_OP_SIGNAL) {
+            if (lane > 0 && !seen[lane]) return ou_fail(-1, "program: lane %d signals before it waited", lane);
+            recorded[v] = 1;
+            ev_lane[v] = lane;
+            last_sig[lane] = v;
+        } else {
+            if (!recorded[v]) return ou_fail(-1, "program: wait on event %d before it is signalled", v);
+            seen[lane] = 1;
+        }
+    }
+    if (lane != 0) return ou_fail(-1, "program: must end on lane 0");
+    for (int l = 1; l < nl; ++l) {
+        if (!ops_in[l]) continue;
+        if (last_sig[l] < 0) return ou_fail(-1, "program: lane %d never signals lane 0", l);
+    }
+    // lane 0 must wait on every side lane's final signal after it was recorded
+    {
+        std::vector<int> done(nl, 0);
+        int cur = 0;
+        for (const auto& o : p->ops) {
+            if (!is_sync(o.kind)) continue;
+            const int v = ((const ou_sync_args*)o.desc.data())->id;
+            if (o.kind == OU_OP_LANE) cur = v;
+            else if (o.kind == OU_OP_WAIT && cur == 0 && ev_lane[v] > 0 && last_sig[ev_lane[v]] == v)
+                done[ev_lane[v]] = 1;
+        }
+        for (int l = 1; l < nl; ++l)
+            if (ops_in[l] && !done[l]) return ou_fail(-1, "program: lane 0 never joins lane %d", l);
+    }
+    *n_lanes = nl;
+    *n_events = ne;
+    return 0;
+}
+
+static int ensure_sync(ou_program* p, int n_lanes, int n_events)
+{
+    while ((int)p->side.size() < n_lanes - 1) {
+        hipStream_t st = nullptr;
+        OU_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "side stream");
+        p->side.push_back(st);
+    }
+    while ((int)p->events.size() < n_events) {
+        hipEvent_t e = nullptr;
+        OU_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming), "program event");
+        p->events.push_back(e);
+    }
+    return 0;
+}
+
+// Replay the op list with lanes on `s0` (lane 0) and the side streams.
+static int run_lanes(ou_program* p, hipStream_t s0)
+{
+    int nl = 1, ne = 0;
+    int rc = validate_lanes(p, &nl, &ne);
+    if (rc) return rc;
+    rc = ensure_sync(p, nl, ne);
+    if (rc) return rc;
+    hipStream_t cur = s0;
+    for (size_t i = 0; i < p->ops.size(); ++i) {
+        const auto& o = p->ops[i];
+        if (is_sync(o.kind)) {
+            const int v = ((const ou_sync_args*)o.desc.data())->id;
+            if (o.kind == OU_OP_LANE) cur = v == 0 ? s0 : p->side[v - 1];
+            else if (o.kind == OU_OP_SIGNAL) OU_HIP_CHECK(hipEventRecord(p->events[v], cur), "program signal");
+            else OU_HIP_CHECK(hipStreamWaitEvent(cur, p->events[v], 0), "program wait");
+            continue;
+        }
+        rc = run_op(o.kind, o.desc.data(), cur);
+        if (rc) return rc;
     }
     return 0;
 }
@@ -82,6 +193,7 @@ static int run_op(int kind, const void* p, hipStream_t s)
         return ou_finish(a->x, a->x_bstride, a->left, a->y, a->batch, a->len, a->mix_rms, s);
     }
     case OU_OP_SNAKE: return ou_snake_aa((const ou_snake_desc*)p, s);
+    case OU_OP_BLOCK: return ou_block((const ou_block_desc*)p, s);
     case OU_OP_MEMSET: {
         auto a = (const ou_memset_desc*)p;
         OU_HIP_CHECK(hipMemsetAsync(a->ptr, 0, a->bytes, s), "memset");
@@ -119,6 +231,8 @@ void ou_program_destroy(ou_program* p)
     if (!p) return;
     drop_graph(p);
     if (p->cap_stream) (void)hipStreamDestroy(p->cap_stream);
+    for (auto st : p->side) (void)hipStreamDestroy(st);
+    for (auto e : p->events) (void)hipEventDestroy(e);
     delete p;
 }
 
@@ -143,12 +257,7 @@ int ou_program_size(const ou_program* p) { return p ? (int)p->ops.size() : -1; }
 int ou_program_run(ou_program* p, void* stream)
 {
     if (!p) return ou_fail(-1, "program_run: null");
-    hipStream_t s = (hipStream_t)stream;
-    for (size_t i = 0; i < p->ops.size(); ++i) {
-        const int rc = run_op(p->ops[i].kind, p->ops[i].desc.data(), s);
-        if (rc) return rc;
-    }
-    return 0;
+    return run_lanes(p, (hipStream_t)stream);
 }
 
 int ou_program_capture(ou_program* p)
@@ -160,9 +269,16 @@ int ou_program_capture(ou_program* p)
                      "capture stream");
     OU_HIP_CHECK(hipStreamBeginCapture(p->cap_stream, hipStreamCaptureModeThreadLocal),
                  "begin capture");
-    int rc = 0;
-    for (size_t i = 0; i < p->ops.size() && rc == 0; ++i)
-        rc = run_op(p->ops[i].kind, p->ops[i].desc.data(), p->cap_stream);
+    int nl = 1, ne = 0;
+    int rc = validate_lanes(p, &nl, &ne);
+    if (rc == 0) rc = ensure_sync(p, nl, ne);
+    if (rc) {
+        hipGraph_t g0 = nullptr;
+        (void)hipStreamEndCapture(p->cap_stream, &g0);
+        if (g0) (void)hipGraphDestroy(g0);
+        return rc;
+    }
+    rc = run_lanes(p, p->cap_stream);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(p->cap_stream, &g);
     if (rc) {
@@ -201,8 +317,9 @@ int ou_program_profile(ou_program* p, void* stream, float* ms)
     for (auto& e : ev) OU_HIP_CHECK(hipEventCreate(&e), "event create");
     int rc = 0;
     (void)hipEventRecord(ev[0], s);
+    // lanes are ignored here: the op list in order is a valid serial schedule
     for (size_t i = 0; i < n && rc == 0; ++i) {
-        rc = run_op(p->ops[i].kind, p->ops[i].desc.data(), s);
+        if (!is_sync(p->ops[i].kind)) rc = run_op(p->ops[i].kind, p->ops[i].desc.data(), s);
         (void)hipEventRecord(ev[i + 1], s);
     }
     if (rc == 0) {

@@ -55,6 +55,24 @@ KSWS_BYTES = 64 << 20
 # f32) and the atomics cost 1-11 us per launch (tools/conv_bench.py --amax).
 AMAX_SLOTS = 256
 _REC = None
+# lane the recorder is on (plan lanes run concurrently): convs recorded on lane
+# i > 0 use the i-th K-slice workspace of their engine
+_LANE = 0
+MAX_LANES = 2
+
+
+def set_lane(prog, i):
+    """Switch the recording program (and conv_desc's K-slice workspace) to lane i."""
+    global _LANE
+    assert 0 <= i < MAX_LANES
+    prog.lane(i)
+    _LANE = i
+
+
+def overlap_enabled():
+    import os
+
+    return os.environ.get("OUHIP_OVERLAP", "1") != "0"
 
 
 def split_amax_enabled():
@@ -251,6 +269,15 @@ def prep_up(sd, p, r, antialias, device):
 
 
 @dataclass
+class FusedW:
+    """The three convs of a ConvBlock packed for ou_block (one launch)."""
+    w: torch.Tensor          # packed halves of conv1 | conv2 | conv3 (int16 storage)
+    offs: tuple              # element offsets of the three packed convs in w
+    unscale: tuple
+    prec: int
+
+
+@dataclass
 class BlockW:
     """ConvBlock weights (blocks.py:234-351)."""
     C: int
@@ -260,18 +287,41 @@ class BlockW:
     conv2: ConvW
     conv3: ConvW
     rate_conv: Optional[ConvW] = None
+    fused: Optional[FusedW] = None
+
+
+def fuse_blocks_enabled():
+    import os
+
+    return os.environ.get("OUHIP_FUSE_BLOCKS", "1") != "0" and not split_amax_enabled()
+
+
+def prep_fused(specs, C, prec, device):
+    """ou_block weights for a ConvBlock whose channel count one workgroup
+    covers (ou_block_supported), else None."""
+    if not (fuse_blocks_enabled() and L.load().ou_block_supported(C, prec)):
+        return None
+    parts, offs, uns, off = [], [], [], 0
+    for sp in specs:
+        packed, un = L.block_pack(sp.w)
+        parts.append(packed)
+        offs.append(off)
+        uns.append(un)
+        off += packed.size
+    w = torch.from_numpy(np.concatenate(parts)).to(device)
+    return FusedW(w, tuple(offs), tuple(uns), prec)
 
 
 def prep_block(sd, p, kind, rate, antialias, device):
-    c1 = prep_same(sd, p + ".conv1", 5, device)
-    c2 = prep_same(sd, p + ".conv2", 3, device)
-    c3 = prep_same(sd, p + ".conv3", 3, device)
+    specs = [spec_same(sd, p + ".conv1", 5), spec_same(sd, p + ".conv2", 3), spec_same(sd, p + ".conv3", 3)]
+    c1, c2, c3 = (make_conv(sp, device) for sp in specs)
     rc = None
     if kind == "down":
         rc = prep_down(sd, p + ".rate_change_conv", rate, antialias, device)
     elif kind == "up":
         rc = prep_up(sd, p + ".rate_change_conv", rate, antialias, device)
-    return BlockW(c1.m, kind, rate, c1, c2, c3, rc)
+    fused = prep_fused(specs, c1.m, c1.prec, device) if c1.prec in (1, 2) else None
+    return BlockW(c1.m, kind, rate, c1, c2, c3, rc, fused)
 
 
 @dataclass
@@ -324,6 +374,8 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
     d.w, d.m, d.kt, d.pad, d.cc = cw.w.data_ptr(), cw.m, cw.kt, cw.pad, cw.cc
     d.prec, d.w_unscale, d.status = cw.prec, cw.w_unscale, cw.status
     d.ks_ws, d.ks_ws_bytes = cw.ks_ws
+    if _LANE and d.ks_ws:   # the engine allocates MAX_LANES workspaces back to back
+        d.ks_ws += _LANE * d.ks_ws_bytes
     if _REC is not None and _REC["prec"] == 1:
         if cw.prec == 1 and x.ptr in _REC["slots"]:
             d.amax_in = _amax_slot(x)
@@ -366,11 +418,52 @@ def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film
        cond_out = conv1(h); c = (cond_out + sc)/sqrt2; c = film(c); c = conv3(conv2(c));
        out = (h + c)/sqrt2 [; out = (out + res2) * s2]"""
     c1_out = cond_out if cond_out is not None else tA
-    prog.add(L.OP_CONV, conv_desc(bw.conv1, h, c1_out, res1=sc, s1=NF2, film=film, film_bs=film_bs))
+    d1 = conv_desc(bw.conv1, h, c1_out, res1=sc, s1=NF2, film=film, film_bs=film_bs)
     if skip_tail:
+        prog.add(L.OP_CONV, d1)
         return
-    prog.add(L.OP_CONV, conv_desc(bw.conv2, c1_out, tB))
-    prog.add(L.OP_CONV, conv_desc(bw.conv3, tB, out, res1=h, s1=NF2, res2=res2, s2=s2))
+    d2 = conv_desc(bw.conv2, c1_out, tB)
+    d3 = conv_desc(bw.conv3, tB, out, res1=h, s1=NF2, res2=res2, s2=s2)
+    if bw.fused is not None and out.ptr != h.ptr:
+        prog.add(L.OP_BLOCK, block_desc(bw, h, out, (d1, d2, d3), sc=sc, film=film, film_bs=film_bs,
+                                        cond_out=cond_out, res2=res2, s2=s2))
+        return
+    prog.add(L.OP_CONV, d1)
+    prog.add(L.OP_CONV, d2)
+    prog.add(L.OP_CONV, d3)
+
+
+def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film_bs=0, cond_out: Act = None,
+               res2: Act = None, s2=1.0):
+    """ou_block descriptor of a ConvBlock's main path; ``descs`` are the three
+    equivalent ou_conv descriptors (their shape checks have run; their
+    algorithmic FLOPs and bytes -- the unfused reference ops -- are kept)."""
+    fw = bw.fused
+    d = L.BlockDesc()
+    d.h, d.h_bstride, d.h_cstride = h.ptr, h.bs, h.cs
+    d.channels, d.length, d.batch, d.prec = bw.C, h.T, h.B, fw.prec
+    assert out.C == bw.C and out.T == h.T and out.B >= h.B, ("block output", out.t.shape, h.t.shape)
+    for i, cw in enumerate((bw.conv1, bw.conv2, bw.conv3)):
+        d.w[i] = fw.w.data_ptr() + 2 * fw.offs[i]
+        d.bias[i] = cw.bias.data_ptr() if cw.bias is not None else 0
+        d.slope[i] = cw.slope
+        d.w_unscale[i] = fw.unscale[i]
+    if sc is not None:
+        assert sc.C == bw.C and sc.T >= h.T and sc.ptr != out.ptr
+        d.sc, d.sc_bstride, d.sc_cstride, d.s_sc = sc.ptr, sc.bs, sc.cs, float(NF2)
+    d.film, d.film_bstride = film or 0, film_bs
+    if cond_out is not None:
+        assert cond_out.C == bw.C and cond_out.T >= h.T and cond_out.ptr != out.ptr
+        d.cond_out, d.co_bstride, d.co_cstride = cond_out.ptr, cond_out.bs, cond_out.cs
+    d.y, d.y_bstride, d.y_cstride = out.ptr, out.bs, out.cs
+    d.s_res, d.s2 = float(NF2), float(s2)
+    if res2 is not None:
+        assert res2.C == bw.C and res2.T >= h.T and res2.ptr != out.ptr
+        d.res2, d.r2_bstride, d.r2_cstride = res2.ptr, res2.bs, res2.cs
+    d.status = bw.conv1.status or 0
+    d._flops = sum(x._flops for x in descs)
+    d._bytes = sum(x._bytes for x in descs)
+    return d
 
 
 GRU_FLAGS = -1   # kernel default (XCD-local chains); see ou_gru_desc.flags
@@ -558,9 +651,10 @@ class Engine:
         self.has_sdl = False
         # [0] GRU hand-off timeout, [1] split-f16 conv range error (plan.check)
         self.status = torch.zeros(4, dtype=torch.int32, device=dev)
-        # K-slice partial sums (ou_conv tile bits 12-13): ops run one after
-        # another on the stream, so every conv of this engine shares one buffer
-        self.ks_ws = torch.empty(KSWS_BYTES // 4, dtype=torch.float32, device=dev)
+        # K-slice partial sums (ou_conv tile bits 12-13): ops of one lane run
+        # one after another, so the convs of a lane share one buffer (one per
+        # plan lane: conv_desc offsets by the recording lane)
+        self.ks_ws = torch.empty(MAX_LANES * KSWS_BYTES // 4, dtype=torch.float32, device=dev)
         saved = _PREP_PREC, _PREP_STATUS, _PREP_KSWS
         _PREP_PREC, _PREP_STATUS = self.conv_prec, self.status.data_ptr() + 4
         _PREP_KSWS = (self.ks_ws.data_ptr(), KSWS_BYTES)
@@ -725,9 +819,11 @@ class Engine:
         n = len(self.s_enc)
         return [n - 1 - l for l in range(n)]
 
-    def rec_score(self, prog, bufs, x: Act, film_base, film_bs, in_scale=0, sc_list=None):
+    def rec_score(self, prog, bufs, x: Act, film_base, film_bs, in_scale=0, sc_list=None, before_decoder=None):
         """ScoreNetwork.forward up to (not including) the head
-        (score.py:278-290).  Returns the decoder output Act."""
+        (score.py:278-290).  Returns the decoder output Act.  The encoder and
+        the bottleneck GRU do not read the conditions (score.py:284-286):
+        ``before_decoder()`` runs at the point the decoder first needs them."""
         n_lvl = len(self.s_enc)
         nr = len(self.rates)
         fb = lambda j: film_base + 4 * self.film_off[j]
@@ -745,6 +841,8 @@ class Engine:
         rec_gru(prog, self.s_gru, 0, bufs[f"V{top}"], bufs["GI"], bufs[f"V{top}"],
                 bufs["gran"], self.status, res=bufs[f"V{top}"], res_scale=NF2)
         # decoder (score.py:197-211)
+        if before_decoder is not None:
+            before_decoder()
         h = None
         for l in range(n_lvl):
             i = top - l

@@ -71,6 +71,7 @@ class _PlanBase:
                 init(self, *a, **k)
             finally:
                 E.end_record()
+                E._LANE = 0
 
         cls.__init__ = wrapped
 
@@ -141,6 +142,17 @@ class EnhancePlan(_PlanBase):
         level = 10 ** (eng.level_db / 20.0)
         p.add(L.OP_NORMALIZE, L.NormArgs(x=self.XP.ptr, y=self.XN.ptr, batch=B, n=Tp,
                                          level=level, eps=1e-5))
+        # The conditioner (and the loop-invariant signal_cond_proj convs) run
+        # on lane 1 concurrently with lane 0's first score-network encoder and
+        # bottleneck GRU, which do not read the conditions (score.py:284-286);
+        # lane 0 waits for them right before the first decoder.  Not with the
+        # aux / warm-start paths, whose initial sample needs the conditioner.
+        self.overlap = E.overlap_enabled() and not use_aux_signal and warm_start is None
+        ev_cond = None
+        if self.overlap:
+            ev_in = p.signal()
+            E.set_lane(p, 1)
+            p.wait(ev_in)
         conds, yaux = eng.rec_cond(p, cb, self.XN, need_aux=use_aux_signal or warm_start is not None)
         if use_aux_signal or warm_start is not None:
             self.AUXT = new_act(B, yaux.C, Tp, dev)
@@ -154,6 +166,9 @@ class EnhancePlan(_PlanBase):
         else:
             self.SC = eng.alloc_sc(B, Tp)
             eng.rec_sc(p, conds, self.SC)
+            if self.overlap:
+                ev_cond = p.signal()
+                E.set_lane(p, 0)
             # FiLM parameters for every step at once (noise embedding, K7)
             steps = list(range(n_start, n_steps))
             snet = np.array([(f32(edm["noise"]) * sig[n]) if edm is not None else sig[n]
@@ -190,8 +205,9 @@ class EnhancePlan(_PlanBase):
             zi = 1
             for n in steps:
                 in_scale = self.WIN[n].data_ptr() if edm is not None else 0
+                join = (lambda: p.wait(ev_cond)) if (ev_cond is not None and n == steps[0]) else None
                 h = eng.rec_score(p, self.sb, self.X, film_base + 4 * n * eng.film_rows, 0,
-                                  in_scale=in_scale, sc_list=self.SC)
+                                  in_scale=in_scale, sc_list=self.SC, before_decoder=join)
                 last = n == n_steps - 1
                 z_ptr = 0 if last else self.NZ[zi].data_ptr()
                 zi += 0 if last else 1

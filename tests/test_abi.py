@@ -36,7 +36,7 @@ STRUCTS = {
     "ou_head_desc": L.HeadDesc, "ou_snake_desc": L.SnakeDesc, "ou_memset_desc": L.MemsetArgs,
     "ou_norm_args": L.NormArgs, "ou_rms_args": L.RmsArgs, "ou_power_args": L.PowerArgs,
     "ou_pad_args": L.PadArgs, "ou_scale_args": L.ScaleArgs, "ou_finish_args": L.FinishArgs,
-    "ou_ensemble_args": L.EnsembleArgs,
+    "ou_ensemble_args": L.EnsembleArgs, "ou_block_desc": L.BlockDesc, "ou_sync_args": L.SyncArgs,
 }
 
 

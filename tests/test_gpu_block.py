@@ -1,0 +1,132 @@
+"""ou_block (fused ConvBlock main path) against the unfused ou_conv sequence
+and a float64 torch evaluation of the reference arithmetic
+(blocks.py:393-416): every supported channel count, every optional epilogue
+input, lengths that are not multiples of the workgroup's frame count (and
+shorter than it), batch 2, split-f16 and f16 operands."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from open_universe_amd import _lib as L
+from open_universe_amd import engine as E
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _specs(C, g):
+    out = []
+    for k in (5, 3, 3):
+        w = torch.randn(C, C, k, generator=g) / np.sqrt(C * k)
+        b = 0.1 * torch.randn(C, generator=g)
+        slope = float(0.05 + 0.4 * torch.rand(1, generator=g))
+        out.append(E.ConvSpec(w.numpy(), C, 1, (k - 1) // 2, 1, slope, b.numpy(), ref_macs=float(w.numel())))
+    return out
+
+
+def _ref(specs, h, sc=None, film=None, res2=None, s2=1.0):
+    """float64 restatement: PReLU -> conv (zero 'same' padding) -> bias."""
+    def pc(sp, x):
+        x = torch.where(x >= 0, x, sp.slope * x)
+        w = torch.from_numpy(sp.w).double()
+        return F.conv1d(x, w, padding=sp.pad) + torch.from_numpy(sp.bias).double()[None, :, None]
+
+    r = 0.5 ** 0.5
+    c1 = pc(specs[0], h)
+    if sc is not None:
+        c1 = (c1 + sc) * r
+    if film is not None:
+        C = h.shape[1]
+        c1 = film[:, :C, None] * c1 + film[:, C:, None]
+    y = (h + pc(specs[2], pc(specs[1], c1))) * r
+    if res2 is not None:
+        y = (y + res2) * s2
+    return y, c1
+
+
+def _run(bw, h, out, fused, **kw):
+    keep = bw.fused
+    if not fused:
+        bw.fused = None
+    try:
+        prog = L.Program()
+        tA = E.new_act(h.B, h.C, h.T, DEV)
+        tB = E.new_act(h.B, h.C, h.T, DEV)
+        E.rec_block(prog, bw, h, out, tA, tB, **kw)
+        kinds = prog.op_kinds()
+        prog.run(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        bw.fused = keep
+    return kinds
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm())
+
+
+@pytest.mark.parametrize("prec", [1, 2])
+@pytest.mark.parametrize("C,T", [(32, 1000), (32, 7), (64, 300), (64, 60), (128, 125), (128, 29), (128, 3)])
+@pytest.mark.parametrize("mode", ["plain", "score_dec", "cond_dec", "res2"])
+def test_block_vs_unfused_and_reference(C, T, mode, prec):
+    g = torch.Generator().manual_seed(C * 1000 + T)
+    specs = _specs(C, g)
+    B = 2
+    status = torch.zeros(4, dtype=torch.int32, device=DEV)
+    saved = E._PREP_STATUS
+    E._PREP_STATUS = status.data_ptr() + 4
+    try:
+        cws = [E.make_conv(sp, DEV, prec=prec) for sp in specs]
+        fused = E.prep_fused(specs, C, prec, DEV)
+    finally:
+        E._PREP_STATUS = saved
+    assert fused is not None
+    bw = E.BlockW(C, "none", None, *cws, None, fused)
+    h = torch.randn(B, C, T, generator=g)
+    sc = torch.randn(B, C, T, generator=g) if mode == "score_dec" else None
+    film = (1.0 + 0.3 * torch.randn(B, 2 * C, generator=g)) if mode == "score_dec" else None
+    res2 = torch.randn(B, C, T, generator=g) if mode == "res2" else None
+    ref, c1 = _ref(specs, h.double(), None if sc is None else sc.double(),
+                   None if film is None else film.double(), None if res2 is None else res2.double(), 0.7)
+    ha = E.Act(h.to(DEV))
+    kw = {}
+    film_dev = film.to(DEV) if film is not None else None   # referenced until the launches ran
+    if sc is not None:
+        kw.update(sc=E.Act(sc.to(DEV)), film=film_dev.data_ptr(), film_bs=2 * C)
+    if res2 is not None:
+        kw.update(res2=E.Act(res2.to(DEV)), s2=0.7)
+    outs = {}
+    for fz in (True, False):
+        out = E.new_act(B, C, T, DEV)
+        co = E.new_act(B, C, T, DEV) if mode == "cond_dec" else None
+        kinds = _run(bw, ha, out, fz, cond_out=co, **kw)
+        assert (L.OP_BLOCK in kinds) == fz
+        outs[fz] = (out.t.clone(), None if co is None else co.t.clone())
+    assert int(status.abs().sum()) == 0
+    tol = 1e-5 if prec == 1 else 3e-3
+    assert _rel(outs[True][0], ref) < tol
+    assert _rel(outs[True][0], outs[False][0]) < (1e-5 if prec == 1 else 3e-3)
+    if mode == "cond_dec":
+        assert _rel(outs[True][1], c1) < tol
+
+
+def test_block_range_flag():
+    """A staged input beyond the split-f16 range sets the status word."""
+    C, T = 64, 200
+    g = torch.Generator().manual_seed(1)
+    specs = _specs(C, g)
+    status = torch.zeros(4, dtype=torch.int32, device=DEV)
+    saved = E._PREP_STATUS
+    E._PREP_STATUS = status.data_ptr() + 4
+    try:
+        cws = [E.make_conv(sp, DEV, prec=1) for sp in specs]
+    finally:
+        E._PREP_STATUS = saved
+    bw = E.BlockW(C, "none", None, *cws, None, E.prep_fused(specs, C, 1, DEV))
+    h = torch.randn(1, C, T, generator=g)
+    h[0, 3, 50] = 3.0e6
+    out = E.new_act(1, C, T, DEV)
+    _run(bw, E.Act(h.to(DEV)), out, True)
+    assert int(status[1]) == 1
