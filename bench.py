@@ -29,6 +29,8 @@ Extra fields:
                 and the config's B.
   f32_value     (c2) a second timed pass with f32 conv operands, beside the
                 default split-f16 operand build.
+  queued_value  (c2) the same batch-1 clips with two enhances in flight on
+                two streams (a queue of batch-1 requests); not the headline.
 Weights are synthetic (no trained checkpoint offline); timing does not depend
 on weight values.
 """
@@ -270,6 +272,8 @@ def main():
     ap.add_argument("--seconds", type=float, default=None, help="override the config's clip length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-queued", action="store_true",
+                    help="skip the extra leg with two batch-1 enhances in flight (queued_value)")
     ap.add_argument("--no-f32-pass", action="store_true",
                     help="skip the second timed pass with f32 conv operands (f32_value)")
     ap.add_argument("--dump-ops", default=None, help="write per-op profile rows (JSON)")
@@ -351,6 +355,19 @@ def main():
                "ms_per_step": round(1000.0 * e32 / args.steps, 3)}
         del m32
 
+    # extra leg: the same B=1 clips with two enhances in flight on two streams
+    # (Universe.enhance_many) -- the throughput of a queue of batch-1
+    # requests; the headline value above stays strictly one clip at a time
+    queued = None
+    if args.config == "c2" and not args.no_queued and not C["n_steps"]:
+        seq = [clips[i % len(clips)] for i in range(args.steps)]
+        with torch.no_grad():
+            model.enhance_many(seq[: max(2, args.warmup)], rng=rng, streams=2)
+            eq = timed_loop(lambda i: model.enhance_many(seq, rng=rng, streams=2), 0, 1, world, sync)
+        queued = {"streams": 2, "clips": args.steps,
+                  "value": round(world * B * args.steps * args.seconds / eq, 3),
+                  "ms_per_clip": round(1000.0 * eq / args.steps, 3)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(model, cfg, C, args.config)
@@ -392,6 +409,10 @@ def main():
                        "parallelism": f"utterance-shard x{world}"},
             "xrt_per_gpu": round(value / world, 3),
         }
+        if queued is not None:
+            out["queued_value"] = queued["value"]
+            out["queued"] = {**queued, "note": "extra leg: the same batch-1 clips, two enhance() calls in "
+                                               "flight on two HIP streams (Universe.enhance_many)"}
         if f32 is not None:
             out["f32_value"] = f32["value"]
             out["f32_pass"] = {**f32, "dtype": "f32 (v_mfma_f32_32x32x2_f32 conv operands)",

@@ -55,10 +55,14 @@ KSWS_BYTES = 64 << 20
 # f32) and the atomics cost 1-11 us per launch (tools/conv_bench.py --amax).
 AMAX_SLOTS = 256
 _REC = None
-# lane the recorder is on (plan lanes run concurrently): convs recorded on lane
-# i > 0 use the i-th K-slice workspace of their engine
+# lane the recorder is on (plan lanes run concurrently) and the plan slot
+# (plans of one model that may run at the same time on different streams,
+# Universe.enhance_many): convs recorded on (slot, lane) use K-slice workspace
+# slot * MAX_LANES + lane of their engine
 _LANE = 0
+_SLOT = 0
 MAX_LANES = 2
+MAX_SLOTS = 2
 
 
 def set_lane(prog, i):
@@ -374,8 +378,8 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
     d.w, d.m, d.kt, d.pad, d.cc = cw.w.data_ptr(), cw.m, cw.kt, cw.pad, cw.cc
     d.prec, d.w_unscale, d.status = cw.prec, cw.w_unscale, cw.status
     d.ks_ws, d.ks_ws_bytes = cw.ks_ws
-    if _LANE and d.ks_ws:   # the engine allocates MAX_LANES workspaces back to back
-        d.ks_ws += _LANE * d.ks_ws_bytes
+    if (_LANE or _SLOT) and d.ks_ws:   # the engine allocates MAX_SLOTS x MAX_LANES workspaces
+        d.ks_ws += (_SLOT * MAX_LANES + _LANE) * d.ks_ws_bytes
     if _REC is not None and _REC["prec"] == 1:
         if cw.prec == 1 and x.ptr in _REC["slots"]:
             d.amax_in = _amax_slot(x)
@@ -517,6 +521,7 @@ class ConvTuner:
         self.cache = {}
         self.reps = reps
         self.path = path
+        self.timed = 0   # geometries tuned by timing (not reused from another length)
         if path and os.path.exists(path):
             with open(path) as fh:
                 self.cache = {tuple(json.loads(k)): v for k, v in json.load(fh).items()}
@@ -529,11 +534,29 @@ class ConvTuner:
                 json.dump({json.dumps(list(k)): v for k, v in self.cache.items()}, fh)
 
     @staticmethod
-    def key(d):
+    def bucket(n):
+        """Octave bucket of a frame count: plans for clips of other lengths
+        reuse the tiles tuned for the same geometry at a similar length."""
+        return int(n).bit_length()
+
+    @staticmethod
+    def geometry(d):
         # bool(ks_ws): K-slice tiles are only valid with a workspace
-        return (d.m, d.cin, d.frame, d.kt, d.pad, d.n_frames, d.batch, d.rout, d.in_len,
-                d.out_len, bool(d.res1), bool(d.film), bool(d.res2), bool(d.in_scale), d.prec,
-                bool(d.amax_out), bool(d.ks_ws))
+        return (d.m, d.cin, d.frame, d.kt, d.pad, d.batch, d.rout, bool(d.res1), bool(d.film), bool(d.res2),
+                bool(d.in_scale), d.prec, bool(d.amax_out), bool(d.ks_ws))
+
+    @classmethod
+    def key(cls, d):
+        return cls.geometry(d) + (cls.bucket(d.n_frames),)
+
+    @staticmethod
+    def fit_workspace(d, tile):
+        """Drop the K-slice bits of a tile whose partial sums might not fit the
+        workspace at this frame count (bound with generous tile padding)."""
+        S = 1 << ((tile >> 12) & 3)
+        if S > 1 and S * (d.n_frames + 256) * (d.m + 256) * d.batch * 4 > d.ks_ws_bytes:
+            return tile & ~(3 << 12)
+        return tile
 
     def __call__(self, d):
         import ctypes
@@ -541,10 +564,19 @@ class ConvTuner:
 
         k = self.key(d)
         if k in self.cache:
-            return self.cache[k]
+            return self.fit_workspace(d, self.cache[k])
+        # the same geometry tuned at another length: reuse its tile (nearest
+        # bucket) instead of timing every candidate again
+        g, b = self.geometry(d), self.bucket(d.n_frames)
+        near = [kk for kk in self.cache if kk[:-1] == g]
+        if near and os.environ.get("OUHIP_TUNE_EVERY_LENGTH", "0") != "1":
+            kk = min(near, key=lambda kk: (abs(kk[-1] - b), kk[-1]))
+            self.cache[k] = self.cache[kk]
+            return self.fit_workspace(d, self.cache[k])
         lib = L.load()
         stream = torch.cuda.current_stream().cuda_stream
         best, best_ms = -1, float("inf")
+        self.timed += 1
         # tile shape x log2(output tiles per workgroup); > 0 = persistent kernel
         # (bit 10: the warp-specialised persistent kernel)
         # (split-f16, bit 11 in the query only, and amax tracking: one-tile workgroups)
@@ -654,7 +686,7 @@ class Engine:
         # K-slice partial sums (ou_conv tile bits 12-13): ops of one lane run
         # one after another, so the convs of a lane share one buffer (one per
         # plan lane: conv_desc offsets by the recording lane)
-        self.ks_ws = torch.empty(MAX_LANES * KSWS_BYTES // 4, dtype=torch.float32, device=dev)
+        self.ks_ws = torch.empty(MAX_SLOTS * MAX_LANES * KSWS_BYTES // 4, dtype=torch.float32, device=dev)
         saved = _PREP_PREC, _PREP_STATUS, _PREP_KSWS
         _PREP_PREC, _PREP_STATUS = self.conv_prec, self.status.data_ptr() + 4
         _PREP_KSWS = (self.ks_ws.data_ptr(), KSWS_BYTES)

@@ -16,8 +16,10 @@ with ``torch.randn(..., generator=rng)`` on the device in the reference's order
 (x0, then one z per step), so a run is bit-comparable in its noise to the
 reference on the same device and generator.
 """
+import collections
 import itertools
 import math
+import os
 from typing import Optional
 
 import torch
@@ -81,7 +83,7 @@ class Universe(nn.Module):
         self.init_losses(score_model, condition_model, self.losses_kwargs, training)
         self.ema = None  # EMA weights are applied at load time (inference only)
         self._engine = None
-        self._plans = {}
+        self._plans = collections.OrderedDict()   # LRU of recorded plans, see _plan()
         self._conv_prec = None   # None: OUHIP_CONV_PREC; 0 after a split-f16 range error
 
     def init_losses(self, score_model, condition_model, losses, training):
@@ -114,12 +116,30 @@ class Universe(nn.Module):
         dev = next(self.parameters()).device
         if self._engine is None or self._engine.device != dev:
             self._engine = Engine(self._model_cfg(), self.state_dict(), dev, conv_prec=self._conv_prec)
-            self._plans = {}
+            self._plans = collections.OrderedDict()
         return self._engine
+
+    def _plan(self, key, make):
+        """The recorded plan for a (batch, length, options) key.  Plans are
+        kept in an LRU of OUHIP_MAX_PLANS (default 8) entries: a stream of clips
+        of many lengths (the CLI over a folder) records one plan per length and
+        evicts the least recently used, whose buffers return to the caching
+        allocator for the next plan.  Tiles are tuned once per layer geometry
+        (engine.ConvTuner reuses them across lengths), so recording a plan for a
+        new length launches nothing but the graph capture."""
+        plan = self._plans.get(key)
+        if plan is not None:
+            self._plans.move_to_end(key)
+            return plan
+        cap = max(1, int(os.environ.get("OUHIP_MAX_PLANS", "8")))
+        while len(self._plans) >= cap:
+            self._plans.popitem(last=False)
+        plan = self._plans[key] = make()
+        return plan
 
     def invalidate(self):
         """Drop the packed device weights (call after changing parameters)."""
-        self._engine, self._plans = None, {}
+        self._engine, self._plans = None, collections.OrderedDict()
 
     def _apply(self, fn, *args, **kwargs):
         self.invalidate()
@@ -205,9 +225,7 @@ class Universe(nn.Module):
                                    diff=dict(self.diff_kwargs), ensemble=ensemble,
                                    ensemble_mode=ens_mode)
 
-            plan = self._plans.get(key)
-            if plan is None:
-                plan = self._plans[key] = make_plan(eng)
+            plan = self._plan(key, lambda: make_plan(eng))
             try:
                 x = plan(mix, rng).clone()[:, None, :]
             except L.OuRangeError:
@@ -216,13 +234,79 @@ class Universe(nn.Module):
                 nz = plan.NZ.clone()
                 self._conv_prec = 0
                 self.invalidate()
-                plan = self._plans[key] = make_plan(self._get_engine())
+                plan = self._plan(key, lambda: make_plan(self._get_engine()))
                 x = plan.run_with_noise(mix, nz).clone()[:, None, :]
         if x_ndim == 1:
             x = x[0, 0]
         elif x_ndim == 2:
             x = x[:, 0, :]
         return x
+
+    def enhance_many(self, mixes, n_steps: Optional[int] = None, epsilon: Optional[float] = None,
+                     rng: Optional[torch.Generator] = None, keep_rms: Optional[bool] = False, streams: int = 2):
+        """Enhance a sequence of clips (each a (T,), (B, T) or (B, 1, T) device
+        tensor, as ``enhance`` takes them) with up to ``streams`` enhances in
+        flight at once, on their own HIP streams and plans.  At batch 1 one
+        enhance leaves most of the chip idle while its GRUs run (a serial
+        801-step chain per clip); a second clip's convolutions fill it.  Each
+        clip's result equals ``enhance`` of that clip with the noise drawn in
+        clip order from ``rng``.  Returns the list of outputs."""
+        from ...plan import EnhancePlan
+        from ... import engine as E
+
+        if epsilon is None:
+            epsilon = self.diff_kwargs.epsilon
+        if n_steps is None:
+            n_steps = self.diff_kwargs.n_steps
+        S = max(1, min(int(streams), E.MAX_SLOTS))
+        eng = self._get_engine()
+        if not hasattr(self, "_streams") or len(self._streams) < S:
+            self._streams = [torch.cuda.Stream(device=eng.device) for _ in range(S)]
+        main = torch.cuda.current_stream(eng.device)
+        shapes, outs, pending = [], [], []
+        for i, mix in enumerate(mixes):
+            nd = mix.ndim
+            m3 = mix[None, None, :] if nd == 1 else mix[:, None, :] if nd == 2 else mix
+            if nd > 3:
+                raise ValueError("The input should have at most 3 dimensions")
+            m3 = m3.to(torch.float32).contiguous()
+            B, _, T = m3.shape
+            slot = i % S
+            key = (B, T, int(n_steps), float(epsilon), bool(keep_rms), False, None, None, None, slot)
+            plan = self._plan(key, lambda: EnhancePlan(eng, B, T, int(n_steps), float(epsilon),
+                                                       keep_rms=bool(keep_rms), diff=dict(self.diff_kwargs),
+                                                       slot=slot))
+            st = self._streams[slot]
+            st.wait_stream(main)   # the input was produced on the caller's stream
+            with torch.cuda.stream(st):
+                out = plan.submit(m3, rng).clone()
+                nz = plan.NZ.clone()   # kept for a rerun with f32 operands
+            out.record_stream(main)
+            nz.record_stream(main)
+            outs.append(out)
+            shapes.append(nd)
+            pending.append((key, m3, nz))
+        for st in self._streams[:S]:
+            main.wait_stream(st)
+        try:
+            plan.check()   # synchronises; the status word is shared by the engine's plans
+        except L.OuRangeError:
+            # as enhance(): a split-f16 input left its range -> f32 operands,
+            # same noise, every clip of the call
+            self._conv_prec = 0
+            self.invalidate()
+            eng = self._get_engine()
+            outs = []
+            for key, m3, nz in pending:
+                B, _, T = m3.shape
+                p0 = self._plan(key[:-1] + (0,), lambda: EnhancePlan(eng, B, T, int(n_steps), float(epsilon),
+                                                                      keep_rms=bool(keep_rms),
+                                                                      diff=dict(self.diff_kwargs)))
+                outs.append(p0.run_with_noise(m3, nz).clone())
+        res = []
+        for x, nd in zip(outs, shapes):
+            res.append(x[0] if nd == 1 else x if nd == 2 else x[:, None, :])
+        return res
 
     @staticmethod
     def _ensemble_reduce(x, stat):

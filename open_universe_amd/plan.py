@@ -72,6 +72,7 @@ class _PlanBase:
             finally:
                 E.end_record()
                 E._LANE = 0
+                E._SLOT = 0
 
         cls.__init__ = wrapped
 
@@ -98,8 +99,12 @@ class EnhancePlan(_PlanBase):
 
     def __init__(self, eng, batch, mix_len, n_steps, epsilon, keep_rms=False,
                  use_aux_signal=False, warm_start=None, diff=None, ensemble=None,
-                 ensemble_mode=None):
+                 ensemble_mode=None, slot=0):
         super().__init__(eng)
+        # plans that may run concurrently (Universe.enhance_many) use their own
+        # K-slice workspaces: engine.conv_desc offsets by the recording slot
+        assert 0 <= slot < E.MAX_SLOTS
+        E._SLOT = slot
         dev, B = self.dev, batch
         self.B, self.mix_len, self.n_steps = B, mix_len, n_steps
         tot = eng.tot_ds
@@ -242,12 +247,18 @@ class EnhancePlan(_PlanBase):
                 torch.randn(shape, generator=rng, out=self.NZ[k])
 
     def __call__(self, mix, rng=None, use_graph=True):
+        out = self.submit(mix, rng, use_graph)
+        self.check()
+        return out
+
+    def submit(self, mix, rng=None, use_graph=True):
+        """Enqueue one enhance on the current stream without waiting for it
+        (the caller checks the status word after synchronising)."""
         assert mix.shape == (self.B, 1, self.mix_len), mix.shape
         self.MIX.copy_(mix)
         self.draw_noise(rng)
         stream = torch.cuda.current_stream(self.dev).cuda_stream
         self._launch(stream, use_graph)
-        self.check()
         return self.OUT if self.RED is None else self.RED
 
     def run_with_noise(self, mix, nz):

@@ -221,3 +221,42 @@ def test_c5_size_f16_enhance_vs_oracle():
     assert eng.conv_prec == 2 and int(eng.status.abs().sum()) == 0
     assert out.shape == ref.shape == (1, 960000)
     assert torch.isfinite(out).all() and si_sdr(out, ref) > 30
+
+
+# ------------------------------------------------ queued / variable lengths
+def test_enhance_many_equals_sequential_enhance():
+    """Two clips in flight on two streams (Universe.enhance_many) give exactly
+    the sequential enhance() results on the same noise sequence, for clips of
+    different lengths."""
+    d, cfg, m = _golden_model("pp16_c4", "pp16", 4)
+    clips = [_t(synth_audio(n, 16000, i)[0]).to(DEV) for i, n in enumerate((4000, 5200, 4000, 3333, 5200))]
+    with torch.no_grad():
+        seq = [m.enhance(c, rng=g).cpu() for g in [torch.Generator().manual_seed(5)] for c in clips]
+        many = [x.cpu() for x in m.enhance_many(clips, rng=torch.Generator().manual_seed(5), streams=2)]
+    for a, b in zip(seq, many):
+        assert a.shape == b.shape and torch.equal(a, b)
+
+
+def test_variable_lengths_bounded_plans_and_memory(monkeypatch):
+    """A stream of clips of distinct lengths (the CLI over a folder): tiles
+    are tuned once per geometry (no new tuning for new lengths), the plan LRU
+    stays bounded, and a second pass over the same lengths (every plan evicted
+    and re-recorded) allocates no more device memory than the first."""
+    monkeypatch.setenv("OUHIP_MAX_PLANS", "3")
+    cfg, m = _synth_model("pp16")
+    from open_universe_amd import engine as E
+
+    lengths = [19000, 16000, 23000, 17500, 21000, 24500] * 2   # six distinct lengths, twice
+    peaks = []
+    with torch.no_grad():
+        for i, n in enumerate(lengths):
+            out = m.enhance(_t(synth_audio(n, 16000, i)[0]).to(DEV), rng=torch.Generator().manual_seed(i))
+            assert out.shape == (n,) and torch.isfinite(out).all()
+            if i == 0:
+                timed = E._TUNER.timed
+            torch.cuda.synchronize()
+            peaks.append(torch.cuda.memory_allocated())
+    assert len(m._plans) <= 3
+    # later lengths reuse the first clip's tiles (new octave buckets copy them)
+    assert E._TUNER.timed == timed
+    assert max(peaks[6:]) <= max(peaks[:6]) * 1.05

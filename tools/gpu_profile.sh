@@ -15,12 +15,12 @@ timeout -k 10 600 python3 "$B" --steps 20 --warmup 3 --dump-ops "$O/ops_$TAG.jso
     > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err" &&
 cd /tmp &&
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt_$TAG" -o kt -- \
-    python3 "$B" --steps 5 --warmup 1 --no-cpu-baseline --no-profile --no-f32-pass > "$O/kt_bench_$TAG.json" 2> "$O/kt_$TAG.err" &&
+    python3 "$B" --steps 5 --warmup 1 --no-cpu-baseline --no-profile --no-f32-pass --no-queued > "$O/kt_bench_$TAG.json" 2> "$O/kt_$TAG.err" &&
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmcf_$TAG" -o pmc -- \
-    python3 "$B" --steps 1 --warmup 1 --no-cpu-baseline --no-profile --no-f32-pass > /dev/null 2> "$O/pmcf_$TAG.err" &&
+    python3 "$B" --steps 1 --warmup 1 --no-cpu-baseline --no-profile --no-f32-pass --no-queued > /dev/null 2> "$O/pmcf_$TAG.err" &&
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmcw_$TAG" -o pmc -- \
-    python3 "$B" --steps 1 --warmup 1 --no-cpu-baseline --no-profile --no-f32-pass > /dev/null 2> "$O/pmcw_$TAG.err" &&
-python3 "$ROOT/tools/pmc_summary.py" --tag "$TAG" --out "$O/pmc_$TAG.json" \
+    python3 "$B" --steps 1 --warmup 1 --no-cpu-baseline --no-profile --no-f32-pass --no-queued > /dev/null 2> "$O/pmcw_$TAG.err" &&
+python3 "$ROOT/tools/pmc_summary.py" --tag "$TAG" --enhances 2 --out "$O/pmc_$TAG.json" \
     "$(find "$O/pmcf_$TAG" -name '*counter_collection.csv' | head -n1)" \
     "$(find "$O/pmcw_$TAG" -name '*counter_collection.csv' | head -n1)" > /dev/null
 rc=$?

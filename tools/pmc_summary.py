@@ -43,6 +43,8 @@ def main():
     ap.add_argument("write")
     ap.add_argument("--out")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--enhances", type=int, default=None, help="enhance() calls in the profiled run")
+    ap.add_argument("--config", default="c2", help="bench.py --config of the profiled run")
     a = ap.parse_args()
     f, w = read(a.fetch, "FETCH_SIZE"), read(a.write, "WRITE_SIZE")
     rows = {}
@@ -53,7 +55,9 @@ def main():
         rows[k] = {"dispatches": n, "fetch_bytes_per_launch": round(fb),
                    "write_bytes_per_launch": round(wb),
                    "traffic_bytes_per_launch": round(fb + wb)}
-    out = {"tag": a.tag, "correction": "FETCH_SIZE x2 (gfx950), KiB->bytes", "kernels": rows}
+    out = {"tag": a.tag, "config": a.config, "correction": "FETCH_SIZE x2 (gfx950), KiB->bytes", "kernels": rows}
+    if a.enhances:
+        out["enhances_profiled"] = a.enhances
     txt = json.dumps(out, indent=1)
     print(txt)
     if a.out:
