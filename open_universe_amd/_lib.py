@@ -248,8 +248,66 @@ def conv_pack(w_logical, cc):
     return out
 
 
+def _split_scale(w):
+    """Per-layer power-of-two scale of the split packings: max|w * 2^e| in
+    [2^9, 2^10); returns (2^e, w_unscale = 2^(6 - e))."""
+    import numpy as np
+
+    if not np.isfinite(w).all():
+        raise OuHipError("split packing: non-finite weight")
+    mx = float(np.abs(w).max()) if w.size else 0.0
+    e = 0
+    if mx > 0.0:
+        e = min(100, max(-100, 10 - int(np.frexp(np.float32(mx))[1])))
+    return np.float32(2.0**e), float(2.0 ** (6 - e))
+
+
+def _hi_lo(a):
+    import numpy as np
+
+    hi = a.astype(np.float16)
+    lo = ((a - hi.astype(np.float32)) * np.float32(2048.0)).astype(np.float16)
+    return hi, lo
+
+
+def conv_pack_split_np(w_logical):
+    """ou_conv_pack_split restated with numpy array ops (byte-identical,
+    tests/test_weight_prep.py): the C loop converts to f16 in software on the
+    host and dominates model load time."""
+    import numpy as np
+
+    w = np.ascontiguousarray(w_logical, dtype=np.float32)
+    m, cin, kt = w.shape
+    sc, unscale = _split_scale(w)
+    mt = (m + 31) // 32
+    cpad = (cin + 63) // 64 * 64
+    a = np.zeros((mt * 32, cpad, kt), dtype=np.float32)
+    a[:m, :cin] = w * sc
+    # out[mt][g][part][k][lane = h*32 + r][j] = a[mt*32 + r][16 g + 2 j + h][k]
+    a = a.reshape(mt, 32, cpad // 16, 8, 2, kt).transpose(0, 2, 5, 4, 1, 3)   # mt, g, k, h, r, j
+    hi, lo = _hi_lo(np.ascontiguousarray(a))
+    out = np.stack([hi, lo], axis=2)                                           # mt, g, part, k, h, r, j
+    return np.ascontiguousarray(out).reshape(-1).view(np.float32), unscale
+
+
+def block_pack_np(w_logical):
+    """ou_block_pack restated with numpy (byte-identical): [mt][tap][ks][hi|lo]
+    [lane = h*32 + r][i] of a[mt*32 + r][16 ks + 8 h + i][tap]."""
+    import numpy as np
+
+    w = np.ascontiguousarray(w_logical, dtype=np.float32)
+    c, c2, kt = w.shape
+    assert c == c2 and c % 32 == 0, w.shape
+    sc, unscale = _split_scale(w)
+    a = (w * sc).reshape(c // 32, 32, c // 16, 2, 8, kt).transpose(0, 5, 2, 3, 1, 4)   # mt, k, ks, h, r, i
+    hi, lo = _hi_lo(np.ascontiguousarray(a))
+    out = np.stack([hi, lo], axis=3)                                                   # mt, k, ks, part, h, r, i
+    return np.ascontiguousarray(out).reshape(-1).view(np.int16), unscale
+
+
 def conv_pack_split(w_logical):
-    """Split-f16 packing (ConvDesc.prec = 1): returns (packed, w_unscale)."""
+    """Split-f16 packing (ConvDesc.prec = 1) through the C ABI: returns
+    (packed, w_unscale)."""
     import numpy as np
 
     w = np.ascontiguousarray(w_logical, dtype=np.float32)

@@ -7,7 +7,9 @@ The folder structure is kept.
 
 Differences: audio is resampled to ``model.fs`` and back on the GPU
 (``audio.resample``); only WAV is read; the model must be a local checkpoint
-(the Hugging Face hub needs the network).  Under torchrun (WORLD_SIZE > 1)
+(the Hugging Face hub needs the network).  Files are enhanced in groups of
+``--chunk`` with ``--streams`` clips in flight (Universe.enhance_many; the
+noise of each file is drawn in file order from the one seeded generator).  Under torchrun (WORLD_SIZE > 1)
 each rank enhances its share of the files on ``cuda:LOCAL_RANK``
 (``sharding.shard_utterances``, balanced by file size) -- no collectives.
 
@@ -43,6 +45,10 @@ def main(argv=None):
     parser.add_argument("--model-strict", action="store_true", help="Strict state-dict loading")
     parser.add_argument("--seed", type=int, default=1028282, help="Seed of the sampler noise")
     parser.add_argument("--device", type=str, default=None, help="cuda:X (default: cuda:LOCAL_RANK)")
+    parser.add_argument("--streams", type=int, default=2,
+                        help="clips in flight at once on separate HIP streams (Universe.enhance_many); 1 = one "
+                             "enhance() per file, as the reference")
+    parser.add_argument("--chunk", type=int, default=8, help="files read, enhanced and written per group")
     args, _ = parser.parse_known_args(argv)
 
     rank, local, world = dist_env()
@@ -65,21 +71,35 @@ def main(argv=None):
     if world > 1:
         mine = shard_utterances([p.stat().st_size for p in files], world)[rank]
         files = [files[i] for i in mine]
-    for path in files:
+    def out_path(path):
         if is_dir:
-            out = args.output / path.relative_to(root)
-        elif args.output.is_dir() or args.output.suffix == "":
-            out = args.output / path.name
-        else:
-            out = args.output
-        out.parent.mkdir(parents=True, exist_ok=True)
-        audio, fs = load_audio(path)
+            return args.output / path.relative_to(root)
+        if args.output.is_dir() or args.output.suffix == "":
+            return args.output / path.name
+        return args.output
+
+    # enhance_many covers the sampler options below; any other option (ensemble,
+    # aux signal, warm start, known-answer target) goes file by file
+    many_ok = args.streams > 1 and all(
+        enhance_kwargs.get(k) in (None, False) for k in ("target", "fake_score_snr", "use_aux_signal", "ensemble",
+                                                         "warm_start"))
+    many_kw = {k: enhance_kwargs.get(k) for k in ("n_steps", "epsilon", "keep_rms", "rng")}
+    step = max(1, args.chunk) if many_ok else 1
+    for i in range(0, len(files), step):
+        group = files[i:i + step]
+        loaded = [load_audio(p) for p in group]
         with torch.no_grad():
-            x = resample(audio.to(device), fs, model.fs)
-            enh = model.enhance(x, **enhance_kwargs)
-            enh = resample(enh, model.fs, fs)
-        save_audio(out, enh, fs)
-        print(f"[rank {rank}] {path} -> {out}", flush=True)
+            xs = [resample(a.to(device), fs, model.fs) for a, fs in loaded]
+            if many_ok:
+                ys = model.enhance_many(xs, streams=args.streams, **many_kw)
+            else:
+                ys = [model.enhance(x, **enhance_kwargs) for x in xs]
+            ys = [resample(y, model.fs, fs) for y, (_, fs) in zip(ys, loaded)]
+        for path, y, (_, fs) in zip(group, ys, loaded):
+            out = out_path(path)
+            out.parent.mkdir(parents=True, exist_ok=True)
+            save_audio(out, y, fs)
+            print(f"[rank {rank}] {path} -> {out}", flush=True)
     return 0
 
 

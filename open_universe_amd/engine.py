@@ -176,7 +176,7 @@ def make_conv(spec, device, prec=None):
             w_logical.reshape(m, spec.cin, spec.frame, kt).transpose(0, 2, 1, 3).reshape(m, cin_eff, kt))
     cc = L.conv_chunk(kt, spec.frame)
     if prec in (1, 2):   # f16 uses the hi halves of the split packing
-        packed_np, unscale = L.conv_pack_split(w_logical)
+        packed_np, unscale = L.conv_pack_split_np(w_logical)
     else:
         packed_np, unscale = L.conv_pack(w_logical, cc), 1.0
     packed = torch.from_numpy(packed_np).to(device)
@@ -307,7 +307,7 @@ def prep_fused(specs, C, prec, device):
         return None
     parts, offs, uns, off = [], [], [], 0
     for sp in specs:
-        packed, un = L.block_pack(sp.w)
+        packed, un = L.block_pack_np(sp.w)
         parts.append(packed)
         offs.append(off)
         uns.append(un)
@@ -363,8 +363,50 @@ class Act:
         self.B, self.C, self.T = t.shape
 
 
+class ArenaFull(Exception):
+    pass
+
+
+class Arena:
+    """One device buffer the plans of one slot carve their buffers from.
+
+    Every buffer of an EnhancePlan is scratch for one replay (outputs are
+    copied out right after it; constants live outside), and the plans of one
+    slot replay one after another on one stream, so all of them can start at
+    offset 0 of the same memory: a stream of clips of many lengths keeps one
+    arena sized for the largest recorded length instead of one allocation set
+    per length."""
+
+    def __init__(self, device, nbytes):
+        self.buf = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+        self.off = 0
+
+    @property
+    def nbytes(self):
+        return self.buf.numel()
+
+    def take(self, shape, dtype):
+        n = math.prod(shape) * torch.empty((), dtype=dtype).element_size()
+        off = (self.off + 255) // 256 * 256
+        if off + n > self.buf.numel():
+            raise ArenaFull(off + n)
+        self.off = off + n
+        return self.buf[off:off + n].view(dtype).view(shape)
+
+
+_ARENA = None   # set while an EnhancePlan records onto an arena
+
+
+def empty(shape, dtype=torch.float32, device=None):
+    return _ARENA.take(tuple(shape), dtype) if _ARENA is not None else torch.empty(shape, dtype=dtype, device=device)
+
+
+def zeros(shape, dtype=torch.float32, device=None):
+    return empty(shape, dtype, device).zero_()
+
+
 def new_act(B, C, T, device):
-    return Act(torch.empty((B, C, T), dtype=torch.float32, device=device))
+    return Act(empty((B, C, T), dtype=torch.float32, device=device))
 
 
 def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=None,
@@ -522,6 +564,9 @@ class ConvTuner:
         self.reps = reps
         self.path = path
         self.timed = 0   # geometries tuned by timing (not reused from another length)
+        self.by_geom = {}   # geometry -> frame-count buckets cached
+        for kk in self.cache:
+            self.by_geom.setdefault(kk[:-1], set()).add(kk[-1])
         if path and os.path.exists(path):
             with open(path) as fh:
                 self.cache = {tuple(json.loads(k)): v for k, v in json.load(fh).items()}
@@ -568,10 +613,11 @@ class ConvTuner:
         # the same geometry tuned at another length: reuse its tile (nearest
         # bucket) instead of timing every candidate again
         g, b = self.geometry(d), self.bucket(d.n_frames)
-        near = [kk for kk in self.cache if kk[:-1] == g]
+        near = self.by_geom.get(g)
         if near and os.environ.get("OUHIP_TUNE_EVERY_LENGTH", "0") != "1":
-            kk = min(near, key=lambda kk: (abs(kk[-1] - b), kk[-1]))
-            self.cache[k] = self.cache[kk]
+            bb = min(near, key=lambda x: (abs(x - b), x))
+            self.cache[k] = self.cache[g + (bb,)]
+            near.add(b)
             return self.fit_workspace(d, self.cache[k])
         lib = L.load()
         stream = torch.cuda.current_stream().cuda_stream
@@ -629,6 +675,7 @@ class ConvTuner:
         d.tile = -1
         d.status = status
         self.cache[k] = best
+        self.by_geom.setdefault(k[:-1], set()).add(k[-1])
         if os.environ.get("OUHIP_TUNE_VERBOSE", "1") != "0":   # progress (long plan builds)
             import sys
 
@@ -843,7 +890,7 @@ class Engine:
                 bufs[f"{k}{i}"] = new_act(B, Cs[li], Ts[li], dev)
         H = self.s_gru.hidden
         bufs["GI"] = new_act(B, 6 * H, Ts[len(self.rates)], dev)
-        bufs["gran"] = torch.zeros(L.load().ou_gru_workspace_bytes(H, B) // 8, dtype=torch.int64, device=dev)
+        bufs["gran"] = zeros((L.load().ou_gru_workspace_bytes(H, B) // 8,), dtype=torch.int64, device=dev)
         return bufs
 
     def score_levels(self):
@@ -942,7 +989,7 @@ class Engine:
         bufs["SPEC"] = new_act(B, 2 * self.mel_nfreq, U, dev)
         bufs["POW"] = new_act(B, self.mel_nfreq, U, dev)
         bufs["MEL"] = new_act(B, self.mel_nmels, U, dev)
-        bufs["INV"] = torch.empty(B, dtype=torch.float32, device=dev)
+        bufs["INV"] = empty((B,), dtype=torch.float32, device=dev)
         CL = Cs[-1]
         for k in ("M0", "MA", "MB", "XMEL", "SUM", "OUT", "LA", "LB", "CB1", "G1", "G2", "H", "D0", "Y4"):
             bufs[k] = new_act(B, CL, U, dev)
@@ -953,7 +1000,7 @@ class Engine:
         bufs[f"E{len(rates)}"] = new_act(B, CL, Ts[len(rates)], dev)
         H = self.c_gru.hidden
         bufs["GI"] = new_act(B, 6 * H, U, dev)
-        bufs["gran"] = torch.zeros(L.load().ou_gru_workspace_bytes(H, B) // 8, dtype=torch.int64, device=dev)
+        bufs["gran"] = zeros((L.load().ou_gru_workspace_bytes(H, B) // 8,), dtype=torch.int64, device=dev)
         # decoder: conditions per level + Y (block outputs) per level
         conds, ys = [], []
         for l in range(n_lvl):

@@ -137,6 +137,33 @@ class Universe(nn.Module):
         plan = self._plans[key] = make()
         return plan
 
+    def _arena_plan(self, key, slot, build):
+        """_plan() for an EnhancePlan recorded onto the engine's arena of
+        ``slot`` (engine.Arena): ``build(arena)`` records the plan.  An arena
+        that is too small is replaced by one of at least twice the size; the
+        plans recorded on the old one are dropped (re-recorded when used)."""
+        from ... import engine as E
+
+        eng = self._get_engine()
+        arenas = eng.__dict__.setdefault("arenas", {})
+
+        def make():
+            while True:
+                ar = arenas.get(slot)
+                if ar is None:
+                    ar = arenas[slot] = E.Arena(eng.device, 64 << 20)
+                try:
+                    return build(ar)
+                except E.ArenaFull as e:
+                    size = max(2 * ar.nbytes, int(e.args[0] * 1.5))
+                    for k in [k for k, p in self._plans.items() if getattr(p, "arena", None) is ar]:
+                        del self._plans[k]
+                    arenas[slot] = None
+                    del ar
+                    arenas[slot] = E.Arena(eng.device, size)
+
+        return self._plan(key, make)
+
     def invalidate(self):
         """Drop the packed device weights (call after changing parameters)."""
         self._engine, self._plans = None, collections.OrderedDict()
@@ -219,13 +246,13 @@ class Universe(nn.Module):
             ens_mode = {"mean": 0, "median": 1, "signal_median": 2}[ensemble_stat] if ensemble is not None else None
             key = (B, T, int(n_steps), float(epsilon), bool(keep_rms), bool(use_aux_signal),
                    warm_start, ensemble, ens_mode)
-            def make_plan(eng):
-                return EnhancePlan(eng, B, T, int(n_steps), float(epsilon), keep_rms=bool(keep_rms),
+            def make_plan(arena):
+                return EnhancePlan(self._get_engine(), B, T, int(n_steps), float(epsilon), keep_rms=bool(keep_rms),
                                    use_aux_signal=bool(use_aux_signal), warm_start=warm_start,
                                    diff=dict(self.diff_kwargs), ensemble=ensemble,
-                                   ensemble_mode=ens_mode)
+                                   ensemble_mode=ens_mode, arena=arena)
 
-            plan = self._plan(key, lambda: make_plan(eng))
+            plan = self._arena_plan(key, 0, make_plan)
             try:
                 x = plan(mix, rng).clone()[:, None, :]
             except L.OuRangeError:
@@ -234,7 +261,7 @@ class Universe(nn.Module):
                 nz = plan.NZ.clone()
                 self._conv_prec = 0
                 self.invalidate()
-                plan = self._plan(key, lambda: make_plan(self._get_engine()))
+                plan = self._arena_plan(key, 0, make_plan)
                 x = plan.run_with_noise(mix, nz).clone()[:, None, :]
         if x_ndim == 1:
             x = x[0, 0]
@@ -273,9 +300,10 @@ class Universe(nn.Module):
             B, _, T = m3.shape
             slot = i % S
             key = (B, T, int(n_steps), float(epsilon), bool(keep_rms), False, None, None, None, slot)
-            plan = self._plan(key, lambda: EnhancePlan(eng, B, T, int(n_steps), float(epsilon),
-                                                       keep_rms=bool(keep_rms), diff=dict(self.diff_kwargs),
-                                                       slot=slot))
+            plan = self._arena_plan(key, slot, lambda ar: EnhancePlan(eng, B, T, int(n_steps), float(epsilon),
+                                                                      keep_rms=bool(keep_rms),
+                                                                      diff=dict(self.diff_kwargs), slot=slot,
+                                                                      arena=ar))
             st = self._streams[slot]
             st.wait_stream(main)   # the input was produced on the caller's stream
             with torch.cuda.stream(st):
@@ -299,9 +327,10 @@ class Universe(nn.Module):
             outs = []
             for key, m3, nz in pending:
                 B, _, T = m3.shape
-                p0 = self._plan(key[:-1] + (0,), lambda: EnhancePlan(eng, B, T, int(n_steps), float(epsilon),
-                                                                      keep_rms=bool(keep_rms),
-                                                                      diff=dict(self.diff_kwargs)))
+                p0 = self._arena_plan(key[:-1] + (0,), 0,
+                                      lambda ar: EnhancePlan(eng, B, T, int(n_steps), float(epsilon),
+                                                             keep_rms=bool(keep_rms), diff=dict(self.diff_kwargs),
+                                                             arena=ar))
                 outs.append(p0.run_with_noise(m3, nz).clone())
         res = []
         for x, nd in zip(outs, shapes):

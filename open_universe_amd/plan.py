@@ -73,11 +73,16 @@ class _PlanBase:
                 E.end_record()
                 E._LANE = 0
                 E._SLOT = 0
+                E._ARENA = None
 
         cls.__init__ = wrapped
 
     def _launch(self, stream, use_graph):
-        if use_graph:
+        # a plan's first replay is eager (native launch loop); the hipGraph is
+        # captured and instantiated from its second replay on, so a plan used
+        # once (a clip of a new length) does not pay for graph instantiation
+        self.uses = getattr(self, "uses", 0) + 1
+        if use_graph and (self.uses > 1 or self.prog.captured):
             if not self.prog.captured:
                 self.prog.capture()
             self.prog.launch(stream)
@@ -99,7 +104,13 @@ class EnhancePlan(_PlanBase):
 
     def __init__(self, eng, batch, mix_len, n_steps, epsilon, keep_rms=False,
                  use_aux_signal=False, warm_start=None, diff=None, ensemble=None,
-                 ensemble_mode=None, slot=0):
+                 ensemble_mode=None, slot=0, arena=None):
+        # arena: record every buffer into this Arena (engine.Arena; the caller
+        # owns it and retries with a bigger one on ArenaFull)
+        if arena is not None:
+            arena.off = 0
+            E._ARENA = arena
+        self.arena = arena
         super().__init__(eng)
         # plans that may run concurrently (Universe.enhance_many) use their own
         # K-slice workspaces: engine.conv_desc offsets by the recording slot
@@ -125,15 +136,15 @@ class EnhancePlan(_PlanBase):
         n_start = 0 if warm_start is None else int(warm_start)
         self.n_start = n_start
         # buffers
-        self.MIX = torch.empty((B, 1, mix_len), dtype=torch.float32, device=dev)
+        self.MIX = E.empty((B, 1, mix_len), dtype=torch.float32, device=dev)
         self.XP = new_act(B, 1, Tp, dev)
         self.XN = new_act(B, 1, Tp, dev)
         self.X = new_act(B, 1, Tp, dev)
         n_noise = 0 if use_aux_signal else 1 + (n_steps - 1 - n_start)
         self.n_noise = n_noise
-        self.NZ = torch.empty((max(n_noise, 1), B, 1, Tp), dtype=torch.float32, device=dev)
-        self.OUT = torch.empty((B, mix_len), dtype=torch.float32, device=dev)
-        self.MIXRMS = torch.empty(B, dtype=torch.float32, device=dev)
+        self.NZ = E.empty((max(n_noise, 1), B, 1, Tp), dtype=torch.float32, device=dev)
+        self.OUT = E.empty((B, mix_len), dtype=torch.float32, device=dev)
+        self.MIXRMS = E.empty((B,), dtype=torch.float32, device=dev)
         cb = eng.alloc_cond(B, Tp, need_aux=use_aux_signal or warm_start is not None)
         self.cb = cb
         p = self.prog
@@ -179,8 +190,8 @@ class EnhancePlan(_PlanBase):
             snet = np.array([(f32(edm["noise"]) * sig[n]) if edm is not None else sig[n]
                              for n in range(n_steps)], dtype=np.float32)
             self.SNET = torch.from_numpy(snet).to(dev)
-            self.FILM = torch.empty((n_steps, eng.film_rows), dtype=torch.float32, device=dev)
-            self.GBUF = torch.empty((n_steps, eng.emb_dim), dtype=torch.float32, device=dev)
+            self.FILM = E.empty((n_steps, eng.film_rows), dtype=torch.float32, device=dev)
+            self.GBUF = E.empty((n_steps, eng.emb_dim), dtype=torch.float32, device=dev)
             eng.rec_embed(p, self.SNET, n_steps, self.FILM, self.GBUF)
             win = np.ones((n_steps, B), dtype=np.float32)
             coefs = []
@@ -228,9 +239,9 @@ class EnhancePlan(_PlanBase):
         if ensemble is not None and ensemble_mode is not None:
             assert B % ensemble == 0
             B0 = B // ensemble
-            self.RED = torch.empty((B0, mix_len), dtype=torch.float32, device=dev)
+            self.RED = E.empty((B0, mix_len), dtype=torch.float32, device=dev)
             # signal_median (mode 2): per-batch-item vote counts
-            self.CNT = torch.zeros((B0, 32), dtype=torch.int32, device=dev)
+            self.CNT = E.zeros((B0, 32), dtype=torch.int32, device=dev)
             p.add(L.OP_ENSEMBLE, L.EnsembleArgs(x=self.OUT.data_ptr(), y=self.RED.data_ptr(),
                                                 ensemble=ensemble, mode=ensemble_mode,
                                                 n=B0 * mix_len, batch=B0, counts=self.CNT.data_ptr()))

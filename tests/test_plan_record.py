@@ -27,3 +27,36 @@ def test_record_enhance_program(tag, name, nch, opts):
     sp = ScorePlan(eng, 1, 800)
     cp = CondPlan(eng, 1, 800)
     assert len(sp.prog) > 30 and len(cp.prog) > 30
+
+
+def test_arena_carves_aligned_views_and_reports_overflow():
+    from open_universe_amd import engine as E
+
+    ar = E.Arena("cpu", 4096)
+    a = ar.take((3, 5), torch.float32)
+    b = ar.take((7,), torch.int64)
+    assert a.shape == (3, 5) and b.shape == (7,)
+    base = ar.buf.data_ptr()   # device allocations are 256-B aligned; offsets keep that
+    assert (a.data_ptr() - base) % 256 == 0 and (b.data_ptr() - base) % 256 == 0
+    assert b.data_ptr() >= a.data_ptr() + 60
+    with pytest.raises(E.ArenaFull):
+        ar.take((1024,), torch.float32)
+    ar.off = 0   # the next plan of the slot starts over at offset 0
+    assert ar.take((3, 5), torch.float32).data_ptr() == a.data_ptr()
+
+
+def test_enhance_plan_records_onto_an_arena():
+    """All EnhancePlan buffers come from the arena when one is given; a too
+    small arena raises ArenaFull (the model then retries with a bigger one)."""
+    from open_universe_amd import engine as E
+
+    d = load_golden("pp16_c4")
+    eng = Engine(get_config("pp16", 4), golden_state_dict(d), "cpu", _record_only=True)
+    with pytest.raises(E.ArenaFull):
+        EnhancePlan(eng, 1, 3000, 8, 1.3, arena=E.Arena("cpu", 1 << 16))
+    assert E._ARENA is None
+    ar = E.Arena("cpu", 64 << 20)
+    plan = EnhancePlan(eng, 1, 3000, 8, 1.3, arena=ar)
+    lo, hi = ar.buf.data_ptr(), ar.buf.data_ptr() + ar.nbytes
+    for t in (plan.MIX, plan.NZ, plan.OUT, plan.X.t, plan.sb["E0"].t, plan.cb["SPEC"].t):
+        assert lo <= t.data_ptr() < hi

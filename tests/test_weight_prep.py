@@ -164,3 +164,34 @@ def test_resample_kernels_match_oracle():
         k2, w2, _, _ = O._sinc_resample_kernel(o, n)
         assert w == w2
         np.testing.assert_allclose(k, k2.reshape(k.shape).numpy(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("m,cin,kt", [(32, 32, 5), (64, 160, 3), (1536, 512, 1), (642, 160, 4), (50, 70, 3)])
+def test_numpy_split_packing_matches_c(m, cin, kt):
+    """The numpy restatements the engine uses are byte-identical to the C ABI
+    packers (ou_conv_pack_split, ou_block_pack)."""
+    import numpy as np
+
+    from open_universe_amd import _lib as L
+
+    g = np.random.default_rng(m + cin + kt)
+    w = (g.standard_normal((m, cin, kt)) * 0.05).astype(np.float32)
+    a, ua = L.conv_pack_split(w)
+    b, ub = L.conv_pack_split_np(w)
+    assert ua == ub and a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    if m == cin and m % 32 == 0:
+        a, ua = L.block_pack(w)
+        b, ub = L.block_pack_np(w)
+        assert ua == ub and np.array_equal(a, b)
+
+
+def test_numpy_block_packing_matches_c():
+    import numpy as np
+
+    from open_universe_amd import _lib as L
+
+    for c, kt in ((32, 5), (64, 3), (128, 5)):
+        w = (np.random.default_rng(c).standard_normal((c, c, kt)) * 0.03).astype(np.float32)
+        a, ua = L.block_pack(w)
+        b, ub = L.block_pack_np(w)
+        assert ua == ub and np.array_equal(a, b)
