@@ -66,8 +66,11 @@ constexpr int kStageShift = 6;   // activations are staged as x * 2^-6 (ou_conv'
 template <int C, int NT, int P>
 struct BCfg {
     static constexpr int MT = C / 32;              // 32-row M tiles (output channels)
-    static constexpr int WM = MT >= 4 ? 4 : MT;    // waves along M
-    static constexpr int WN = 4 / WM;              // waves along N (frames)
+    static constexpr int WAVES = 4;                // waves per workgroup (block_threads() must agree;
+                                                   // 8 waves at C = 256 measured slower: 64 vs 53 us)
+    static constexpr int NTH = 64 * WAVES;
+    static constexpr int WM = MT >= WAVES ? WAVES : MT;   // waves along M
+    static constexpr int WN = WAVES / WM;          // waves along N (frames)
     static constexpr int MR = MT / WM;             // M tiles per wave
     static constexpr int NR = NT / WN;             // N tiles per wave
     static constexpr int NF = 32 * NT;             // frames of one conv stage
@@ -83,7 +86,7 @@ struct BCfg {
     static constexpr int LDS_BYTES = 2 * (NPL * PA + NPL * PB);
     static constexpr int KS = C / 16;              // 16-channel k-steps per tap
     static constexpr int RING = MR == 1 ? 6 : 4;   // weight-fragment ring depth (k-steps)
-    static_assert(C % 32 == 0 && WM * WN == 4 && MT % WM == 0 && NT % WN == 0, "block tiling");
+    static_assert(C % 32 == 0 && WM * WN == WAVES && MT % WM == 0 && NT % WN == 0, "block tiling");
     static_assert((SX / 8) % 2 == 1, "LDS row stride must be an odd number of 16-B slots");
 };
 
@@ -176,8 +179,14 @@ __device__ __forceinline__ void split4(float x0, float x1, float x2, float x3, h
     ovf |= !(m < 32768.f);
 }
 
+template <int C>
+constexpr int block_threads()
+{
+    return C > 0 ? 256 : 0;
+}
+
 template <int C, int NT, int P, int EPI>
-__global__ __launch_bounds__(256, 2) void block_kernel(ou_block_desc d)
+__global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 : 1) void block_kernel(ou_block_desc d)
 {
     using K = BCfg<C, NT, P>;
     constexpr int MR = K::MR, NR = K::NR, F = K::F, NF = K::NF, SX = K::SX;
@@ -201,14 +210,14 @@ __global__ __launch_bounds__(256, 2) void block_kernel(ou_block_desc d)
     // loads of a thread are issued before any arithmetic.
     {
         constexpr int NI = (C / 8) * K::R1;
-        constexpr int NIT = (NI + 255) / 256;
+        constexpr int NIT = (NI + K::NTH - 1) / K::NTH;
         const float a1 = d.slope[0];
         float v[NIT][8];
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
             // out-of-range items / frames load a clamped (valid) address and
             // are zeroed afterwards: no branches around the loads
-            const int item = min(tid + 256 * it, NI - 1);
+            const int item = min(tid + K::NTH * it, NI - 1);
             const int g = item / K::R1, r = item - g * K::R1;
             const int t = t0 - 4 + r;
             const int tc = min(max(t, 0), T - 1);
@@ -222,8 +231,8 @@ __global__ __launch_bounds__(256, 2) void block_kernel(ou_block_desc d)
         }
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
-            const int item = tid + 256 * it;
-            if (NIT * 256 > NI && item >= NI) break;
+            const int item = tid + K::NTH * it;
+            if (NIT * K::NTH > NI && item >= NI) break;
             const int g = item / K::R1, r = item - g * K::R1;
             float x[8];
 #pragma unroll
@@ -308,7 +317,7 @@ __global__ __launch_bounds__(256, 2) void block_kernel(ou_block_desc d)
                 }
             }
         // rows NF, NF + 1 feed only discarded conv2 columns: keep them zero
-        for (int e = tid; e < 2 * (C / 8); e += 256) {
+        for (int e = tid; e < 2 * (C / 8); e += K::NTH) {
             _Float16* dst = xbuf + (NF + e / (C / 8)) * SX + 8 * (e % (C / 8));
             *(half8_t*)dst = half8_t{};
             if constexpr (P == 1) *(half8_t*)(dst + K::PB) = half8_t{};
@@ -349,7 +358,7 @@ __global__ __launch_bounds__(256, 2) void block_kernel(ou_block_desc d)
                     if constexpr (P == 1) *(half4_t*)(dst + K::PA) = lo;
                 }
             }
-        for (int e = tid; e < 2 * (C / 8); e += 256) {
+        for (int e = tid; e < 2 * (C / 8); e += K::NTH) {
             _Float16* dst = xa + (NF + e / (C / 8)) * SX + 8 * (e % (C / 8));
             *(half8_t*)dst = half8_t{};
             if constexpr (P == 1) *(half8_t*)(dst + K::PA) = half8_t{};
@@ -411,7 +420,7 @@ int launch(const ou_block_desc& d, hipStream_t s)
         attr = true;
     }
     dim3 grid((d.length + K::F - 1) / K::F, d.batch);
-    hipLaunchKernelGGL((block_kernel<C, NT, P, EPI>), grid, dim3(256), K::LDS_BYTES, s, d);
+    hipLaunchKernelGGL((block_kernel<C, NT, P, EPI>), grid, dim3(K::NTH), K::LDS_BYTES, s, d);
     return ou_check_launch("block");
 }
 
@@ -454,9 +463,9 @@ int launch_p(const ou_block_desc& d, hipStream_t s)
 // C = 256 (and the 512-channel bottleneck) stay on ou_conv: with one
 // workgroup owning every channel, the fused form re-streams the whole
 // 256 x 256 x 11 weight set for every 28 frames and is weight-bandwidth bound
-// (127 us against 52 us for the three ou_conv launches at 4005 frames,
-// tools/block_bench.py); at 32 / 64 / 128 channels it is 2.0x / 1.4x / 1.2x
-// faster than the unfused launches.
+// (53 us with 4 waves, 64 us with 8, against 52 us for the three ou_conv
+// launches at 4005 frames, tools/block_bench.py); at 32 / 64 / 128 channels
+// it is 2.0x / 1.4x / 1.2x faster than the unfused launches.
 extern "C" int ou_block_supported(int channels, int prec)
 {
     return (prec == 1 || prec == 2) && (channels == 32 || channels == 64 || channels == 128);
