@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 
 #include "../../include/ouhip.h"
 #include "ou_common.h"
@@ -190,6 +191,61 @@ __global__ __launch_bounds__(256) void head_kernel(ou_head_desc d)
 }
 
 // ---------------------------------------------------------------- reductions
+// One workgroup per batch item reads the whole signal (128k samples at 8 s):
+// 16-B loads with four independent partial sums per thread keep several loads
+// in flight, instead of one dependent scalar load per iteration.
+template <class F>
+__device__ float reduce_sum(const float* x, int64_t n, F f, float* red)
+{
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    const int64_t bd = blockDim.x;
+    int64_t done = 0;
+    if (((uintptr_t)x & 15) == 0) {
+        const float4* x4 = (const float4*)x;
+        const int64_t n4 = n >> 2;
+        int64_t i = threadIdx.x;
+        for (; i + 3 * bd < n4; i += 4 * bd) {
+            const float4 v0 = x4[i], v1 = x4[i + bd], v2 = x4[i + 2 * bd], v3 = x4[i + 3 * bd];
+            a0 += (f(v0.x) + f(v0.y)) + (f(v0.z) + f(v0.w));
+            a1 += (f(v1.x) + f(v1.y)) + (f(v1.z) + f(v1.w));
+            a2 += (f(v2.x) + f(v2.y)) + (f(v2.z) + f(v2.w));
+            a3 += (f(v3.x) + f(v3.y)) + (f(v3.z) + f(v3.w));
+        }
+        for (; i < n4; i += bd) {
+            const float4 v = x4[i];
+            a0 += (f(v.x) + f(v.y)) + (f(v.z) + f(v.w));
+        }
+        done = n4 << 2;
+    }
+    for (int64_t i = done + threadIdx.x; i < n; i += bd) a1 += f(x[i]);
+    return block_sum((a0 + a1) + (a2 + a3), red);
+}
+
+template <class F>
+__device__ float reduce_max(const float* x, int64_t n, F f, float* red)
+{
+    float m0 = 0.f, m1 = 0.f;
+    const int64_t bd = blockDim.x;
+    int64_t done = 0;
+    if (((uintptr_t)x & 15) == 0) {
+        const float4* x4 = (const float4*)x;
+        const int64_t n4 = n >> 2;
+        int64_t i = threadIdx.x;
+        for (; i + bd < n4; i += 2 * bd) {
+            const float4 v0 = x4[i], v1 = x4[i + bd];
+            m0 = fmaxf(m0, fmaxf(fmaxf(f(v0.x), f(v0.y)), fmaxf(f(v0.z), f(v0.w))));
+            m1 = fmaxf(m1, fmaxf(fmaxf(f(v1.x), f(v1.y)), fmaxf(f(v1.z), f(v1.w))));
+        }
+        for (; i < n4; i += bd) {
+            const float4 v = x4[i];
+            m0 = fmaxf(m0, fmaxf(fmaxf(f(v.x), f(v.y)), fmaxf(f(v.z), f(v.w))));
+        }
+        done = n4 << 2;
+    }
+    for (int64_t i = done + threadIdx.x; i < n; i += bd) m1 = fmaxf(m1, f(x[i]));
+    return block_max(fmaxf(m0, m1), red);
+}
+
 __global__ __launch_bounds__(1024) void normalize_kernel(const float* x, float* y, int64_t n,
                                                           float level, float eps)
 {
@@ -197,15 +253,9 @@ __global__ __launch_bounds__(1024) void normalize_kernel(const float* x, float* 
     const int b = blockIdx.x;
     const float* xb = x + (int64_t)b * n;
     float* yb = y + (int64_t)b * n;
-    float s = 0.f;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += xb[i];
-    const float mean = block_sum(s, red) / (float)n;
-    float ss = 0.f;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const float v = xb[i] - mean;
-        ss = fmaf(v, v, ss);
-    }
-    const float var = block_sum(ss, red) / (float)(n > 1 ? n - 1 : 1);
+    const float mean = reduce_sum(xb, n, [](float v) { return v; }, red) / (float)n;
+    const float ss = reduce_sum(xb, n, [mean](float v) { return (v - mean) * (v - mean); }, red);
+    const float var = ss / (float)(n > 1 ? n - 1 : 1);
     const float gain = level / fmaxf(sqrtf(var), eps);
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) yb[i] = (xb[i] - mean) * gain;
 }
@@ -215,10 +265,7 @@ __global__ __launch_bounds__(1024) void sumsq_kernel(const float* x, float* out,
 {
     __shared__ float red[16];
     const int b = blockIdx.x;
-    const float* xb = x + (int64_t)b * n;
-    float ss = 0.f;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) ss = fmaf(xb[i], xb[i], ss);
-    const float tot = block_sum(ss, red);
+    const float tot = reduce_sum(x + (int64_t)b * n, n, [](float v) { return v * v; }, red);
     if (threadIdx.x == 0) {
         const float rms = sqrtf(tot / denom);
         out[b] = mode == 0 ? 1.0f / fmaxf(rms, eps) : rms;
@@ -234,17 +281,11 @@ __global__ __launch_bounds__(1024) void finish_kernel(const float* x, int64_t xb
     float* yb = y + (int64_t)b * len;
     float ratio = 1.f;
     if (mix_rms) {
-        float ss = 0.f;
-        for (int i = threadIdx.x; i < len; i += blockDim.x) ss = fmaf(xb[i], xb[i], ss);
-        const float xr = fmaxf(sqrtf(block_sum(ss, red) / (float)len), 1e-5f);
+        const float ss = reduce_sum(xb, len, [](float v) { return v * v; }, red);
+        const float xr = fmaxf(sqrtf(ss / (float)len), 1e-5f);
         ratio = mix_rms[b] / xr;
     }
-    float mx = 0.f;
-    for (int i = threadIdx.x; i < len; i += blockDim.x) {
-        const float v = mix_rms ? xb[i] * ratio : xb[i];
-        mx = fmaxf(mx, fabsf(v));
-    }
-    const float peak = block_max(mx, red);
+    const float peak = reduce_max(xb, len, [ratio](float v) { return fabsf(v * ratio); }, red);
     for (int i = threadIdx.x; i < len; i += blockDim.x) {
         float v = mix_rms ? xb[i] * ratio : xb[i];
         if (peak > 1.0f) v = v / peak;
