@@ -273,7 +273,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-queued", action="store_true",
-                    help="skip the extra leg with two batch-1 enhances in flight (queued_value)")
+                    help="skip the extra leg with batch-1 enhances in flight on several streams (queued_value)")
+    ap.add_argument("--queued-streams", type=int, default=2, help="streams of the queued leg")
     ap.add_argument("--no-f32-pass", action="store_true",
                     help="skip the second timed pass with f32 conv operands (f32_value)")
     ap.add_argument("--dump-ops", default=None, help="write per-op profile rows (JSON)")
@@ -362,9 +363,10 @@ def main():
     if args.config == "c2" and not args.no_queued and not C["n_steps"]:
         seq = [clips[i % len(clips)] for i in range(args.steps)]
         with torch.no_grad():
-            model.enhance_many(seq[: max(2, args.warmup)], rng=rng, streams=2)
-            eq = timed_loop(lambda i: model.enhance_many(seq, rng=rng, streams=2), 0, 1, world, sync)
-        queued = {"streams": 2, "clips": args.steps,
+            qs = args.queued_streams
+            model.enhance_many(seq[: max(2 * qs, args.warmup)], rng=rng, streams=qs)
+            eq = timed_loop(lambda i: model.enhance_many(seq, rng=rng, streams=qs), 0, 1, world, sync)
+        queued = {"streams": qs, "clips": args.steps,
                   "value": round(world * B * args.steps * args.seconds / eq, 3),
                   "ms_per_clip": round(1000.0 * eq / args.steps, 3)}
 
@@ -411,8 +413,8 @@ def main():
         }
         if queued is not None:
             out["queued_value"] = queued["value"]
-            out["queued"] = {**queued, "note": "extra leg: the same batch-1 clips, two enhance() calls in "
-                                               "flight on two HIP streams (Universe.enhance_many)"}
+            out["queued"] = {**queued, "note": "extra leg: the same batch-1 clips, enhance() calls in flight "
+                                               "on several HIP streams (Universe.enhance_many)"}
         if f32 is not None:
             out["f32_value"] = f32["value"]
             out["f32_pass"] = {**f32, "dtype": "f32 (v_mfma_f32_32x32x2_f32 conv operands)",

@@ -62,7 +62,7 @@ _REC = None
 _LANE = 0
 _SLOT = 0
 MAX_LANES = 2
-MAX_SLOTS = 2
+MAX_SLOTS = 3
 
 
 def set_lane(prog, i):

@@ -78,16 +78,16 @@ class _PlanBase:
         cls.__init__ = wrapped
 
     def _launch(self, stream, use_graph):
-        # OUHIP_EAGER_FIRST=1: a plan's first replay is eager (native launch
-        # loop) and the hipGraph is captured from its second replay on, so a
-        # plan used once does not pay for graph instantiation.  Off by default:
-        # with it, two plans replayed concurrently on two streams
-        # (enhance_many) measured 626x instead of 832x real time (bench
-        # queued leg, profiles/bench_r02_*), i.e. their graphs serialised.
+        # A plan's first replay is eager (native launch loop) and the hipGraph is
+        # captured from its second replay on, so a plan used once (a clip of a
+        # new length) does not pay for graph instantiation (OUHIP_EAGER_FIRST=0
+        # captures at once).  The programs' capture and side-lane streams are
+        # process-wide (csrc/ou_program.hip): per-program streams had bound two
+        # callers' streams to one hardware queue and serialised them.
         self.uses = getattr(self, "uses", 0) + 1
         import os
 
-        eager_first = os.environ.get("OUHIP_EAGER_FIRST", "0") == "1"
+        eager_first = os.environ.get("OUHIP_EAGER_FIRST", "1") != "0"
         if use_graph and (self.uses > 1 or self.prog.captured or not eager_first):
             if not self.prog.captured:
                 self.prog.capture()
