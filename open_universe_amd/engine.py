@@ -898,11 +898,12 @@ class Engine:
         n = len(self.s_enc)
         return [n - 1 - l for l in range(n)]
 
-    def rec_score(self, prog, bufs, x: Act, film_base, film_bs, in_scale=0, sc_list=None, before_decoder=None):
+    def rec_score(self, prog, bufs, x: Act, film_base, film_bs, in_scale=0, sc_list=None, before_level=None):
         """ScoreNetwork.forward up to (not including) the head
         (score.py:278-290).  Returns the decoder output Act.  The encoder and
-        the bottleneck GRU do not read the conditions (score.py:284-286):
-        ``before_decoder()`` runs at the point the decoder first needs them."""
+        the bottleneck GRU do not read the conditions (score.py:284-286), and
+        decoder level l reads only condition l: ``before_level(l)`` runs right
+        before decoder level l first needs it."""
         n_lvl = len(self.s_enc)
         nr = len(self.rates)
         fb = lambda j: film_base + 4 * self.film_off[j]
@@ -920,12 +921,12 @@ class Engine:
         rec_gru(prog, self.s_gru, 0, bufs[f"V{top}"], bufs["GI"], bufs[f"V{top}"],
                 bufs["gran"], self.status, res=bufs[f"V{top}"], res_scale=NF2)
         # decoder (score.py:197-211)
-        if before_decoder is not None:
-            before_decoder()
         h = None
         for l in range(n_lvl):
             i = top - l
             bw = self.s_dec[l]
+            if before_level is not None:
+                before_level(l)
             if bw.kind == "up":
                 li = min(i, nr)
                 prog.add(L.OP_CONV, conv_desc(bw.rate_conv, h, bufs[f"V{i}"], n_frames=h.T,
@@ -1015,8 +1016,9 @@ class Engine:
         bufs["TB"] = [new_act(B, self.c_dec[l].C, Ts[min(n_lvl - 1 - l, len(rates))], dev) for l in range(n_lvl)]
         return bufs
 
-    def rec_cond(self, prog, bufs, x: Act, need_aux=False):
-        """ConditionerNetwork.forward (condition.py:346-377)."""
+    def rec_cond(self, prog, bufs, x: Act, need_aux=False, after_level=None):
+        """ConditionerNetwork.forward (condition.py:346-377).  ``after_level(l,
+        cond_l)`` runs right after decoder level l has produced its condition."""
         rates = list(self.ccfg["rate_factors"])
         nr = len(rates)
         n_lvl = len(self.c_enc)
@@ -1072,6 +1074,8 @@ class Engine:
             last = l == n_lvl - 1
             rec_block(prog, bw, h, bufs["Y"][l], None, bufs["TB"][l], cond_out=bufs["COND"][l],
                       skip_tail=last and not need_aux)
+            if after_level is not None:
+                after_level(l, bufs["COND"][l])
             h = bufs["Y"][l]
         return bufs["COND"], bufs["Y"][-1]
 

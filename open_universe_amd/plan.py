@@ -170,12 +170,22 @@ class EnhancePlan(_PlanBase):
         # lane 0 waits for them right before the first decoder.  Not with the
         # aux / warm-start paths, whose initial sample needs the conditioner.
         self.overlap = E.overlap_enabled() and not use_aux_signal and warm_start is None
-        ev_cond = None
+        ev_cond = {}
+        after_level = None
         if self.overlap:
+            # condition l is projected (signal_cond_proj) and signalled as soon
+            # as the conditioner's decoder level l has produced it: the score
+            # decoder of the first pass waits level by level
             ev_in = p.signal()
             E.set_lane(p, 1)
             p.wait(ev_in)
-        conds, yaux = eng.rec_cond(p, cb, self.XN, need_aux=use_aux_signal or warm_start is not None)
+            self.SC = eng.alloc_sc(B, Tp)
+
+            def after_level(l, cond):
+                p.add(L.OP_CONV, E.conv_desc(eng.s_sc[l], cond, self.SC[l]))
+                ev_cond[l] = p.signal()
+        conds, yaux = eng.rec_cond(p, cb, self.XN, need_aux=use_aux_signal or warm_start is not None,
+                                   after_level=after_level)
         if use_aux_signal or warm_start is not None:
             self.AUXT = new_act(B, yaux.C, Tp, dev)
             self.SIG = new_act(B, 1, Tp, dev)
@@ -186,11 +196,11 @@ class EnhancePlan(_PlanBase):
         if use_aux_signal:
             x_final = self.SIG
         else:
-            self.SC = eng.alloc_sc(B, Tp)
-            eng.rec_sc(p, conds, self.SC)
             if self.overlap:
-                ev_cond = p.signal()
                 E.set_lane(p, 0)
+            else:
+                self.SC = eng.alloc_sc(B, Tp)
+                eng.rec_sc(p, conds, self.SC)
             # FiLM parameters for every step at once (noise embedding, K7)
             steps = list(range(n_start, n_steps))
             snet = np.array([(f32(edm["noise"]) * sig[n]) if edm is not None else sig[n]
@@ -227,9 +237,9 @@ class EnhancePlan(_PlanBase):
             zi = 1
             for n in steps:
                 in_scale = self.WIN[n].data_ptr() if edm is not None else 0
-                join = (lambda: p.wait(ev_cond)) if (ev_cond is not None and n == steps[0]) else None
+                join = (lambda l: p.wait(ev_cond[l])) if (ev_cond and n == steps[0]) else None
                 h = eng.rec_score(p, self.sb, self.X, film_base + 4 * n * eng.film_rows, 0,
-                                  in_scale=in_scale, sc_list=self.SC, before_decoder=join)
+                                  in_scale=in_scale, sc_list=self.SC, before_level=join)
                 last = n == n_steps - 1
                 z_ptr = 0 if last else self.NZ[zi].data_ptr()
                 zi += 0 if last else 1
