@@ -329,6 +329,17 @@ typedef struct ou_block_desc {
     const float* res2;         /* or NULL                                        */
     int64_t r2_bstride, r2_cstride;
     int32_t* status;           /* split-f16 range flag (as ou_conv), or NULL     */
+    /* 32 channels only, the score network's ends (both optional, NULL = off):
+     * the block input is h = conv1d(in_scale[b] * x, w_in, b_in) (score
+     * input_conv, 1 -> C, k3, score.py:244-246,285) instead of reading h;
+     * and/or the block output goes through the score head (ou_head fields of
+     * `head`; head.h is ignored) instead of being stored to y.            */
+    const float* x;            /* [B][T] sampler state                           */
+    int64_t x_bstride;
+    const float* in_scale;     /* [B] or NULL                                    */
+    const float* w_in;         /* [C][3]                                         */
+    const float* b_in;         /* [C]                                            */
+    ou_head_desc head;         /* head.w == NULL: no head                        */
 } ou_block_desc;
 
 /* 1 when ou_block handles this channel count and operand precision. */

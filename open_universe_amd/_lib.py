@@ -136,6 +136,8 @@ class BlockDesc(ctypes.Structure):
         ("y", fp), ("y_bstride", c_int64), ("y_cstride", c_int64), ("s_res", c_float), ("s2", c_float),
         ("res2", fp), ("r2_bstride", c_int64), ("r2_cstride", c_int64),
         ("status", fp),
+        ("x", fp), ("x_bstride", c_int64), ("in_scale", fp), ("w_in", fp), ("b_in", fp),
+        ("head", HeadDesc),
     ]
 
 

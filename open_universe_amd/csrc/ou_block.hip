@@ -157,6 +157,19 @@ __device__ __forceinline__ void stage_mma(const half8_t* __restrict__ wp, const 
 // run-time branches): the score encoder's FiLM, the score decoder's
 // input_cond residual + FiLM, the conditioner decoder's cond_out store.
 constexpr int kEpiFilm = 1, kEpiSc = 2, kEpiCond = 4, kEpiRes2 = 8;
+// fusions at the score network's 32-channel ends: kEpiIn computes the block
+// input h = input_conv(in_scale * x) (1 -> C channels, k3, score.py:244-246,285)
+// instead of reading it; kEpiHead runs the score head (two PReLUs,
+// output_conv C -> 1 k3, EDM wrapper and sampler update, as ou_head) on the
+// block output instead of storing it.  With the head, conv3 covers one extra
+// frame on each side (the head's taps), so a workgroup owns F - 2 frames.
+constexpr int kEpiIn = 16, kEpiHead = 32;
+
+template <int C, int NT, int P, int EPI>
+constexpr int block_f()
+{
+    return BCfg<C, NT, P>::NF - 4 - ((EPI & kEpiHead) ? 2 : 0);
+}
 
 typedef float float2_t __attribute__((ext_vector_type(2)));
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
@@ -189,7 +202,9 @@ template <int C, int NT, int P, int EPI>
 __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 : 1) void block_kernel(ou_block_desc d)
 {
     using K = BCfg<C, NT, P>;
-    constexpr int MR = K::MR, NR = K::NR, F = K::F, NF = K::NF, SX = K::SX;
+    constexpr int MR = K::MR, NR = K::NR, NF = K::NF, SX = K::SX;
+    constexpr int OFF = (EPI & kEpiHead) ? 1 : 0;   // conv3 starts one frame early (head halo)
+    constexpr int F = block_f<C, NT, P, EPI>();
     constexpr float kIn = 1.f / (1 << kStageShift);
     OU_DYNAMIC_LDS(half8_t, lds8);
     _Float16* lds = (_Float16*)lds8;
@@ -204,7 +219,16 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
     const float* __restrict__ hb = d.h + (int64_t)b * d.h_bstride;
     bool ovf = false;
 
-    // ---- stage 0: PReLU1(h) * 2^-6 over frames [t0 - 4, t0 + NF + 4) -> region A.
+    // scaled input sample of the fused input conv (zero outside [0, T))
+    const float* __restrict__ xin = (EPI & kEpiIn) ? d.x + (int64_t)b * d.x_bstride : nullptr;
+    const float xsc = (EPI & kEpiIn) ? (d.in_scale ? d.in_scale[b] : 1.f) : 0.f;
+    auto xs = [&](int t) { return (t >= 0 && t < T) ? xsc * xin[t] : 0.f; };
+    auto in_conv = [&](int c, float xl, float xm, float xr) {   // conv1d(1 -> C, k3) at one frame
+        return __builtin_fmaf(d.w_in[3 * c + 2], xr,
+                              __builtin_fmaf(d.w_in[3 * c + 1], xm, __builtin_fmaf(d.w_in[3 * c], xl, d.b_in[c])));
+    };
+
+    // ---- stage 0: PReLU1(h) * 2^-6 over frames [t0 - 4 - OFF, ...) -> region A.
     // A work item is (8-channel group, frame): 8 coalesced loads (consecutive
     // lanes = consecutive frames), then one 16-B LDS write per plane.  All
     // loads of a thread are issued before any arithmetic.
@@ -219,11 +243,17 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
             // are zeroed afterwards: no branches around the loads
             const int item = min(tid + K::NTH * it, NI - 1);
             const int g = item / K::R1, r = item - g * K::R1;
-            const int t = t0 - 4 + r;
+            const int t = t0 - 4 - OFF + r;
             const int tc = min(max(t, 0), T - 1);
-            const float* src = hb + (int64_t)(8 * g) * d.h_cstride + tc;
+            if constexpr (EPI & kEpiIn) {
+                const float xl = xs(t - 1), xm = xs(t), xr = xs(t + 1);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[it][i] = src[(int64_t)i * d.h_cstride];
+                for (int i = 0; i < 8; ++i) v[it][i] = in_conv(8 * g + i, xl, xm, xr);
+            } else {
+                const float* src = hb + (int64_t)(8 * g) * d.h_cstride + tc;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[it][i] = src[(int64_t)i * d.h_cstride];
+            }
             if (t != tc || (d.dbg & 1)) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[it][i] = 0.f;
@@ -272,7 +302,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
                 if constexpr (EPI & kEpiSc) {
 #pragma unroll
                     for (int nr = 0; nr < NR; ++nr) {   // frames outside [0, T) are zeroed below
-                        const int t = min(max(t0 - 2 + (wn * NR + nr) * 32 + l32, 0), T - 1);
+                        const int t = min(max(t0 - 2 - OFF + (wn * NR + nr) * 32 + l32, 0), T - 1);
                         scv[mr][nr][r] = d.sc[(int64_t)b * d.sc_bstride + (int64_t)m * d.sc_cstride + t];
                     }
                 }
@@ -283,7 +313,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
 #pragma unroll
             for (int nr = 0; nr < NR; ++nr) {
                 const int u = (wn * NR + nr) * 32 + l32;
-                const int t = t0 - 2 + u;
+                const int t = t0 - 2 - OFF + u;
                 const bool inside = t >= 0 && t < T;
                 float o[16];
 #pragma unroll
@@ -339,7 +369,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
 #pragma unroll
             for (int nr = 0; nr < NR; ++nr) {
                 const int v_ = (wn * NR + nr) * 32 + l32;
-                const int t = t0 - 1 + v_;
+                const int t = t0 - 1 - OFF + v_;
                 const float keep = (t >= 0 && t < T) ? kIn : 0.f;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -366,7 +396,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
     }
     __syncthreads();
 
-    // ---- stage 3: conv3 (k3) over frames t0 + w, w < F -> y
+    // ---- stage 3: conv3 (k3) over frames t0 - OFF + w, w < F + 2 OFF -> y
     stage_mma<3, C, NT, P>((const half8_t*)d.w[2], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
     {
         const float un = d.w_unscale[2];
@@ -374,36 +404,100 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = row(mr, r);
-                bia[mr][r] = d.bias[2] ? d.bias[2][m] : 0.f;
+            for (int r = 0; r < 16; ++r) bia[mr][r] = d.bias[2] ? d.bias[2][row(mr, r)] : 0.f;
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+            const int w = (wn * NR + nr) * 32 + l32;
+            const int t = t0 - OFF + w;
+            const int tc = min(max(t, 0), T - 1);   // frames outside [0, T) are not stored
+            if constexpr (EPI & kEpiIn) {
+                const float xl = xs(t - 1), xm = xs(t), xr = xs(t + 1);
+#pragma unroll
+                for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) hv[mr][nr][r] = in_conv(row(mr, r), xl, xm, xr);
+            } else {
+#pragma unroll
+                for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) hv[mr][nr][r] = hb[(int64_t)row(mr, r) * d.h_cstride + tc];
+            }
+            if constexpr (EPI & kEpiRes2) {
+#pragma unroll
+                for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        rv[mr][nr][r] = d.res2[(int64_t)b * d.r2_bstride + (int64_t)row(mr, r) * d.r2_cstride + tc];
+            }
+        }
+        if constexpr (EPI & kEpiHead) {
+            // the score head on the block output: Y[w][c] = prelu2(prelu1(y))
+            // (f32, region A, zero outside [0, T)), then one thread per frame
+            __syncthreads();   // every wave is done reading region A (conv3 input)
+            float* Y = (float*)xa;
+            constexpr int YS = C + 1;
+            const ou_head_desc& hd = d.head;
+#pragma unroll
+            for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr) {
+                    const int w = (wn * NR + nr) * 32 + l32;
+                    const int t = t0 - OFF + w;
+                    const bool inside = t >= 0 && t < T && w < F + 2;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        float v = __builtin_fmaf(__builtin_fmaf(accx[mr][nr][r], 1.f / 2048.f, acc[mr][nr][r]), un,
+                                                 bia[mr][r]);
+                        v = (v + hv[mr][nr][r]) * d.s_res;
+                        v = v >= 0.f ? v : v * hd.slope1;
+                        v = v >= 0.f ? v : v * hd.slope2;
+                        if (w < F + 2) Y[w * YS + row(mr, r)] = inside ? v : 0.f;
+                    }
+                }
+            __syncthreads();
+            for (int f = tid; f < F; f += K::NTH) {
+                const int t = t0 + f;
+                if (t >= T) break;
+                float net = 0.f;
+                for (int c = 0; c < C; ++c)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) net = __builtin_fmaf(hd.w[c * 3 + k], Y[(f + k) * YS + c], net);
+                net += hd.bias;
+                const int64_t o = (int64_t)b * T + t;
+                float out;
+                if (hd.mode == 0) {
+                    out = net;
+                } else {
+                    const float x = hd.x[o];
+                    float score = net;
+                    if (hd.edm) {
+                        const float est = __fadd_rn(__fmul_rn(hd.w_skip, x), __fmul_rn(hd.w_out, net));
+                        score = __fdiv_rn(__fsub_rn(est, x), hd.s2);
+                    }
+                    out = __fadd_rn(x, __fmul_rn(hd.c_score, score));
+                    if (hd.mode == 1) out = __fadd_rn(out, __fmul_rn(hd.c_noise, __fmul_rn(hd.z[o], hd.s_next)));
+                }
+                hd.out[o] = out;
+            }
+        } else {
+            float* yb = d.y + (int64_t)b * d.y_bstride;
+#pragma unroll
+            for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
                 for (int nr = 0; nr < NR; ++nr) {
                     const int w = (wn * NR + nr) * 32 + l32;
                     const int t = t0 + w;
-                    const int tc = min(t, T - 1);   // the stores below skip t >= T
-                    hv[mr][nr][r] = hb[(int64_t)m * d.h_cstride + tc];
-                    if constexpr (EPI & kEpiRes2)
-                        rv[mr][nr][r] = d.res2[(int64_t)b * d.r2_bstride + (int64_t)m * d.r2_cstride + tc];
+                    if (w >= F || t >= T || ((d.dbg & 4) && !(d.dbg & 1024))) continue;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        float v = __builtin_fmaf(__builtin_fmaf(accx[mr][nr][r], 1.f / 2048.f, acc[mr][nr][r]), un,
+                                                 bia[mr][r]);
+                        v = (v + hv[mr][nr][r]) * d.s_res;
+                        if constexpr (EPI & kEpiRes2) v = (v + rv[mr][nr][r]) * d.s2;
+                        yb[(int64_t)row(mr, r) * d.y_cstride + t] = v;
+                    }
                 }
-            }
-        float* yb = d.y + (int64_t)b * d.y_bstride;
-#pragma unroll
-        for (int mr = 0; mr < MR; ++mr)
-#pragma unroll
-            for (int nr = 0; nr < NR; ++nr) {
-                const int w = (wn * NR + nr) * 32 + l32;
-                const int t = t0 + w;
-                if (w >= F || t >= T || ((d.dbg & 4) && !(d.dbg & 1024))) continue;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    float v = __builtin_fmaf(__builtin_fmaf(accx[mr][nr][r], 1.f / 2048.f, acc[mr][nr][r]), un,
-                                             bia[mr][r]);
-                    v = (v + hv[mr][nr][r]) * d.s_res;
-                    if constexpr (EPI & kEpiRes2) v = (v + rv[mr][nr][r]) * d.s2;
-                    yb[(int64_t)row(mr, r) * d.y_cstride + t] = v;
-                }
-            }
+        }
     }
     if (__any(ovf) && lane == 0 && d.status) atomicOr(d.status, 1);
 }
@@ -419,7 +513,8 @@ int launch(const ou_block_desc& d, hipStream_t s)
                      "block: LDS attribute");
         attr = true;
     }
-    dim3 grid((d.length + K::F - 1) / K::F, d.batch);
+    constexpr int F = block_f<C, NT, P, EPI>();
+    dim3 grid((d.length + F - 1) / F, d.batch);
     hipLaunchKernelGGL((block_kernel<C, NT, P, EPI>), grid, dim3(K::NTH), K::LDS_BYTES, s, d);
     return ou_check_launch("block");
 }
@@ -428,7 +523,7 @@ template <int C, int NT, int P>
 int launch_epi(const ou_block_desc& d, hipStream_t s)
 {
     const int epi = (d.film ? kEpiFilm : 0) | (d.sc ? kEpiSc : 0) | (d.cond_out ? kEpiCond : 0) |
-                    (d.res2 ? kEpiRes2 : 0);
+                    (d.res2 ? kEpiRes2 : 0) | (d.x ? kEpiIn : 0) | (d.head.w ? kEpiHead : 0);
     switch (epi) {
     case 0: return launch<C, NT, P, 0>(d, s);
     case kEpiFilm: return launch<C, NT, P, kEpiFilm>(d, s);
@@ -436,7 +531,15 @@ int launch_epi(const ou_block_desc& d, hipStream_t s)
     case kEpiCond: return launch<C, NT, P, kEpiCond>(d, s);
     case kEpiRes2: return launch<C, NT, P, kEpiRes2>(d, s);
     }
-    return ou_fail(-1, "block: unsupported epilogue combination %d", epi);
+    if constexpr (C == 32) {   // the score network's ends (32 channels at level 0)
+        switch (epi) {
+        case kEpiFilm | kEpiIn: return launch<C, NT, P, kEpiFilm | kEpiIn>(d, s);
+        case kEpiFilm | kEpiSc | kEpiHead: return launch<C, NT, P, kEpiFilm | kEpiSc | kEpiHead>(d, s);
+        case kEpiIn: return launch<C, NT, P, kEpiIn>(d, s);
+        case kEpiHead: return launch<C, NT, P, kEpiHead>(d, s);
+        }
+    }
+    return ou_fail(-1, "block: unsupported epilogue combination %d at %d channels", epi, C);
 }
 
 // 32-frame N tiles per workgroup, per channel count

@@ -300,6 +300,13 @@ def fuse_blocks_enabled():
     return os.environ.get("OUHIP_FUSE_BLOCKS", "1") != "0" and not split_amax_enabled()
 
 
+def fuse_ends_enabled():
+    """OUHIP_FUSE_ENDS=0 keeps the score input conv and head as their own launches."""
+    import os
+
+    return os.environ.get("OUHIP_FUSE_ENDS", "1") != "0"
+
+
 def prep_fused(specs, C, prec, device):
     """ou_block weights for a ConvBlock whose channel count one workgroup
     covers (ou_block_supported), else None."""
@@ -459,7 +466,8 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
 
 
 def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film_bs=0,
-              sc: Act = None, res2: Act = None, s2=1.0, cond_out: Act = None, skip_tail=False):
+              sc: Act = None, res2: Act = None, s2=1.0, cond_out: Act = None, skip_tail=False,
+              x_in=None, head=None):
     """ConvBlock main stage (blocks.py:393-407):
        cond_out = conv1(h); c = (cond_out + sc)/sqrt2; c = film(c); c = conv3(conv2(c));
        out = (h + c)/sqrt2 [; out = (out + res2) * s2]"""
@@ -471,19 +479,25 @@ def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film
     d2 = conv_desc(bw.conv2, c1_out, tB)
     d3 = conv_desc(bw.conv3, tB, out, res1=h, s1=NF2, res2=res2, s2=s2)
     if bw.fused is not None and out.ptr != h.ptr:
-        prog.add(L.OP_BLOCK, block_desc(bw, h, out, (d1, d2, d3), sc=sc, film=film, film_bs=film_bs,
-                                        cond_out=cond_out, res2=res2, s2=s2))
-        return
+        descs = (d1, d2, d3) + ((x_in[4],) if x_in is not None else ())
+        prog.add(L.OP_BLOCK, block_desc(bw, h, out, descs, sc=sc, film=film, film_bs=film_bs,
+                                        cond_out=cond_out, res2=res2, s2=s2,
+                                        x_in=x_in[:4] if x_in is not None else None, head=head))
+        return True
+    assert x_in is None and head is None, "input / head fusion needs the fused block"
     prog.add(L.OP_CONV, d1)
     prog.add(L.OP_CONV, d2)
     prog.add(L.OP_CONV, d3)
 
 
 def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film_bs=0, cond_out: Act = None,
-               res2: Act = None, s2=1.0):
-    """ou_block descriptor of a ConvBlock's main path; ``descs`` are the three
+               res2: Act = None, s2=1.0, x_in=None, head=None):
+    """ou_block descriptor of a ConvBlock's main path; ``descs`` are the
     equivalent ou_conv descriptors (their shape checks have run; their
-    algorithmic FLOPs and bytes -- the unfused reference ops -- are kept)."""
+    algorithmic FLOPs and bytes -- the unfused reference ops -- are kept).
+    x_in = (x Act, in_scale ptr, w_in, b_in): compute h from the score input
+    conv instead of reading it; head: an ou_head descriptor run on the block
+    output instead of storing it."""
     fw = bw.fused
     d = L.BlockDesc()
     d.h, d.h_bstride, d.h_cstride = h.ptr, h.bs, h.cs
@@ -507,7 +521,15 @@ def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film
         assert res2.C == bw.C and res2.T >= h.T and res2.ptr != out.ptr
         d.res2, d.r2_bstride, d.r2_cstride = res2.ptr, res2.bs, res2.cs
     d.status = bw.conv1.status or 0
-    d._flops = sum(x._flops for x in descs)
+    if x_in is not None:
+        xa, scale, w_in, b_in = x_in
+        assert bw.C == 32 and xa.C == 1 and xa.T == h.T and xa.B >= h.B
+        d.x, d.x_bstride, d.in_scale = xa.ptr, xa.bs, scale or 0
+        d.w_in, d.b_in = w_in.data_ptr(), b_in.data_ptr()
+    if head is not None:
+        assert bw.C == 32 and head.length == h.T and head.channels == bw.C
+        d.head = head
+    d._flops = sum(x._flops for x in descs) + (head._flops if head is not None else 0.0)
     d._bytes = sum(x._bytes for x in descs)
     return d
 
@@ -756,6 +778,13 @@ class Engine:
         rates = self.rates
         n_lvl = len(rates) + (1 if self.extra else 0)
         self.s_input = prep_plain(sd, p + ".input_conv", cfg.get("fb_kernel_size", 3), dev)
+        # raw input-conv weights for the fused first block (ou_block kEpiIn)
+        w_in = fold_weight(sd, p + ".input_conv")
+        b_in = _bias(sd, p + ".input_conv.bias")
+        self.s_in_w = torch.from_numpy(np.ascontiguousarray(w_in.reshape(w_in.shape[0], -1), np.float32)).to(dev)
+        self.s_in_b = torch.from_numpy(np.ascontiguousarray(
+            b_in if b_in is not None else np.zeros(w_in.shape[0]), np.float32)).to(dev)
+        self.s_in_fusable = w_in.shape[1] == 1 and w_in.shape[2] == 3
         self.s_enc = []
         for i in range(n_lvl):
             q = f"{p}.encoder.ds_modules.{i}"
@@ -898,22 +927,31 @@ class Engine:
         n = len(self.s_enc)
         return [n - 1 - l for l in range(n)]
 
-    def rec_score(self, prog, bufs, x: Act, film_base, film_bs, in_scale=0, sc_list=None, before_level=None):
-        """ScoreNetwork.forward up to (not including) the head
-        (score.py:278-290).  Returns the decoder output Act.  The encoder and
-        the bottleneck GRU do not read the conditions (score.py:284-286), and
+    def rec_score(self, prog, bufs, x: Act, film_base, film_bs, in_scale=0, sc_list=None, before_level=None,
+                  head=None):
+        """ScoreNetwork.forward (score.py:278-298).  The encoder and the
+        bottleneck GRU do not read the conditions (score.py:284-286), and
         decoder level l reads only condition l: ``before_level(l)`` runs right
-        before decoder level l first needs it."""
+        before decoder level l first needs it.  With ``head`` (an ou_head
+        descriptor, h unset) the head is recorded too and None is returned;
+        otherwise the decoder output Act is returned.  When the 32-channel end
+        blocks are fused, the input conv runs inside the first encoder block and
+        the head inside the last decoder block (ou_block kEpiIn / kEpiHead)."""
         n_lvl = len(self.s_enc)
         nr = len(self.rates)
         fb = lambda j: film_base + 4 * self.film_off[j]
         # input conv (score.py:244-246, 285)
-        prog.add(L.OP_CONV, conv_desc(self.s_input, x, bufs["E0"], in_scale=in_scale))
+        d_in = conv_desc(self.s_input, x, bufs["E0"], in_scale=in_scale)
+        fuse_in = (self.s_enc[0].fused is not None and self.s_enc[0].C == 32 and self.s_in_fusable
+                   and fuse_ends_enabled())
+        if not fuse_in:
+            prog.add(L.OP_CONV, d_in)
         # encoder (score.py:105-115)
         for i in range(n_lvl):
             bw = self.s_enc[i]
+            x_in = (x, in_scale, self.s_in_w, self.s_in_b, d_in) if (i == 0 and fuse_in) else None
             rec_block(prog, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
-                      film=fb(i), film_bs=film_bs)
+                      film=fb(i), film_bs=film_bs, x_in=x_in)
             if bw.kind == "down":
                 prog.add(L.OP_CONV, conv_desc(bw.rate_conv, bufs[f"V{i}"], bufs[f"E{i+1}"]))
         # bottleneck GRU, fused with the decoder's first residual add
@@ -932,9 +970,17 @@ class Engine:
                 prog.add(L.OP_CONV, conv_desc(bw.rate_conv, h, bufs[f"V{i}"], n_frames=h.T,
                                               out_len=bufs["T"][li], valid_len=bw.rate * h.T,
                                               res1=bufs[f"V{i}"], s1=NF2))
+            last = l == n_lvl - 1
+            fuse_head = (last and head is not None and bw.fused is not None and bw.C == 32
+                         and fuse_ends_enabled())
             rec_block(prog, bw, bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
-                      film=fb(n_lvl + l), film_bs=film_bs, sc=sc_list[l])
+                      film=fb(n_lvl + l), film_bs=film_bs, sc=sc_list[l], head=head if fuse_head else None)
             h = bufs[f"A{i}"]
+            if last and head is not None:
+                if not fuse_head:
+                    head.h, head.h_bstride = h.ptr, h.bs
+                    prog.add(L.OP_HEAD, head)
+                return None
         return h
 
     def rec_sc(self, prog, conds, scs):
@@ -965,10 +1011,15 @@ class Engine:
         d._flops = 2.0 * self.film_rows * self.emb_dim * n
         prog.add(L.OP_EMBED, d)
 
-    def head_desc(self, h: Act, out_ptr, B, T, mode=0, x_ptr=0, z_ptr=0, coef=None):
+    def head_desc(self, h: Optional[Act], out_ptr, B, T, mode=0, x_ptr=0, z_ptr=0, coef=None):
+        """ou_head descriptor; h = None leaves the input unset (rec_score
+        fills it in, or fuses the head into the last decoder block)."""
         d = L.HeadDesc()
-        d.h, d.h_bstride = h.ptr, h.bs
-        d.channels, d.length, d.batch, d.mode = h.C, T, B, mode
+        C = self.s_dec[-1].C
+        if h is not None:
+            d.h, d.h_bstride = h.ptr, h.bs
+            C = h.C
+        d.channels, d.length, d.batch, d.mode = C, T, B, mode
         d.slope1, d.slope2 = self.head_s1, self.head_s2
         d.w, d.bias = self.head_w.data_ptr(), self.head_b
         d.edm = 1 if self.edm is not None else 0
@@ -976,7 +1027,7 @@ class Engine:
             for k, v in coef.items():
                 setattr(d, k, float(v))
         d.x, d.z, d.out = x_ptr, z_ptr, out_ptr
-        d._flops = 2.0 * h.C * 3 * T * B
+        d._flops = 2.0 * C * 3 * T * B
         return d
 
     # -------------------------------------------------------------- conditioner

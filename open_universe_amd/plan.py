@@ -238,13 +238,13 @@ class EnhancePlan(_PlanBase):
             for n in steps:
                 in_scale = self.WIN[n].data_ptr() if edm is not None else 0
                 join = (lambda l: p.wait(ev_cond[l])) if (ev_cond and n == steps[0]) else None
-                h = eng.rec_score(p, self.sb, self.X, film_base + 4 * n * eng.film_rows, 0,
-                                  in_scale=in_scale, sc_list=self.SC, before_level=join)
                 last = n == n_steps - 1
                 z_ptr = 0 if last else self.NZ[zi].data_ptr()
                 zi += 0 if last else 1
-                p.add(L.OP_HEAD, eng.head_desc(h, self.X.ptr, B, Tp, mode=2 if last else 1,
-                                               x_ptr=self.X.ptr, z_ptr=z_ptr, coef=coefs[n]))
+                head = eng.head_desc(None, self.X.ptr, B, Tp, mode=2 if last else 1,
+                                     x_ptr=self.X.ptr, z_ptr=z_ptr, coef=coefs[n])
+                eng.rec_score(p, self.sb, self.X, film_base + 4 * n * eng.film_rows, 0,
+                              in_scale=in_scale, sc_list=self.SC, before_level=join, head=head)
             x_final = self.X
         p.add(L.OP_FINISH, L.FinishArgs(x=x_final.ptr, x_bstride=Tp, left=self.pad // 2,
                                         batch=B, len=mix_len, y=self.OUT.data_ptr(),
@@ -315,8 +315,8 @@ class ScorePlan(_PlanBase):
         p = self.prog
         eng.rec_embed(p, self.SIG, B, self.FILM, self.GBUF)
         eng.rec_sc(p, self.CIN, self.SC)
-        h = eng.rec_score(p, self.sb, self.XIN, self.FILM.data_ptr(), eng.film_rows, sc_list=self.SC)
-        p.add(L.OP_HEAD, eng.head_desc(h, self.OUT.ptr, B, T, mode=0))
+        eng.rec_score(p, self.sb, self.XIN, self.FILM.data_ptr(), eng.film_rows, sc_list=self.SC,
+                      head=eng.head_desc(None, self.OUT.ptr, B, T, mode=0))
 
     def __call__(self, x, sigma, cond, use_graph=False):
         self.XIN.t.copy_(x)

@@ -130,3 +130,31 @@ def test_block_range_flag():
     out = E.new_act(1, C, T, DEV)
     _run(bw, E.Act(h.to(DEV)), out, True)
     assert int(status[1]) == 1
+
+
+def test_score_ends_fused_equal_unfused(monkeypatch):
+    """The score input conv fused into the first encoder block and the head
+    (EDM wrapper + sampler update) fused into the last decoder block give the
+    same enhance as separate ou_conv / ou_head launches (f32 summation-order
+    level), and the fused program has fewer launches."""
+    from conftest import golden_state_dict, load_golden
+    from open_universe_amd.configs import get_config
+    from open_universe_amd.networks.universe import UniverseGAN
+
+    d = load_golden("pp16")
+    outs, nops = {}, {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("OUHIP_FUSE_ENDS", fuse)
+        cfg = get_config("pp16", None)
+        m = UniverseGAN(**{k: v for k, v in cfg.items() if k != "_target_"})
+        m.load_state_dict(golden_state_dict(d), strict=False)
+        m = m.to(DEV).eval()
+        mix = torch.from_numpy(d["enh_mix"]).to(DEV)
+        with torch.no_grad():
+            outs[fuse] = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
+            sc = m.get_score_model()(torch.from_numpy(d["score_x"]).to(DEV), torch.from_numpy(d["score_sigma"]).to(DEV),
+                                     [torch.from_numpy(d[f"cond_out{i}"]).to(DEV) for i in range(5)]).cpu()
+        nops[fuse] = len(next(iter(m._plans.values())).prog)
+        assert _rel(sc, torch.from_numpy(d["score_out"])) < 1e-4
+    assert _rel(outs["1"], outs["0"]) < 1e-5
+    assert nops["1"] < nops["0"]
