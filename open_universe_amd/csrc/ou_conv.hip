@@ -154,6 +154,121 @@ constexpr int kSplitShift = 6;
 typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
 typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
 
+// Epilogue of one wave's MR x NR accumulator tiles (scaled, K complete):
+// bias, zero-fill past valid_len, residual 1, FiLM, residual 2, the rout
+// pixel shuffle and the store.  mtb: the wave's first 32-row m-tile; ub: the
+// first output frame of its columns; slot: amax_out slot seed.
+template <int MR, int NR>
+__device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int mtb, int ub,
+                                              floatx16 (&acc)[MR][NR], int lane, int slot)
+{
+    const int h = lane >> 5, l32 = lane & 31;
+    // Branch-free: every out-of-range element gets a sentinel offset, so its
+    // buffer load returns 0 and its buffer store is dropped.  All residual
+    // loads of the tile are issued before any arithmetic, so their latency is
+    // paid once, not once per row.
+    const int M = d.m;
+    const int rout = d.rout;
+    const int cout = M / rout;
+    const int yrows = cout;
+    const int ylen = d.out_len;
+    const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)yrows * d.y_cstride * 4);
+    const __amdgpu_buffer_rsrc_t r1s = ou_rsrc(d.res1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y, d.res1 ? (int64_t)yrows * d.r1_cstride * 4 : 0);
+    const __amdgpu_buffer_rsrc_t r2s = ou_rsrc(d.res2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y, d.res2 ? (int64_t)yrows * d.r2_cstride * 4 : 0);
+    // absent operands get zero-size resources (their loads return 0): every
+    // load is unconditional -- a per-element `ptr ? load : default` makes hipcc
+    // branch around each load and drain vmcnt(0) per element
+    const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr, has_fm = d.film != nullptr;
+    // branch-free epilogue: an absent operand loads 0 and meets a unit scale
+    const float s1e = has_r1 ? d.s1 : 1.f, s2e = has_r2 ? d.s2 : 1.f, fadd = has_fm ? 0.f : 1.f;
+    const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
+    const __amdgpu_buffer_rsrc_t fs = ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y,
+                                              has_fm ? (int64_t)cout * 8 : 0);
+    float ymax = 0.f;   // max |stored y| of this wave (d.amax_out)
+#pragma unroll
+    for (int mr = 0; mr < MR; ++mr) {
+        const int mt = mtb + mr;
+        int co[16], ph[16];
+        float bias[16], fa[16], fb[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = min(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
+            ph[r] = rout > 1 ? m / cout : 0;
+            co[r] = m - ph[r] * cout;
+        }
+        // absent operands: one uniform branch around the whole group of loads
+        // (never a per-element select between a load and a default)
+        if (d.bias) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bias[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, co[r] * 4, 0, 0));
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bias[r] = 0.f;
+        }
+        if (has_fm) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                fa[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, co[r] * 4, 0, 0));
+                fb[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, (cout + co[r]) * 4, 0, 0));
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                fa[r] = 0.f;
+                fb[r] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+            const int u = ub + nr * 32 + l32;
+            int off[16];
+            float v1[16], v2[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int t = u * rout + ph[r];
+                const bool ok = m < M && u < d.n_frames && t < ylen;
+                off[r] = ok ? t : -1;   // column; row offsets differ per tensor
+            }
+            if (has_r1) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    v1[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        r1s, off[r] >= 0 ? (co[r] * (int)d.r1_cstride + off[r]) * 4 : kSentinel, 0, 0));
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v1[r] = 0.f;
+            }
+            if (has_r2) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    v2[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        r2s, off[r] >= 0 ? (co[r] * (int)d.r2_cstride + off[r]) * 4 : kSentinel, 0, 0));
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v2[r] = 0.f;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float v = acc[mr][nr][r] + bias[r];
+                if (off[r] >= d.valid_len) v = 0.f;
+                v = (v + v1[r]) * s1e;
+                v = (fa[r] + fadd) * v + fb[r];
+                v = (v + v2[r]) * s2e;
+                ymax = fmaxf(ymax, off[r] >= 0 ? fabsf(v) : 0.f);
+                __builtin_amdgcn_raw_buffer_store_b32(
+                    __float_as_uint(v), ys, off[r] >= 0 ? (co[r] * (int)d.y_cstride + off[r]) * 4 : kSentinel, 0, 0);
+            }
+        }
+    }
+    if (d.amax_out) {   // wave max, then one atomic per wave into 64 spread slots
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) ymax = fmaxf(ymax, __shfl_xor(ymax, o));
+        if (lane == 0)
+            atomicMax((unsigned int*)d.amax_out + (slot & 63), __float_as_uint(ymax));
+    }
+}
+
 //
 // K slices (tile bits 12-13, S = 2..8; for grids too small to fill the chip):
 // ksmode 1 runs the workgroups of slice ks = blockIdx.z % S over chunks
@@ -520,112 +635,199 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     }
 
     // ---- epilogue ----
-    // Branch-free: every out-of-range element gets a sentinel offset, so its
-    // buffer load returns 0 and its buffer store is dropped.  All residual
-    // loads of the tile are issued before any arithmetic, so their latency is
-    // paid once, not once per row.
-    const int M = d.m;
-    const int rout = d.rout;
-    const int cout = M / rout;
-    const int yrows = cout;
-    const int ylen = d.out_len;
-    const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)yrows * d.y_cstride * 4);
-    const __amdgpu_buffer_rsrc_t r1s = ou_rsrc(d.res1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y, d.res1 ? (int64_t)yrows * d.r1_cstride * 4 : 0);
-    const __amdgpu_buffer_rsrc_t r2s = ou_rsrc(d.res2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y, d.res2 ? (int64_t)yrows * d.r2_cstride * 4 : 0);
-    // absent operands get zero-size resources (their loads return 0): every
-    // load is unconditional -- a per-element `ptr ? load : default` makes hipcc
-    // branch around each load and drain vmcnt(0) per element
-    const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr, has_fm = d.film != nullptr;
-    // branch-free epilogue: an absent operand loads 0 and meets a unit scale
-    const float s1e = has_r1 ? d.s1 : 1.f, s2e = has_r2 ? d.s2 : 1.f, fadd = has_fm ? 0.f : 1.f;
-    const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
-    const __amdgpu_buffer_rsrc_t fs = ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y,
-                                              has_fm ? (int64_t)cout * 8 : 0);
-    float ymax = 0.f;   // max |stored y| of this wave (d.amax_out)
-#pragma unroll
-    for (int mr = 0; mr < MR; ++mr) {
-        const int mt = mt0 + wm * MR + mr;
-        int co[16], ph[16];
-        float bias[16], fa[16], fb[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int m = min(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
-            ph[r] = rout > 1 ? m / cout : 0;
-            co[r] = m - ph[r] * cout;
-        }
-        // absent operands: one uniform branch around the whole group of loads
-        // (never a per-element select between a load and a default)
-        if (d.bias) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) bias[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, co[r] * 4, 0, 0));
-        } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) bias[r] = 0.f;
-        }
-        if (has_fm) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                fa[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, co[r] * 4, 0, 0));
-                fb[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, (cout + co[r]) * 4, 0, 0));
-            }
-        } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                fa[r] = 0.f;
-                fb[r] = 0.f;
-            }
-        }
-#pragma unroll
-        for (int nr = 0; nr < NR; ++nr) {
-            const int u = n0 + wn * (32 * NR) + nr * 32 + l32;
-            int off[16];
-            float v1[16], v2[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const int t = u * rout + ph[r];
-                const bool ok = m < M && u < d.n_frames && t < ylen;
-                off[r] = ok ? t : -1;   // column; row offsets differ per tensor
-            }
-            if (has_r1) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    v1[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                        r1s, off[r] >= 0 ? (co[r] * (int)d.r1_cstride + off[r]) * 4 : kSentinel, 0, 0));
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) v1[r] = 0.f;
-            }
-            if (has_r2) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    v2[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                        r2s, off[r] >= 0 ? (co[r] * (int)d.r2_cstride + off[r]) * 4 : kSentinel, 0, 0));
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) v2[r] = 0.f;
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float v = acc[mr][nr][r] + bias[r];
-                if (off[r] >= d.valid_len) v = 0.f;
-                v = (v + v1[r]) * s1e;
-                v = (fa[r] + fadd) * v + fb[r];
-                v = (v + v2[r]) * s2e;
-                ymax = fmaxf(ymax, off[r] >= 0 ? fabsf(v) : 0.f);
-                __builtin_amdgcn_raw_buffer_store_b32(
-                    __float_as_uint(v), ys, off[r] >= 0 ? (co[r] * (int)d.y_cstride + off[r]) * 4 : kSentinel, 0, 0);
-            }
-        }
-    }
-    if (d.amax_out) {   // wave max, then one atomic per wave into 64 spread slots
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) ymax = fmaxf(ymax, __shfl_xor(ymax, o));
-        if (lane == 0)
-            atomicMax((unsigned int*)d.amax_out + ((blockIdx.x + blockIdx.y + blockIdx.z) & 63), __float_as_uint(ymax));
-    }
+    conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane,
+                          (int)(blockIdx.x + blockIdx.y + blockIdx.z));
     OU_CSTAMP(5);
     OU_CSTAMP_SAVE;
+}
+
+// ---------------------------------------------------------------------------
+// Register-streamed variant (tile bit 14; split-f16 / f16, frame 1, cin a
+// multiple of 16): for the deep, short levels (256 / 512 channels at 4005 /
+// 801 frames), where the chunked kernel above pays one L2 round trip per
+// 16-64-channel chunk and, to fill the chip, a K-slice pass plus a second
+// launch.  Here a workgroup stages its whole input window -- every input
+// channel x (32 NR + KT - 1) frames, PReLU'd and split -- into LDS once, and
+// the weights stream straight from L2 into a register ring (each A fragment
+// is read by exactly one wave: the packed ou_conv_pack_split order is already
+// lane-linear, no LDS copy).  4 waves as WM (32-row m-tiles) x WK (K halves or
+// quarters of every tap x 16-channel step), reduced through LDS in a fixed
+// order; the epilogue is conv_kernel's.
+//   X image: [frame w][h * cin/2 + p] = split(PReLU(x[2p + h][t0 + w]) 2^-6),
+//   row stride cin + 8 halves (an odd number of 16-B slots), lo plane after.
+template <int P>
+__device__ __forceinline__ void split4r(float x0, float x1, float x2, float x3, half4_t& hi, half4_t& lo, bool& ovf)
+{
+    hi = half4_t{(_Float16)x0, (_Float16)x1, (_Float16)x2, (_Float16)x3};
+    if constexpr (P == 1)
+        lo = half4_t{(_Float16)((x0 - (float)hi[0]) * 2048.f), (_Float16)((x1 - (float)hi[1]) * 2048.f),
+                     (_Float16)((x2 - (float)hi[2]) * 2048.f), (_Float16)((x3 - (float)hi[3]) * 2048.f)};
+    const float m = fmaxf(fmaxf(fabsf(x0), fabsf(x1)), fmaxf(fabsf(x2), fabsf(x3)));
+    ovf |= !(m < 32768.f);
+}
+
+template <int KT, int WM, int WK, int NR>
+struct RCfg {
+    static constexpr int BM = 32 * WM, BN = 32 * NR, W = BN + KT - 1;
+    static constexpr int RING = 8;   // weight-fragment ring depth (steps): 7 steps of MFMA hide the L2 latency
+    static constexpr int RED = (WK - 1) * WM * NR * 16 * 64;   // floats of the K-split reduction
+    static_assert(WM * WK == 4, "4 waves per workgroup");
+};
+
+// LDS bytes of the register-streamed kernel at cin input channels
+template <int KT, int WM, int WK, int NR, int P>
+int rlds_bytes(int cin)
+{
+    using R = RCfg<KT, WM, WK, NR>;
+    const int x = R::W * (cin + 8) * (P == 1 ? 2 : 1) * 2;
+    return std::max(x, R::RED * 4);
+}
+
+template <int KT, int WM, int WK, int NR, int P>
+__global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride)
+{
+    using R = RCfg<KT, WM, WK, NR>;
+    constexpr int W = R::W, D = R::RING;
+    OU_DYNAMIC_LDS(float4, lds4);
+    _Float16* xs = (_Float16*)lds4;
+    const int cin = d.cin, SX = cin + 8, HALF = cin / 2, plane = W * SX;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave % WM, wk = wave / WM;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int b = blockIdx.z;
+    const int n0 = blockIdx.x * R::BN;
+    const int mtu = blockIdx.y * WM + wm;       // this wave's m-tile (rows past M: computed, not stored)
+    const int mt = min(mtu, mtiles - 1);
+    const int diag = (d.tile >> 8) & 3;   // diagnostics (tools/conv_bench.py --rdiag): 1 no input loads, 2 no K loop
+
+    // ---- K loop: steps s = (16-channel group g, tap k), s = g * KT + k;
+    // wave wk owns steps [s0, s1).  A fragments (hi | lo) stream from the
+    // packed global order [m-tile][g][hi | lo][tap][lane][8] through a D-deep
+    // ring whose first D - 1 steps are issued before the input staging, so
+    // their L2 latency overlaps it.
+    floatx16 acc[1][NR], accx[NR];
+#pragma unroll
+    for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[0][nr][r] = 0.f, accx[nr][r] = 0.f;
+    const int NS = (cin / 16) * KT;
+    const int s0 = wk * NS / WK, s1 = (wk + 1) * NS / WK;
+    const half8_t* ap = (const half8_t*)d.w + mt * (a_mt_stride / 4) + lane;
+    half8_t ra[D][2];
+    auto load_a = [&](int s, half8_t (&dst)[2]) {
+        const int sc = min(s, s1 - 1);
+        const int g = sc / KT, k = sc - (sc / KT) * KT;
+        const half8_t* p = ap + ((int64_t)(2 * g) * KT + k) * 64;
+        dst[0] = p[0];
+        if constexpr (P == 1) dst[1] = p[KT * 64];
+    };
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j) load_a(s0 + j, ra[j]);
+    // ---- stage the input window: item = (8-channel group g, frame w); 8
+    // loads, consecutive lanes = consecutive frames; then even channels to the
+    // h = 0 half of the row, odd channels to the h = 1 half
+    const float* xb = d.x + (int64_t)b * d.x_bstride;
+    const int64_t xc = d.x_cstride;
+    const float scale = d.in_scale ? d.in_scale[b] : 1.f, slope = d.slope;
+    constexpr float xsc = 1.f / (1 << kSplitShift);
+    const int t0 = n0 - d.pad + d.shift;
+    const int in_len = d.in_len;
+    const int NI = (cin / 8) * W;
+    bool ovf = false;
+    for (int base = 0; base < NI; base += 4 * 256) {
+        float v[4][8];
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int item = min(base + tid + 256 * it, NI - 1);
+            const int g = item / W, w = item - g * W;
+            const int t = t0 + w;
+            const int tc = min(max(t, 0), in_len - 1);
+            const float* src = xb + (int64_t)(8 * g) * xc + tc;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = (diag & 1) ? 0.f : src[i * xc];
+            if (t != tc) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[it][i] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int item = base + tid + 256 * it;
+            if (item >= NI) break;
+            const int g = item / W, w = item - g * W;
+            float x[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float q = v[it][i] * scale;
+                x[i] = (q >= 0.f ? q : q * slope) * xsc;
+            }
+            half4_t he, le, ho, lo;
+            split4r<P>(x[0], x[2], x[4], x[6], he, le, ovf);
+            split4r<P>(x[1], x[3], x[5], x[7], ho, lo, ovf);
+            _Float16* dst = xs + w * SX + 4 * g;
+            *(half4_t*)dst = he;
+            *(half4_t*)(dst + HALF) = ho;
+            if constexpr (P == 1) {
+                *(half4_t*)(dst + plane) = le;
+                *(half4_t*)(dst + plane + HALF) = lo;
+            }
+        }
+    }
+    __syncthreads();
+
+    const _Float16* xp = xs + l32 * SX + h * HALF;
+    for (int s = s0; s < ((diag & 2) ? s0 : s1); s += D) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            load_a(s + j + D - 1, ra[(j + D - 1) % D]);
+            if (s + j < s1) {
+                const int st = s + j;
+                const int g = st / KT, k = st - (st / KT) * KT;
+                half8_t bq[NR], bl[NR];
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr) {
+                    const _Float16* q = xp + (nr * 32 + k) * SX + 8 * g;
+                    bq[nr] = *(const half8_t*)q;
+                    if constexpr (P == 1) bl[nr] = *(const half8_t*)(q + plane);
+                }
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr) {
+                    acc[0][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[j][0], bq[nr], acc[0][nr], 0, 0, 0);
+                    if constexpr (P == 1) {
+                        accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[j][0], bl[nr], accx[nr], 0, 0, 0);
+                        accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[j][1], bq[nr], accx[nr], 0, 0, 0);
+                    }
+                }
+            }
+        }
+    }
+    if (__any(ovf) && lane == 0 && d.status) atomicOr(d.status, 1);
+    const float su = d.w_unscale, sx = su * (1.f / 2048.f);
+#pragma unroll
+    for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            acc[0][nr][r] = P == 1 ? fmaf(accx[nr][r], sx, acc[0][nr][r] * su) : acc[0][nr][r] * su;
+
+    // ---- K-split reduction in wave order (deterministic)
+    if constexpr (WK > 1) {
+        float* red = (float*)lds4;
+        __syncthreads();   // every wave is done reading the X image
+        if (wk > 0) {
+#pragma unroll
+            for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) red[((((wk - 1) * WM + wm) * NR + nr) * 16 + r) * 64 + lane] = acc[0][nr][r];
+        }
+        __syncthreads();
+        if (wk > 0) return;
+        for (int j = 1; j < WK; ++j)
+#pragma unroll
+            for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[0][nr][r] += red[((((j - 1) * WM + wm) * NR + nr) * 16 + r) * 64 + lane];
+    }
+    conv_epilogue<1, NR>(d, b, mtu, n0, acc, lane, (int)(blockIdx.x + blockIdx.y + blockIdx.z));
 }
 
 // ---------------------------------------------------------------------------
@@ -1574,6 +1776,7 @@ int launch_w(const ou_conv_desc& d, hipStream_t s)
 }
 
 constexpr int kWsBit = 1 << 10;   // tile bit: warp-specialised persistent kernel
+constexpr int kRsBit = 1 << 14;   // tile bit: register-streamed kernel (conv_rkernel)
 constexpr int kSplitBit = 1 << 11;   // tile-query bit (LDS size, tile_ok): the split-f16 kernel
 
 template <int KT>
@@ -1605,9 +1808,53 @@ int lds_bytes_kt(int tile)
 }
 
 
+// register-streamed shapes (tile bit 14): id, WM (32-row m-tiles), WK (K parts), NR (32-frame tiles)
+#define OU_RTILES(X) X(0, 2, 2, 1) X(1, 2, 2, 2) X(2, 4, 1, 1) X(3, 1, 4, 1) X(4, 4, 1, 2) X(5, 1, 4, 2)
+[[maybe_unused]] constexpr int kNumRTiles = 6;
+
+template <int KT, int WM, int WK, int NR, int P>
+int launch_r(const ou_conv_desc& d, hipStream_t s)
+{
+    using R = RCfg<KT, WM, WK, NR>;
+    const int lds = rlds_bytes<KT, WM, WK, NR, P>(d.cin);
+    if (lds > kMaxLds)
+        return ou_fail(-2, "conv: register-streamed tile needs %d B of LDS at cin %d", lds, d.cin);
+    auto kern = conv_rkernel<KT, WM, WK, NR, P>;
+    static bool attr = false;   // opt in to the full 160 KiB once
+    if (!attr) {
+        OU_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds),
+                     "conv: LDS attribute");
+        attr = true;
+    }
+    const int mtiles = (d.m + 31) / 32;
+    const int cin_pad = (d.cin + kCinAlign - 1) / kCinAlign * kCinAlign;
+    const int64_t a_mt_stride = (int64_t)cin_pad * KT * 32;
+    dim3 grid((d.n_frames + R::BN - 1) / R::BN, (mtiles + WM - 1) / WM, d.batch);
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, d, mtiles, a_mt_stride);
+    return ou_check_launch("conv");
+}
+
+template <int KT>
+int launch_rs(const ou_conv_desc& d, int shape, hipStream_t s)
+{
+    if constexpr (KT == 1 || KT == 3 || KT == 5) {
+        switch (shape) {
+#define OU_RTILE_CASE(id, wm, wk, nr) \
+    case id: return d.prec == 1 ? launch_r<KT, wm, wk, nr, 1>(d, s) : launch_r<KT, wm, wk, nr, 2>(d, s);
+            OU_RTILES(OU_RTILE_CASE)
+#undef OU_RTILE_CASE
+        }
+        return ou_fail(-2, "conv: bad register-streamed tile %d", shape);
+    } else {
+        (void)d, (void)shape, (void)s;
+        return ou_fail(-2, "conv: no register-streamed kernel for kt %d", KT);
+    }
+}
+
 template <int KT>
 int launch_kt(const ou_conv_desc& d, int tile, int tpw, bool ws, hipStream_t s)
 {
+    if (tile & kRsBit) return launch_rs<KT>(d, tile & 0xff, s);
     if (d.prec == 1) {   // split-f16: one-tile workgroups (checked by ou_conv)
         switch (tile) {
 #define OU_TILE_CASE(id, wm, wn, wk, mr, nr, big) case id: return launch_t<KT, wm, wn, wk, mr, nr, big, 1>(d, 1, s);
@@ -1805,6 +2052,21 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     if (!d.x || !d.w || !d.y || d.m <= 0 || d.batch <= 0 || d.n_frames <= 0 || d.cin <= 0 ||
         d.frame <= 0 || d.rout <= 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0)
         return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d frame=%d)", d.m, d.rout, d.frame);
+    if (d.tile >= 0 && (d.tile & kRsBit)) {   // register-streamed kernel (bits 0-7: RTILES shape)
+        if ((d.tile & ~(kRsBit | 0x3ff)) || (d.tile & 0xff) >= kNumRTiles)
+            return ou_fail(-2, "conv: bad register-streamed tile 0x%x", d.tile);
+        if ((d.prec != 1 && d.prec != 2) || d.frame != 1 || d.cin % 16 || d.amax_in)
+            return ou_fail(-2, "conv: the register-streamed kernel needs prec 1/2, frame 1, cin %% 16 == 0, no amax_in");
+        if (!(d.w_unscale > 0.f)) return ou_fail(-1, "conv: split-f16 needs the w_unscale of ou_conv_pack_split");
+        hipStream_t rs = (hipStream_t)stream;
+        const int t = d.tile & (0xff | kRsBit);   // bits 8-9 (diagnostics) travel in d.tile
+        switch (d.kt) {
+        case 1: return OU_LAUNCH_KT(1, d, t, 1, false, rs);
+        case 3: return OU_LAUNCH_KT(3, d, t, 1, false, rs);
+        case 5: return OU_LAUNCH_KT(5, d, t, 1, false, rs);
+        }
+        return ou_fail(-2, "conv: no register-streamed kernel for kt %d", d.kt);
+    }
     // d.tile: bits 0-7 tile shape (kTiles), bits 8-9 log2(output tiles per
     // workgroup: > 1 selects the persistent kernel, shapes without split-K),
     // bit 10 the warp-specialised persistent kernel (shapes 0-12)
@@ -1858,6 +2120,8 @@ extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile_f
 extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int ou_conv_tile_ok(int kt, int tile)
 {
+    if (tile & kRsBit)   // register-streamed: shape id only; LDS (cin-dependent) checked at launch
+        return !(tile & ~(kRsBit | 0xff)) && (tile & 0xff) < kNumRTiles && (kt == 1 || kt == 3 || kt == 5);
     if (tile & kSplitBit) {   // split-f16 (d.prec = 1): one-tile workgroups, no other bits
         if (tile & ~(kSplitBit | 0xff)) return 0;
         if ((tile & 0xff) >= kNumTiles) return 0;

@@ -45,6 +45,7 @@ _PREP_PREC = None     # set by Engine while it packs its weights
 _PREP_STATUS = 0      # device int32* the split-f16 convs flag range errors into
 _PREP_KSWS = (0, 0)   # (device float*, bytes): the engine's K-slice workspace
 KSWS_BYTES = 64 << 20
+RS_BIT = 1 << 14      # ConvDesc.tile bit: the register-streamed conv kernel (conv_rkernel)
 
 # Optional per-tensor input exponents for split-f16 (OUHIP_SPLIT_AMAX=1): every
 # conv of a split engine records max |y| of what it stores (ConvDesc.amax_out,
@@ -657,6 +658,10 @@ class ConvTuner:
         if d.prec in (1, 2):
             cands = [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))
                      for k in ksl]
+            # register-streamed kernel (tile bit 14): frame-1 convs over whole
+            # input windows; ou_conv refuses the shapes whose window exceeds LDS
+            if d.frame == 1 and d.cin % 16 == 0 and not d.amax_in:
+                cands += [t | RS_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | RS_BIT)]
         elif d.amax_out:
             cands = [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t) for k in ksl]
         else:

@@ -216,3 +216,66 @@ def test_conv_f16_every_tile(geom):
             if not (1e-5 < err < 2e-3):   # f16-rounded, not f32-exact, and not wrong
                 bad.append((t, ks, err))
     assert n and not bad, bad
+
+
+RS_BIT = 1 << 14
+# (m, cin, kt, rout, T, batch): deep same-convs, the GRU input projection, a
+# transposed (rout) up-conv, rows past M and a ragged short clip
+RS_GEOMS = [
+    (512, 512, 3, 1, 801, 1),
+    (512, 512, 5, 1, 203, 2),
+    (256, 256, 3, 1, 1001, 2),
+    (1536, 512, 1, 1, 99, 1),
+    (1280, 512, 3, 5, 157, 1),
+    (96, 48, 3, 1, 77, 2),
+    (48, 80, 1, 1, 45, 1),
+]
+
+
+@pytest.mark.parametrize("geom", RS_GEOMS, ids=[str(g) for g in RS_GEOMS])
+def test_conv_register_streamed_every_shape(geom):
+    """The register-streamed kernel (tile bit 14), every shape, split-f16 and
+    f16, with the full epilogue (bias, residual 1, FiLM, residual 2, valid_len,
+    the rout pixel shuffle): equal to the chunked kernel on the same packed
+    weights up to f32 summation order."""
+    m, cin, kt, rout, T, B = geom
+    g = torch.Generator().manual_seed(m + cin + kt)
+    w = torch.randn(m, cin, kt, generator=g) * (1.0 / np.sqrt(cin * kt))
+    cout = m // rout
+    bias = torch.randn(cout, generator=g) * 0.1
+    spec = E.ConvSpec(w.numpy(), cin, 1, (kt - 1) // 2, rout, 0.25, bias.numpy())
+    x = torch.randn(B, cin, T, generator=g)
+    L_out = T * rout
+    r1 = torch.randn(B, cout, L_out, generator=g)
+    r2 = torch.randn(B, cout, L_out, generator=g)
+    film = torch.randn(B, 2 * cout, generator=g).to(DEV)
+    xa, r1a, r2a = E.Act(x.to(DEV)), E.Act(r1.to(DEV)), E.Act(r2.to(DEV))
+    lib = L.load()
+    stream = torch.cuda.current_stream().cuda_stream
+    bad, n = [], 0
+    for prec in (1, 2):
+        cw = E.make_conv(spec, DEV, prec=prec)
+
+        def run(tile):
+            y = E.new_act(B, cout, L_out, DEV)
+            d = E.conv_desc(cw, xa, y, res1=r1a, s1=0.7, film=film.data_ptr(), film_bs=2 * cout, res2=r2a,
+                            s2=0.5, n_frames=T, out_len=L_out, valid_len=L_out - 2)
+            d.tile = tile
+            rc = lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
+            torch.cuda.synchronize()
+            return rc, y.t.cpu()
+
+        rc, ref = run(-1)
+        assert rc == 0
+        for t in range(16):
+            if not lib.ou_conv_tile_ok(kt, t | RS_BIT):
+                continue
+            rc, y = run(t | RS_BIT)
+            if rc == -2:
+                continue   # input window over LDS for this shape
+            assert rc == 0, lib.ou_last_error()
+            n += 1
+            err = ((y - ref).norm() / ref.norm()).item()
+            if not err < 2e-6:
+                bad.append((prec, t, err))
+    assert n >= 6 and not bad, bad

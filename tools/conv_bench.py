@@ -33,6 +33,8 @@ LAYERS = {
     "D3": (512, 256, 5, 3, 800, 1, False),     # down-sampling conv, rate 5 (polyphase)
     "U3": (1280, 512, 1, 3, 800, 5, True),     # up-sampling conv, rate 5
     "GI": (1536, 512, 1, 1, 800, 1, False),    # GRU input projection
+    "U2": (512, 256, 1, 3, 4000, 4, True),     # up-sampling conv, rate 4 (level 3 -> 2)
+    "U1": (256, 128, 1, 3, 16000, 4, True),    # up-sampling conv, rate 4 (level 2 -> 1)
 }
 
 
@@ -75,6 +77,8 @@ def main():
     ap.add_argument("--layer", default=None)
     ap.add_argument("--tile", type=int, default=None)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rdiag", action="store_true",
+                    help="register-streamed tiles: also time without input loads (bit 8) / without the K loop (bit 9)")
     ap.add_argument("--stamps", action="store_true", help="diag library: per-phase cycles")
     ap.add_argument("--wstamps", action="store_true", help="diag library: warp-specialised kernel phases")
     ap.add_argument("--amax", action="store_true",
@@ -83,13 +87,17 @@ def main():
     dev = "cuda:0"
     stream = torch.cuda.current_stream().cuda_stream
     lib = L.load()
-    names = [a.layer] if a.layer else list(LAYERS)
+    names = a.layer.split(",") if a.layer else list(LAYERS)
     for name in names:
         d, keep = make(name, dev)
         if d.prec == 1:
             tiles = [a.tile] if a.tile is not None else [t | k for t in range(lib.ou_conv_num_tiles())
                                                           if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))
                                                           for k in (0, 1 << 12, 2 << 12, 3 << 12)]
+            if a.tile is None and d.frame == 1 and d.cin % 16 == 0:   # register-streamed kernel
+                tiles += [t | E.RS_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | E.RS_BIT)]
+                if a.rdiag:
+                    tiles += [t | v for t in tiles if t & E.RS_BIT for v in (1 << 8, 2 << 8, 3 << 8)]
         else:
             tiles = [a.tile] if a.tile is not None else [t | v for t in range(lib.ou_conv_num_tiles())
                                                           for v in (0, 1 << 8, 2 << 8, 1 << 10)
@@ -101,9 +109,12 @@ def main():
                 res.append((ms, t))
         res.sort()
         fl = d._flops
-        nm = lambda t: (f"t{t & 0xff}" + ("w" if (t >> 10) & 1 else (f"p{1 << ((t >> 8) & 3)}" if (t >> 8) & 3 else ""))
-                        + (f"k{1 << (t >> 12)}" if t >> 12 else ""))
-        line = "  ".join(f"{nm(t)}:{ms * 1e3:.1f}us" for ms, t in res[:12])
+        def nm(t):
+            if t & E.RS_BIT:
+                return f"r{t & 0xff}" + ("" if not (t >> 8) & 3 else f"d{(t >> 8) & 3}")
+            return (f"t{t & 0xff}" + ("w" if (t >> 10) & 1 else (f"p{1 << ((t >> 8) & 3)}" if (t >> 8) & 3 else ""))
+                    + (f"k{1 << (t >> 12)}" if t >> 12 else ""))
+        line = "  ".join(f"{nm(t)}:{ms * 1e3:.1f}us" for ms, t in res[:40 if a.rdiag else 12])
         print(f"{name:5s} {fl / 1e9:6.2f} GFLOP  best {nm(res[0][1])} {res[0][0] * 1e3:.1f} us "
               f"{fl / res[0][0] / 1e9:.1f} TF/s | {line}", flush=True)
         if a.amax:
