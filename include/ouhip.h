@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define OUHIP_ABI_VERSION 3
+#define OUHIP_ABI_VERSION 4
 
 int ou_abi_version(void);
 const char* ou_last_error(void);
@@ -340,6 +340,20 @@ typedef struct ou_block_desc {
     const float* w_in;         /* [C][3]                                         */
     const float* b_in;         /* [C]                                            */
     ou_head_desc head;         /* head.w == NULL: no head                        */
+    /* 32 / 64 channels (ou_block_down_supported): the encoder's strided
+     * rate-change conv (blocks.py:203-231,268-275) on the block output, which
+     * is still stored to y: e = conv(PReLU_down(y)) with stride `rate` and 2C
+     * output rows over down_kt frames of `rate` samples per output frame
+     * (down_kt 3: the anti-alias FIR folded in, frames -1, 0, +1; down_kt 1:
+     * plain), zero outside [0, length).                                     */
+    const void* w_down;        /* ou_block_pack_rect(2C, C, down_kt * rate) of
+                                  the tap-major weights (tap k * rate + phase),
+                                  or NULL: no rate-change conv                   */
+    const float* b_down;       /* [2C] or NULL                                   */
+    float slope_down, w_down_unscale;
+    int32_t rate, down_kt;
+    float* e;                  /* [B][2C][ceil(length / rate)]                   */
+    int64_t e_bstride, e_cstride;
 } ou_block_desc;
 
 /* 1 when ou_block handles this channel count and operand precision. */
@@ -352,6 +366,11 @@ int64_t ou_block_packed_halves(int channels, int kt);
  * [lane][8 halves] of a = w * 2^e (max|a| in [2^9, 2^10)); *w_unscale =
  * 2^(6 - e). */
 int ou_block_pack(const float* w, int channels, int kt, void* out, float* w_unscale);
+/* The same packing for w[m][channels][kt] (m % 32 == 0, channels % 16 == 0):
+ * the fused rate-change conv's 2C x C x (down_kt * rate) weights.            */
+int ou_block_pack_rect(const float* w, int m, int channels, int kt, void* out, float* w_unscale);
+/* 1 when ou_block fuses the rate-change conv for (channels, rate, kt, prec). */
+int ou_block_down_supported(int channels, int rate, int kt, int prec);
 int ou_block(const ou_block_desc* d, void* stream);
 
 /* ------------------------------------------------------------------------

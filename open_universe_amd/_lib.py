@@ -12,7 +12,7 @@ from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OUHIP_LIB", os.path.join(_HERE, "libouhip.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 fp = c_void_p  # device pointers are passed as integers
 
@@ -138,6 +138,8 @@ class BlockDesc(ctypes.Structure):
         ("status", fp),
         ("x", fp), ("x_bstride", c_int64), ("in_scale", fp), ("w_in", fp), ("b_in", fp),
         ("head", HeadDesc),
+        ("w_down", fp), ("b_down", fp), ("slope_down", c_float), ("w_down_unscale", c_float),
+        ("rate", c_int32), ("down_kt", c_int32), ("e", fp), ("e_bstride", c_int64), ("e_cstride", c_int64),
     ]
 
 
@@ -181,6 +183,8 @@ EXPORTS = {
     "ou_block_frames": (c_int, [c_int]),
     "ou_block_packed_halves": (c_int64, [c_int, c_int]),
     "ou_block_pack": (c_int, [POINTER(c_float), c_int, c_int, c_void_p, POINTER(c_float)]),
+    "ou_block_pack_rect": (c_int, [POINTER(c_float), c_int, c_int, c_int, c_void_p, POINTER(c_float)]),
+    "ou_block_down_supported": (c_int, [c_int, c_int, c_int, c_int]),
     "ou_block": (c_int, [POINTER(BlockDesc), c_void_p]),
     "ou_resample": (c_int, [fp, c_int64, fp, c_int64, c_int, c_int, c_int, fp, c_int, c_int, c_int, c_int,
                             c_void_p]),
@@ -298,10 +302,10 @@ def block_pack_np(w_logical):
     import numpy as np
 
     w = np.ascontiguousarray(w_logical, dtype=np.float32)
-    c, c2, kt = w.shape
-    assert c == c2 and c % 32 == 0, w.shape
+    m, c, kt = w.shape
+    assert m % 32 == 0 and c % 16 == 0, w.shape
     sc, unscale = _split_scale(w)
-    a = (w * sc).reshape(c // 32, 32, c // 16, 2, 8, kt).transpose(0, 5, 2, 3, 1, 4)   # mt, k, ks, h, r, i
+    a = (w * sc).reshape(m // 32, 32, c // 16, 2, 8, kt).transpose(0, 5, 2, 3, 1, 4)   # mt, k, ks, h, r, i
     hi, lo = _hi_lo(np.ascontiguousarray(a))
     out = np.stack([hi, lo], axis=3)                                                   # mt, k, ks, part, h, r, i
     return np.ascontiguousarray(out).reshape(-1).view(np.int16), unscale
@@ -324,17 +328,17 @@ def conv_pack_split(w_logical):
 
 
 def block_pack(w_logical):
-    """Fused-block packing of one C x C x kt conv: returns (packed f16 as an
-    int16 numpy array, w_unscale)."""
+    """Fused-block packing of one m x C x kt conv (ou_block_pack_rect; m = C
+    for the block's own convs): returns (packed f16 as an int16 numpy array,
+    w_unscale)."""
     import numpy as np
 
     w = np.ascontiguousarray(w_logical, dtype=np.float32)
-    c, c2, kt = w.shape
-    assert c == c2, w.shape
-    out = np.empty(load().ou_block_packed_halves(c, kt), dtype=np.int16)
+    m, c, kt = w.shape
+    out = np.empty(2 * m * c * kt, dtype=np.int16)
     un = c_float(0.0)
-    check(load().ou_block_pack(w.ctypes.data_as(POINTER(c_float)), c, kt, out.ctypes.data, ctypes.byref(un)),
-          "block_pack")
+    check(load().ou_block_pack_rect(w.ctypes.data_as(POINTER(c_float)), m, c, kt, out.ctypes.data,
+                                    ctypes.byref(un)), "block_pack")
     return out, float(un.value)
 
 

@@ -164,10 +164,28 @@ constexpr int kEpiFilm = 1, kEpiSc = 2, kEpiCond = 4, kEpiRes2 = 8;
 // block output instead of storing it.  With the head, conv3 covers one extra
 // frame on each side (the head's taps), so a workgroup owns F - 2 frames.
 constexpr int kEpiIn = 16, kEpiHead = 32;
+// kEpiDown: the encoder's strided rate-change conv (blocks.py:203-231,268-275)
+// as a fourth MFMA stage on the block output, which is still stored: e =
+// conv(PReLU(y)), stride R, 2C rows, KF frames of R samples per output frame
+// (KF = 3: the anti-alias FIR folded in, centred; KF = 1: plain).  conv3 then
+// covers the conv's sample halo (R (KF-1)/2 on each side) and a workgroup owns
+// a multiple of R frames.
+constexpr int kEpiDown = 64;
 
-template <int C, int NT, int P, int EPI>
+// conv3 frames before t0 (the halo of whatever consumes the block output)
+template <int EPI, int R, int KF>
+constexpr int block_off()
+{
+    return (EPI & kEpiHead) ? 1 : (EPI & kEpiDown) ? R * ((KF - 1) / 2) : 0;
+}
+
+template <int C, int NT, int P, int EPI, int R = 1, int KF = 1>
 constexpr int block_f()
 {
+    if constexpr (EPI & kEpiDown) {
+        constexpr int halo = 2 * R * ((KF - 1) / 2);
+        return (BCfg<C, NT, P>::NF - 4 - halo) / R * R;
+    }
     return BCfg<C, NT, P>::NF - 4 - ((EPI & kEpiHead) ? 2 : 0);
 }
 
@@ -192,19 +210,77 @@ __device__ __forceinline__ void split4(float x0, float x1, float x2, float x3, h
     ovf |= !(m < 32768.f);
 }
 
+// kEpiDown's fourth stage: e = conv(PReLU_down(y)) over region A (rows w <->
+// frames t0 - OFF + w, split like every stage input).  Output frame
+// t0 / R + u reads rows u R + j, j < KF R (tap j = k R + phase of the tap-major
+// packed weights, ou_block_pack of [2C][C][KF R]).  2C / 32 x ceil(F / R / 32)
+// 32 x 32 tiles, dealt over the 4 waves.
+template <int C, int P, int R, int KF, int F, int SX>
+__device__ __forceinline__ void down_stage(const ou_block_desc& d, const _Float16* xa, int pstride, int t0, int T,
+                                           int b, int wave, int lane)
+{
+    constexpr int KT = KF * R, KS = C / 16, NS = KT * KS;
+    constexpr int M4 = 2 * C / 32, NU = F / R, N4 = (NU + 31) / 32;
+    constexpr int D = NS < 6 ? NS : 6;
+    const int l32 = lane & 31, h = lane >> 5;
+    const half8_t* wp = (const half8_t*)d.w_down;
+    const int TE = (T + R - 1) / R;
+    const int e0 = t0 / R;
+    const float un = d.w_down_unscale;
+    for (int tile = wave; tile < M4 * N4; tile += 4) {
+        const int m4 = tile % M4, n4 = tile / M4;
+        const int u = n4 * 32 + l32;
+        const _Float16* xb = xa + (u < NU ? u * R : 0) * SX + 8 * h;
+        floatx16 acc, accx;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f, accx[r] = 0.f;
+        half8_t ra[D][2];
+        auto load_a = [&](int s, half8_t (&dst)[2]) {
+            const int k = s / KS, ks = s - (s / KS) * KS;
+            const half8_t* p = wp + (((int64_t)(m4 * KT + k) * KS + ks) * 2) * 64 + lane;
+            dst[0] = p[0];
+            if constexpr (P == 1) dst[1] = p[64];
+        };
+#pragma unroll
+        for (int s = 0; s < D - 1; ++s) load_a(s, ra[s]);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (s + D - 1 < NS) load_a(s + D - 1, ra[(s + D - 1) % D]);
+            const int k = s / KS, ks = s - (s / KS) * KS;
+            const _Float16* q = xb + k * SX + 16 * ks;
+            const half8_t bq = *(const half8_t*)q;
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][0], bq, acc, 0, 0, 0);
+            if constexpr (P == 1) {
+                const half8_t bl = *(const half8_t*)(q + pstride);
+                accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][0], bl, accx, 0, 0, 0);
+                accx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][1], bq, accx, 0, 0, 0);
+            }
+        }
+        const int te = e0 + u;
+        if (u >= NU || te >= TE) continue;
+        float* eb = d.e + (int64_t)b * d.e_bstride + te;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = m4 * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float bias = d.b_down ? d.b_down[m] : 0.f;
+            eb[(int64_t)m * d.e_cstride] = __builtin_fmaf(__builtin_fmaf(accx[r], 1.f / 2048.f, acc[r]), un, bias);
+        }
+    }
+}
+
 template <int C>
 constexpr int block_threads()
 {
     return C > 0 ? 256 : 0;
 }
 
-template <int C, int NT, int P, int EPI>
+template <int C, int NT, int P, int EPI, int R = 1, int KF = 1>
 __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 : 1) void block_kernel(ou_block_desc d)
 {
     using K = BCfg<C, NT, P>;
     constexpr int MR = K::MR, NR = K::NR, NF = K::NF, SX = K::SX;
-    constexpr int OFF = (EPI & kEpiHead) ? 1 : 0;   // conv3 starts one frame early (head halo)
-    constexpr int F = block_f<C, NT, P, EPI>();
+    constexpr int OFF = block_off<EPI, R, KF>();   // conv3 starts OFF frames before t0
+    constexpr int F = block_f<C, NT, P, EPI, R, KF>();
     constexpr float kIn = 1.f / (1 << kStageShift);
     OU_DYNAMIC_LDS(half8_t, lds8);
     _Float16* lds = (_Float16*)lds8;
@@ -481,49 +557,112 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
             }
         } else {
             float* yb = d.y + (int64_t)b * d.y_bstride;
+            // kEpiDown: PReLU_down(y) 2^-6 also goes to region A (split), rows
+            // w <-> frames t0 - OFF + w, zero outside [0, T) and past the rows
+            // the strided conv reads
+            if constexpr (EPI & kEpiDown) __syncthreads();   // every wave is done reading region A
+            const float ad = (EPI & kEpiDown) ? d.slope_down : 0.f;
 #pragma unroll
             for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
                 for (int nr = 0; nr < NR; ++nr) {
                     const int w = (wn * NR + nr) * 32 + l32;
-                    const int t = t0 + w;
-                    if (w >= F || t >= T || ((d.dbg & 4) && !(d.dbg & 1024))) continue;
+                    const int t = t0 - OFF + w;
+                    const bool own = w >= OFF && w < OFF + F && t < T && !((d.dbg & 4) && !(d.dbg & 1024));
+                    float vv[16];
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
                         float v = __builtin_fmaf(__builtin_fmaf(accx[mr][nr][r], 1.f / 2048.f, acc[mr][nr][r]), un,
                                                  bia[mr][r]);
                         v = (v + hv[mr][nr][r]) * d.s_res;
                         if constexpr (EPI & kEpiRes2) v = (v + rv[mr][nr][r]) * d.s2;
-                        yb[(int64_t)row(mr, r) * d.y_cstride + t] = v;
+                        vv[r] = v;
+                        if (own) yb[(int64_t)row(mr, r) * d.y_cstride + t] = v;
+                    }
+                    if constexpr (EPI & kEpiDown) {
+                        constexpr int RH = R * (KF - 1 - (KF - 1) / 2);
+                        const float keep = (t >= 0 && t < T && w < F + OFF + RH) ? kIn : 0.f;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            float x[4];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const float q = vv[4 * j + i];
+                                x[i] = (q >= 0.f ? keep : ad * keep) * q;
+                            }
+                            half4_t hi, lo;
+                            split4<P>(x[0], x[1], x[2], x[3], hi, lo, ovf);
+                            _Float16* dst = xa + w * SX + (wm * MR + mr) * 32 + 8 * j + 4 * h;
+                            *(half4_t*)dst = hi;
+                            if constexpr (P == 1) *(half4_t*)(dst + K::PA) = lo;
+                        }
                     }
                 }
+            if constexpr (EPI & kEpiDown) {
+                __syncthreads();
+                down_stage<C, P, R, KF, F, SX>(d, xa, K::PA, t0, T, b, wave, lane);
+            }
         }
     }
     if (__any(ovf) && lane == 0 && d.status) atomicOr(d.status, 1);
 }
 
-template <int C, int NT, int P, int EPI>
+template <int C, int NT, int P, int EPI, int R = 1, int KF = 1>
 int launch(const ou_block_desc& d, hipStream_t s)
 {
     using K = BCfg<C, NT, P>;
     static bool attr = false;
     if (!attr) {
-        OU_HIP_CHECK(hipFuncSetAttribute((const void*)block_kernel<C, NT, P, EPI>,
+        OU_HIP_CHECK(hipFuncSetAttribute((const void*)block_kernel<C, NT, P, EPI, R, KF>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS_BYTES),
                      "block: LDS attribute");
         attr = true;
     }
-    constexpr int F = block_f<C, NT, P, EPI>();
+    constexpr int F = block_f<C, NT, P, EPI, R, KF>();
+    static_assert(F > 0 && F % R == 0, "block: frames per workgroup");
     dim3 grid((d.length + F - 1) / F, d.batch);
-    hipLaunchKernelGGL((block_kernel<C, NT, P, EPI>), grid, dim3(K::NTH), K::LDS_BYTES, s, d);
+    hipLaunchKernelGGL((block_kernel<C, NT, P, EPI, R, KF>), grid, dim3(K::NTH), K::LDS_BYTES, s, d);
     return ou_check_launch("block");
+}
+
+// rate-change variants instantiated (PP16 / ORIG16 encoders: rates 2 and 4
+// at 32 and 64 channels; the score encoder folds the FIR, KF = 3, the
+// conditioner's does not, KF = 1).  Every workgroup streams the stage's
+// 2C x C x KF R weights for its F / R output frames: at 64 channels with the
+// folded FIR (393 KB for 13 frames) that stream costs more than the separate
+// launch saves (score encoder level 1: 70 -> 82 us per block with 60-frame
+// windows, 77-92 us with 116-frame ones), so that variant stays unfused.
+constexpr bool down_ok(int C, int rate, int kt)
+{
+    return (C == 32 && rate == 2 && (kt == 3 || kt == 1)) || (C == 64 && rate == 4 && kt == 1);
+}
+
+template <int C, int NT, int P, int EPI>
+int launch_down(const ou_block_desc& d, hipStream_t s)
+{
+    if constexpr (C == 32) {
+        if (d.rate == 2 && d.down_kt == 3) return launch<C, NT, P, EPI, 2, 3>(d, s);
+        if (d.rate == 2 && d.down_kt == 1) return launch<C, NT, P, EPI, 2, 1>(d, s);
+    } else if constexpr (C == 64) {
+        if (d.rate == 4 && d.down_kt == 1) return launch<C, NT, P, EPI, 4, 1>(d, s);
+    }
+    return ou_fail(-1, "block: no fused rate-change conv for %d channels, rate %d, kt %d", C, d.rate, d.down_kt);
 }
 
 template <int C, int NT, int P>
 int launch_epi(const ou_block_desc& d, hipStream_t s)
 {
     const int epi = (d.film ? kEpiFilm : 0) | (d.sc ? kEpiSc : 0) | (d.cond_out ? kEpiCond : 0) |
-                    (d.res2 ? kEpiRes2 : 0) | (d.x ? kEpiIn : 0) | (d.head.w ? kEpiHead : 0);
+                    (d.res2 ? kEpiRes2 : 0) | (d.x ? kEpiIn : 0) | (d.head.w ? kEpiHead : 0) |
+                    (d.w_down ? kEpiDown : 0);
+    if constexpr (C == 32 || C == 64) {   // encoder blocks with their rate-change conv
+        switch (epi) {
+        case kEpiDown: return launch_down<C, NT, P, kEpiDown>(d, s);
+        case kEpiFilm | kEpiDown: return launch_down<C, NT, P, kEpiFilm | kEpiDown>(d, s);
+        }
+        if constexpr (C == 32)
+            if (epi == (kEpiFilm | kEpiIn | kEpiDown)) return launch_down<C, NT, P, kEpiFilm | kEpiIn | kEpiDown>(d, s);
+    }
     switch (epi) {
     case 0: return launch<C, NT, P, 0>(d, s);
     case kEpiFilm: return launch<C, NT, P, kEpiFilm>(d, s);
@@ -574,6 +713,11 @@ extern "C" int ou_block_supported(int channels, int prec)
     return (prec == 1 || prec == 2) && (channels == 32 || channels == 64 || channels == 128);
 }
 
+extern "C" int ou_block_down_supported(int channels, int rate, int kt, int prec)
+{
+    return ou_block_supported(channels, prec) && down_ok(channels, rate, kt);
+}
+
 extern "C" int ou_block_frames(int channels)
 {
     switch (channels) {
@@ -592,10 +736,15 @@ extern "C" int64_t ou_block_packed_halves(int channels, int kt)
 
 extern "C" int ou_block_pack(const float* w, int channels, int kt, void* out, float* w_unscale)
 {
-    if (!w || !out || !w_unscale || channels <= 0 || channels % 32 || kt <= 0)
+    return ou_block_pack_rect(w, channels, channels, kt, out, w_unscale);
+}
+
+extern "C" int ou_block_pack_rect(const float* w, int m, int channels, int kt, void* out, float* w_unscale)
+{
+    if (!w || !out || !w_unscale || m <= 0 || m % 32 || channels <= 0 || channels % 16 || kt <= 0)
         return ou_fail(-1, "block_pack: bad arguments");
-    const int C = channels, KS = C / 16, MT = C / 32;
-    const int64_t n = (int64_t)C * C * kt;
+    const int C = channels, KS = C / 16, MT = m / 32;
+    const int64_t n = (int64_t)m * C * kt;
     float mx = 0.f;
     for (int64_t i = 0; i < n; ++i) {
         if (!std::isfinite(w[i])) return ou_fail(-1, "block_pack: non-finite weight at %lld", (long long)i);

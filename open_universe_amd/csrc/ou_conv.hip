@@ -666,6 +666,8 @@ __device__ __forceinline__ void split4r(float x0, float x1, float x2, float x3, 
     ovf |= !(m < 32768.f);
 }
 
+constexpr int kStageItems = 9;   // conv_rkernel: staging items (8 channels x 1 frame) per thread per round trip
+
 template <int KT, int WM, int WK, int NR>
 struct RCfg {
     static constexpr int BM = 32 * WM, BN = 32 * NR, W = BN + KT - 1;
@@ -734,10 +736,13 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     const int in_len = d.in_len;
     const int NI = (cin / 8) * W;
     bool ovf = false;
-    for (int base = 0; base < NI; base += 4 * 256) {
-        float v[4][8];
+    // up to kStageItems items per thread in flight at once: the window is one
+    // L2 / HBM round trip for cin * W <= 8 * 256 * kStageItems
+    constexpr int IPT = kStageItems;
+    for (int base = 0; base < NI; base += IPT * 256) {
+        float v[IPT][8];
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
+        for (int it = 0; it < IPT; ++it) {
             const int item = min(base + tid + 256 * it, NI - 1);
             const int g = item / W, w = item - g * W;
             const int t = t0 + w;
@@ -751,7 +756,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
             }
         }
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
+        for (int it = 0; it < IPT; ++it) {
             const int item = base + tid + 256 * it;
             if (item >= NI) break;
             const int g = item / W, w = item - g * W;
@@ -776,27 +781,32 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     __syncthreads();
 
     const _Float16* xp = xs + l32 * SX + h * HALF;
-    for (int s = s0; s < ((diag & 2) ? s0 : s1); s += D) {
+    // branch-free blocks of D steps: steps past s1 (the last block's padding)
+    // multiply a zeroed A fragment, so the scheduler can hoist every LDS read
+    const int nblk = (diag & 2) ? 0 : (s1 - s0 + D - 1) / D;
+    for (int blk = 0; blk < nblk; ++blk) {
+        const int s = s0 + blk * D;
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             load_a(s + j + D - 1, ra[(j + D - 1) % D]);
-            if (s + j < s1) {
-                const int st = s + j;
-                const int g = st / KT, k = st - (st / KT) * KT;
-                half8_t bq[NR], bl[NR];
+            const int st = min(s + j, s1 - 1);
+            const bool live = s + j < s1;
+            const int g = st / KT, k = st - (st / KT) * KT;
+            half8_t a0 = ra[j][0], a1 = ra[j][1];
+            if (!live) a0 = half8_t{}, a1 = half8_t{};
+            half8_t bq[NR], bl[NR];
 #pragma unroll
-                for (int nr = 0; nr < NR; ++nr) {
-                    const _Float16* q = xp + (nr * 32 + k) * SX + 8 * g;
-                    bq[nr] = *(const half8_t*)q;
-                    if constexpr (P == 1) bl[nr] = *(const half8_t*)(q + plane);
-                }
+            for (int nr = 0; nr < NR; ++nr) {
+                const _Float16* q = xp + (nr * 32 + k) * SX + 8 * g;
+                bq[nr] = *(const half8_t*)q;
+                if constexpr (P == 1) bl[nr] = *(const half8_t*)(q + plane);
+            }
 #pragma unroll
-                for (int nr = 0; nr < NR; ++nr) {
-                    acc[0][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[j][0], bq[nr], acc[0][nr], 0, 0, 0);
-                    if constexpr (P == 1) {
-                        accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[j][0], bl[nr], accx[nr], 0, 0, 0);
-                        accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[j][1], bq[nr], accx[nr], 0, 0, 0);
-                    }
+            for (int nr = 0; nr < NR; ++nr) {
+                acc[0][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq[nr], acc[0][nr], 0, 0, 0);
+                if constexpr (P == 1) {
+                    accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bl[nr], accx[nr], 0, 0, 0);
+                    accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bq[nr], accx[nr], 0, 0, 0);
                 }
             }
         }

@@ -283,6 +283,18 @@ class FusedW:
 
 
 @dataclass
+class DownW:
+    """An encoder block's strided rate-change conv packed for ou_block's fused
+    fourth stage (ou_block_desc.w_down): [2C][C][kt * rate] tap-major."""
+    w: torch.Tensor
+    unscale: float
+    bias: Optional[torch.Tensor]
+    slope: float
+    rate: int
+    kt: int
+
+
+@dataclass
 class BlockW:
     """ConvBlock weights (blocks.py:234-351)."""
     C: int
@@ -293,6 +305,7 @@ class BlockW:
     conv3: ConvW
     rate_conv: Optional[ConvW] = None
     fused: Optional[FusedW] = None
+    down: Optional[DownW] = None
 
 
 def fuse_blocks_enabled():
@@ -324,16 +337,39 @@ def prep_fused(specs, C, prec, device):
     return FusedW(w, tuple(offs), tuple(uns), prec)
 
 
+def fuse_down_enabled():
+    """OUHIP_FUSE_DOWN=0 keeps the encoder's rate-change convs as their own launches."""
+    import os
+
+    return os.environ.get("OUHIP_FUSE_DOWN", "1") != "0"
+
+
+def prep_down_fused(spec, C, prec, bias, device):
+    """The rate-change conv in ou_block's layout (DownW), or None where the
+    fused block has no such stage."""
+    m, cr, kt = spec.w.shape
+    r = spec.frame
+    if not (fuse_down_enabled() and m == 2 * C and cr == C * r
+            and L.load().ou_block_down_supported(C, r, kt, prec)):
+        return None
+    # frame-view channel ci*r + ph at frame k -> tap k*r + ph of channel ci
+    w4 = np.ascontiguousarray(spec.w.reshape(m, C, r, kt).transpose(0, 1, 3, 2).reshape(m, C, kt * r))
+    packed, un = L.block_pack_np(w4)
+    return DownW(torch.from_numpy(packed).to(device), un, bias, float(spec.slope), r, kt)
+
+
 def prep_block(sd, p, kind, rate, antialias, device):
     specs = [spec_same(sd, p + ".conv1", 5), spec_same(sd, p + ".conv2", 3), spec_same(sd, p + ".conv3", 3)]
     c1, c2, c3 = (make_conv(sp, device) for sp in specs)
-    rc = None
+    rc, rc_spec = None, None
     if kind == "down":
-        rc = prep_down(sd, p + ".rate_change_conv", rate, antialias, device)
+        rc_spec = spec_down(sd, p + ".rate_change_conv", rate, antialias)
+        rc = make_conv(rc_spec, device)
     elif kind == "up":
         rc = prep_up(sd, p + ".rate_change_conv", rate, antialias, device)
     fused = prep_fused(specs, c1.m, c1.prec, device) if c1.prec in (1, 2) else None
-    return BlockW(c1.m, kind, rate, c1, c2, c3, rc, fused)
+    down = prep_down_fused(rc_spec, c1.m, c1.prec, rc.bias, device) if (fused and rc_spec) else None
+    return BlockW(c1.m, kind, rate, c1, c2, c3, rc, fused, down)
 
 
 @dataclass
@@ -468,10 +504,13 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
 
 def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film_bs=0,
               sc: Act = None, res2: Act = None, s2=1.0, cond_out: Act = None, skip_tail=False,
-              x_in=None, head=None):
+              x_in=None, head=None, e_out: Act = None):
     """ConvBlock main stage (blocks.py:393-407):
        cond_out = conv1(h); c = (cond_out + sc)/sqrt2; c = film(c); c = conv3(conv2(c));
-       out = (h + c)/sqrt2 [; out = (out + res2) * s2]"""
+       out = (h + c)/sqrt2 [; out = (out + res2) * s2]
+    and, for a down block given ``e_out``, its rate-change conv e_out =
+    rate_conv(out) (blocks.py:268-275): fused into the block where ou_block
+    has the stage, else its own launch."""
     c1_out = cond_out if cond_out is not None else tA
     d1 = conv_desc(bw.conv1, h, c1_out, res1=sc, s1=NF2, film=film, film_bs=film_bs)
     if skip_tail:
@@ -479,20 +518,27 @@ def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film
         return
     d2 = conv_desc(bw.conv2, c1_out, tB)
     d3 = conv_desc(bw.conv3, tB, out, res1=h, s1=NF2, res2=res2, s2=s2)
+    d_rc = conv_desc(bw.rate_conv, out, e_out) if e_out is not None else None
     if bw.fused is not None and out.ptr != h.ptr:
-        descs = (d1, d2, d3) + ((x_in[4],) if x_in is not None else ())
+        fuse_rc = d_rc is not None and bw.down is not None
+        descs = (d1, d2, d3) + ((x_in[4],) if x_in is not None else ()) + ((d_rc,) if fuse_rc else ())
         prog.add(L.OP_BLOCK, block_desc(bw, h, out, descs, sc=sc, film=film, film_bs=film_bs,
                                         cond_out=cond_out, res2=res2, s2=s2,
-                                        x_in=x_in[:4] if x_in is not None else None, head=head))
+                                        x_in=x_in[:4] if x_in is not None else None, head=head,
+                                        e_out=e_out if fuse_rc else None))
+        if d_rc is not None and not fuse_rc:
+            prog.add(L.OP_CONV, d_rc)
         return True
     assert x_in is None and head is None, "input / head fusion needs the fused block"
     prog.add(L.OP_CONV, d1)
     prog.add(L.OP_CONV, d2)
     prog.add(L.OP_CONV, d3)
+    if d_rc is not None:
+        prog.add(L.OP_CONV, d_rc)
 
 
 def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film_bs=0, cond_out: Act = None,
-               res2: Act = None, s2=1.0, x_in=None, head=None):
+               res2: Act = None, s2=1.0, x_in=None, head=None, e_out: Act = None):
     """ou_block descriptor of a ConvBlock's main path; ``descs`` are the
     equivalent ou_conv descriptors (their shape checks have run; their
     algorithmic FLOPs and bytes -- the unfused reference ops -- are kept).
@@ -530,6 +576,14 @@ def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film
     if head is not None:
         assert bw.C == 32 and head.length == h.T and head.channels == bw.C
         d.head = head
+    if e_out is not None:
+        dn = bw.down
+        assert e_out.C == 2 * bw.C and e_out.T == -(-h.T // dn.rate) and e_out.B >= h.B, ("block e", e_out.t.shape)
+        assert e_out.ptr not in (h.ptr, out.ptr)
+        d.w_down, d.w_down_unscale = dn.w.data_ptr(), dn.unscale
+        d.b_down = dn.bias.data_ptr() if dn.bias is not None else 0
+        d.slope_down, d.rate, d.down_kt = dn.slope, dn.rate, dn.kt
+        d.e, d.e_bstride, d.e_cstride = e_out.ptr, e_out.bs, e_out.cs
     d._flops = sum(x._flops for x in descs) + (head._flops if head is not None else 0.0)
     d._bytes = sum(x._bytes for x in descs)
     return d
@@ -956,9 +1010,8 @@ class Engine:
             bw = self.s_enc[i]
             x_in = (x, in_scale, self.s_in_w, self.s_in_b, d_in) if (i == 0 and fuse_in) else None
             rec_block(prog, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
-                      film=fb(i), film_bs=film_bs, x_in=x_in)
-            if bw.kind == "down":
-                prog.add(L.OP_CONV, conv_desc(bw.rate_conv, bufs[f"V{i}"], bufs[f"E{i+1}"]))
+                      film=fb(i), film_bs=film_bs, x_in=x_in,
+                      e_out=bufs[f"E{i+1}"] if bw.kind == "down" else None)
         # bottleneck GRU, fused with the decoder's first residual add
         top = n_lvl - 1
         rec_gru(prog, self.s_gru, 0, bufs[f"V{top}"], bufs["GI"], bufs[f"V{top}"],
@@ -1095,8 +1148,8 @@ class Engine:
         for i in range(n_lvl):
             bw = self.c_enc[i]
             if i < nr:
-                rec_block(prog, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"])
-                prog.add(L.OP_CONV, conv_desc(bw.rate_conv, bufs[f"V{i}"], bufs[f"E{i+1}"]))
+                rec_block(prog, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
+                          e_out=bufs[f"E{i+1}"])
                 if i < nr - 1:
                     prev = bufs["XMEL"] if nsum == 0 else bufs["SUM"]
                     prog.add(L.OP_CONV, conv_desc(self.c_st[i], bufs[f"V{i}"], bufs["SUM"],

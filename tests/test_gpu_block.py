@@ -158,3 +158,91 @@ def test_score_ends_fused_equal_unfused(monkeypatch):
         assert _rel(sc, torch.from_numpy(d["score_out"])) < 1e-4
     assert _rel(outs["1"], outs["0"]) < 1e-5
     assert nops["1"] < nops["0"]
+
+
+def _down_spec(C, r, kt, g):
+    """A strided rate-change conv in the engine's frame-view form (spec_down):
+    w[2C][ci*r + ph][kt], zero padding; kt 3 is centred (frames -1, 0, +1)."""
+    w = torch.randn(2 * C, C * r, kt, generator=g) / np.sqrt(C * r * kt)
+    b = 0.1 * torch.randn(2 * C, generator=g)
+    return E.ConvSpec(w.numpy(), C, r, (kt - 1) // 2, 1, 0.2, b.numpy(), ref_macs=float(w.numel()))
+
+
+def _down_ref(sp, y):
+    """float64: PReLU, zero right-pad to a multiple of r, frame view, conv."""
+    r, kt = sp.frame, sp.w.shape[2]
+    B, C, T = y.shape
+    U = -(-T // r)
+    x = torch.where(y >= 0, y, sp.slope * y)
+    x = F.pad(x, (0, U * r - T)).reshape(B, C, U, r).permute(0, 1, 3, 2).reshape(B, C * r, U)
+    w = torch.from_numpy(sp.w).double()
+    return F.conv1d(x, w, padding=(kt - 1) // 2) + torch.from_numpy(sp.bias).double()[None, :, None]
+
+
+@pytest.mark.parametrize("prec", [1, 2])
+@pytest.mark.parametrize("C,r,kt,T", [(32, 2, 3, 1001), (32, 2, 3, 119), (32, 2, 3, 3), (32, 2, 1, 250),
+                                      (64, 4, 1, 503), (64, 4, 1, 61), (64, 4, 1, 5)])
+def test_block_fused_down(C, r, kt, T, prec):
+    """The encoder's rate-change conv as ou_block's fourth stage: the block
+    output y and e = rate_conv(y) against the unfused launches and float64,
+    ragged lengths (the last workgroup's frames, a partial last output
+    frame), batch 2, with and without FiLM."""
+    g = torch.Generator().manual_seed(C + r + kt + T)
+    specs = _specs(C, g)
+    rsp = _down_spec(C, r, kt, g)
+    cws = [E.make_conv(sp, DEV, prec=prec) for sp in specs]
+    rc = E.make_conv(rsp, DEV, prec=prec)
+    fused = E.prep_fused(specs, C, prec, DEV)
+    down = E.prep_down_fused(rsp, C, prec, rc.bias, DEV)
+    assert fused is not None and down is not None
+    bw = E.BlockW(C, "down", r, *cws, rc, fused, down)
+    B = 2
+    h = torch.randn(B, C, T, generator=g)
+    film = torch.randn(B, 2 * C, generator=g) * 0.5 + torch.cat([torch.ones(C), torch.zeros(C)])
+    U = -(-T // r)
+    filmd = film.to(DEV)
+    for use_film in (False, True):
+        kw = {"film": filmd.data_ptr(), "film_bs": 2 * C} if use_film else {}
+        res = {}
+        for fz in ("fused", "unfused"):
+            if fz == "unfused":
+                bw.down = None
+            out, e = E.new_act(B, C, T, DEV), E.new_act(B, 2 * C, U, DEV)
+            kinds = _run(bw, E.Act(h.to(DEV)), out, True, e_out=e, **kw)
+            bw.down = down
+            res[fz] = (out.t.cpu(), e.t.cpu(), kinds)
+        assert res["fused"][2].count(L.OP_CONV) == 0 and res["unfused"][2].count(L.OP_CONV) == 1
+        y_ref, _ = _ref(specs, h.double(), film=film.double() if use_film else None)
+        e_ref = _down_ref(rsp, y_ref)
+        tol = 1e-5 if prec == 1 else 3e-3
+        assert _rel(res["fused"][0], y_ref) < tol
+        assert _rel(res["fused"][1], e_ref) < tol, _rel(res["fused"][1], e_ref)
+        assert _rel(res["fused"][1], res["unfused"][1]) < tol
+
+
+def test_encoder_down_fused_equal_unfused(monkeypatch):
+    """The encoders' rate-change convs fused into their blocks (score and
+    conditioner, 32 and 64 channels) give the same enhance as separate
+    launches, the score network still matches the reference's output, and the
+    fused program has fewer launches."""
+    from conftest import golden_state_dict, load_golden
+    from open_universe_amd.configs import get_config
+    from open_universe_amd.networks.universe import UniverseGAN
+
+    d = load_golden("pp16")
+    outs, nops = {}, {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("OUHIP_FUSE_DOWN", fuse)
+        cfg = get_config("pp16", None)
+        m = UniverseGAN(**{k: v for k, v in cfg.items() if k != "_target_"})
+        m.load_state_dict(golden_state_dict(d), strict=False)
+        m = m.to(DEV).eval()
+        mix = torch.from_numpy(d["enh_mix"]).to(DEV)
+        with torch.no_grad():
+            outs[fuse] = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
+            sc = m.get_score_model()(torch.from_numpy(d["score_x"]).to(DEV), torch.from_numpy(d["score_sigma"]).to(DEV),
+                                     [torch.from_numpy(d[f"cond_out{i}"]).to(DEV) for i in range(5)]).cpu()
+        nops[fuse] = len(next(iter(m._plans.values())).prog)
+        assert _rel(sc, torch.from_numpy(d["score_out"])) < 1e-4
+    assert _rel(outs["1"], outs["0"]) < 1e-5
+    assert nops["1"] <= nops["0"] - 3

@@ -190,8 +190,9 @@ def test_numpy_block_packing_matches_c():
 
     from open_universe_amd import _lib as L
 
-    for c, kt in ((32, 5), (64, 3), (128, 5)):
-        w = (np.random.default_rng(c).standard_normal((c, c, kt)) * 0.03).astype(np.float32)
+    # square block convs and the fused rate-change convs (2C x C x kt * rate)
+    for m, c, kt in ((32, 32, 5), (64, 64, 3), (128, 128, 5), (64, 32, 6), (128, 64, 12), (64, 32, 2)):
+        w = (np.random.default_rng(m + c + kt).standard_normal((m, c, kt)) * 0.03).astype(np.float32)
         a, ua = L.block_pack(w)
         b, ub = L.block_pack_np(w)
         assert ua == ub and np.array_equal(a, b)
