@@ -316,8 +316,16 @@ def main():
             dist.destroy_process_group()
         return
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU; more ranks than GPUs (a rehearsal of the N-rank path on
+    # a smaller box) share devices round-robin.  device_count() does not
+    # initialise the GPU.
+    ndev = torch.cuda.device_count()
+    gpu = local % ndev if ndev else local
+    if ndev and world > ndev and rank == 0:
+        print(f"[bench] {world} ranks on {ndev} GPU(s): ranks share devices round-robin (rehearsal, not a "
+              f"scaling measurement)", file=sys.stderr)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if C.get("conv_prec") and "OUHIP_CONV_PREC" not in os.environ:
         os.environ["OUHIP_CONV_PREC"] = C["conv_prec"]
     cfg, model = build_model(dev, arch=C["arch"])
@@ -395,6 +403,7 @@ def main():
                                "time (bench contract); the per-GPU figure the metric names is value_per_gpu",
             "value_per_gpu": round(value / world, 3),
             "n_gpus": world,
+            **({"gpus_visible": ndev, "ranks_share_gpus": True} if ndev and world > ndev else {}),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
