@@ -642,8 +642,8 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 }
 
 // ---------------------------------------------------------------------------
-// Register-streamed variant (tile bit 14; split-f16 / f16, frame 1, cin a
-// multiple of 16): for the deep, short levels (256 / 512 channels at 4005 /
+// Register-streamed variant (tile bit 14; split-f16 / f16, cin a multiple
+// of 16, any frame view R whose window fits LDS): for the deep, short levels (256 / 512 channels at 4005 /
 // 801 frames), where the chunked kernel above pays one L2 round trip per
 // 16-64-channel chunk and, to fill the chip, a K-slice pass plus a second
 // launch.  Here a workgroup stages its whole input window -- every input
@@ -653,8 +653,10 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 // lane-linear, no LDS copy).  4 waves as WM (32-row m-tiles) x WK (K halves or
 // quarters of every tap x 16-channel step), reduced through LDS in a fixed
 // order; the epilogue is conv_kernel's.
-//   X image: [frame w][h * cin/2 + p] = split(PReLU(x[2p + h][t0 + w]) 2^-6),
-//   row stride cin + 8 halves (an odd number of 16-B slots), lo plane after.
+//   X image: [frame w][h * CE/2 + p] = split(PReLU(x'[2p + h][t0 + w]) 2^-6)
+//   over the CE = cin * R frame-view channels, row stride CE + 8 halves (an
+//   odd number of 16-B slots), lo plane after; staged from consecutive
+//   samples, so the loads are coalesced whatever R is.
 template <int P>
 __device__ __forceinline__ void split4r(float x0, float x1, float x2, float x3, half4_t& hi, half4_t& lo, bool& ovf)
 {
@@ -692,7 +694,8 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     constexpr int W = R::W, D = R::RING;
     OU_DYNAMIC_LDS(float4, lds4);
     _Float16* xs = (_Float16*)lds4;
-    const int cin = d.cin, SX = cin + 8, HALF = cin / 2, plane = W * SX;
+    // K channels: the frame view's cin * R (phase-major: ph * cin + ci)
+    const int cin = d.cin, RF = d.frame, CE = cin * RF, SX = CE + 8, HALF = CE / 2, plane = W * SX;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave % WM, wk = wave / WM;
     const int h = lane >> 5, l32 = lane & 31;
@@ -712,7 +715,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     for (int nr = 0; nr < NR; ++nr)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[0][nr][r] = 0.f, accx[nr][r] = 0.f;
-    const int NS = (cin / 16) * KT;
+    const int NS = (CE / 16) * KT;
     const int s0 = wk * NS / WK, s1 = (wk + 1) * NS / WK;
     const half8_t* ap = (const half8_t*)d.w + mt * (a_mt_stride / 4) + lane;
     half8_t ra[D][2];
@@ -732,20 +735,24 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     const int64_t xc = d.x_cstride;
     const float scale = d.in_scale ? d.in_scale[b] : 1.f, slope = d.slope;
     constexpr float xsc = 1.f / (1 << kSplitShift);
-    const int t0 = n0 - d.pad + d.shift;
+    // item = (8 input channels, sample s of the window): consecutive lanes
+    // load consecutive samples (coalesced for any R); sample s is frame s / R,
+    // phase s % R, i.e. K channels ph * cin + 8 g .. + 7 of row s / R
+    const int WS = W * RF;                                 // window samples
+    const int t0 = (n0 - d.pad) * RF + d.shift;            // first window sample
     const int in_len = d.in_len;
-    const int NI = (cin / 8) * W;
+    const int NI = (cin / 8) * WS;
     bool ovf = false;
     // up to kStageItems items per thread in flight at once: the window is one
-    // L2 / HBM round trip for cin * W <= 8 * 256 * kStageItems
+    // L2 / HBM round trip for cin * W * R <= 8 * 256 * kStageItems
     constexpr int IPT = kStageItems;
     for (int base = 0; base < NI; base += IPT * 256) {
         float v[IPT][8];
 #pragma unroll
         for (int it = 0; it < IPT; ++it) {
             const int item = min(base + tid + 256 * it, NI - 1);
-            const int g = item / W, w = item - g * W;
-            const int t = t0 + w;
+            const int g = item / WS, sm = item - g * WS;
+            const int t = t0 + sm;
             const int tc = min(max(t, 0), in_len - 1);
             const float* src = xb + (int64_t)(8 * g) * xc + tc;
 #pragma unroll
@@ -759,7 +766,8 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
         for (int it = 0; it < IPT; ++it) {
             const int item = base + tid + 256 * it;
             if (item >= NI) break;
-            const int g = item / W, w = item - g * W;
+            const int g = item / WS, sm = item - g * WS;
+            const int w = sm / RF, ph = sm - w * RF;
             float x[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -769,7 +777,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
             half4_t he, le, ho, lo;
             split4r<P>(x[0], x[2], x[4], x[6], he, le, ovf);
             split4r<P>(x[1], x[3], x[5], x[7], ho, lo, ovf);
-            _Float16* dst = xs + w * SX + 4 * g;
+            _Float16* dst = xs + w * SX + (ph * cin + 8 * g) / 2;
             *(half4_t*)dst = he;
             *(half4_t*)(dst + HALF) = ho;
             if constexpr (P == 1) {
@@ -1826,9 +1834,9 @@ template <int KT, int WM, int WK, int NR, int P>
 int launch_r(const ou_conv_desc& d, hipStream_t s)
 {
     using R = RCfg<KT, WM, WK, NR>;
-    const int lds = rlds_bytes<KT, WM, WK, NR, P>(d.cin);
+    const int lds = rlds_bytes<KT, WM, WK, NR, P>(d.cin * d.frame);
     if (lds > kMaxLds)
-        return ou_fail(-2, "conv: register-streamed tile needs %d B of LDS at cin %d", lds, d.cin);
+        return ou_fail(-2, "conv: register-streamed tile needs %d B of LDS at %d K channels", lds, d.cin * d.frame);
     auto kern = conv_rkernel<KT, WM, WK, NR, P>;
     static bool attr = false;   // opt in to the full 160 KiB once
     if (!attr) {
@@ -1837,7 +1845,8 @@ int launch_r(const ou_conv_desc& d, hipStream_t s)
         attr = true;
     }
     const int mtiles = (d.m + 31) / 32;
-    const int cin_pad = (d.cin + kCinAlign - 1) / kCinAlign * kCinAlign;
+    const int cin_eff = d.cin * d.frame;
+    const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
     const int64_t a_mt_stride = (int64_t)cin_pad * KT * 32;
     dim3 grid((d.n_frames + R::BN - 1) / R::BN, (mtiles + WM - 1) / WM, d.batch);
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, d, mtiles, a_mt_stride);
@@ -2065,8 +2074,8 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     if (d.tile >= 0 && (d.tile & kRsBit)) {   // register-streamed kernel (bits 0-7: RTILES shape)
         if ((d.tile & ~(kRsBit | 0x3ff)) || (d.tile & 0xff) >= kNumRTiles)
             return ou_fail(-2, "conv: bad register-streamed tile 0x%x", d.tile);
-        if ((d.prec != 1 && d.prec != 2) || d.frame != 1 || d.cin % 16 || d.amax_in)
-            return ou_fail(-2, "conv: the register-streamed kernel needs prec 1/2, frame 1, cin %% 16 == 0, no amax_in");
+        if ((d.prec != 1 && d.prec != 2) || d.cin % 16 || d.amax_in)
+            return ou_fail(-2, "conv: the register-streamed kernel needs prec 1/2, cin %% 16 == 0, no amax_in");
         if (!(d.w_unscale > 0.f)) return ou_fail(-1, "conv: split-f16 needs the w_unscale of ou_conv_pack_split");
         hipStream_t rs = (hipStream_t)stream;
         const int t = d.tile & (0xff | kRsBit);   // bits 8-9 (diagnostics) travel in d.tile

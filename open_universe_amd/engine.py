@@ -712,9 +712,9 @@ class ConvTuner:
         if d.prec in (1, 2):
             cands = [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))
                      for k in ksl]
-            # register-streamed kernel (tile bit 14): frame-1 convs over whole
-            # input windows; ou_conv refuses the shapes whose window exceeds LDS
-            if d.frame == 1 and d.cin % 16 == 0 and not d.amax_in:
+            # register-streamed kernel (tile bit 14): whole input windows
+            # staged once; ou_conv refuses the shapes whose window exceeds LDS
+            if d.cin % 16 == 0 and not d.amax_in:
                 cands += [t | RS_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | RS_BIT)]
         elif d.amax_out:
             cands = [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t) for k in ksl]

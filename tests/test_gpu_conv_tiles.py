@@ -219,16 +219,20 @@ def test_conv_f16_every_tile(geom):
 
 
 RS_BIT = 1 << 14
-# (m, cin, kt, rout, T, batch): deep same-convs, the GRU input projection, a
-# transposed (rout) up-conv, rows past M and a ragged short clip
+# (m, cin, frame, kt, rout, T, batch): deep same-convs, the GRU input
+# projection, a transposed (rout) up-conv, frame-view (strided) down-convs
+# with and without the folded FIR, rows past M and a ragged short clip
 RS_GEOMS = [
-    (512, 512, 3, 1, 801, 1),
-    (512, 512, 5, 1, 203, 2),
-    (256, 256, 3, 1, 1001, 2),
-    (1536, 512, 1, 1, 99, 1),
-    (1280, 512, 3, 5, 157, 1),
-    (96, 48, 3, 1, 77, 2),
-    (48, 80, 1, 1, 45, 1),
+    (512, 512, 1, 3, 1, 801, 1),
+    (512, 512, 1, 5, 1, 203, 2),
+    (256, 256, 1, 3, 1, 1001, 2),
+    (1536, 512, 1, 1, 1, 99, 1),
+    (1280, 512, 1, 3, 5, 157, 1),
+    (96, 48, 1, 3, 1, 77, 2),
+    (48, 80, 1, 1, 1, 45, 1),
+    (128, 64, 4, 3, 1, 2003, 2),
+    (64, 32, 2, 1, 1, 999, 1),
+    (256, 128, 4, 3, 1, 401, 1),
 ]
 
 
@@ -236,16 +240,17 @@ RS_GEOMS = [
 def test_conv_register_streamed_every_shape(geom):
     """The register-streamed kernel (tile bit 14), every shape, split-f16 and
     f16, with the full epilogue (bias, residual 1, FiLM, residual 2, valid_len,
-    the rout pixel shuffle): equal to the chunked kernel on the same packed
-    weights up to f32 summation order."""
-    m, cin, kt, rout, T, B = geom
-    g = torch.Generator().manual_seed(m + cin + kt)
-    w = torch.randn(m, cin, kt, generator=g) * (1.0 / np.sqrt(cin * kt))
+    the rout pixel shuffle, the frame view): equal to the chunked kernel on the
+    same packed weights up to f32 summation order."""
+    m, cin, frame, kt, rout, T, B = geom
+    g = torch.Generator().manual_seed(m + cin + kt + frame)
+    w = torch.randn(m, cin * frame, kt, generator=g) * (1.0 / np.sqrt(cin * frame * kt))
     cout = m // rout
     bias = torch.randn(cout, generator=g) * 0.1
-    spec = E.ConvSpec(w.numpy(), cin, 1, (kt - 1) // 2, rout, 0.25, bias.numpy())
+    spec = E.ConvSpec(w.numpy(), cin, frame, (kt - 1) // 2, rout, 0.25, bias.numpy())
     x = torch.randn(B, cin, T, generator=g)
-    L_out = T * rout
+    U = -(-T // frame)
+    L_out = U * rout
     r1 = torch.randn(B, cout, L_out, generator=g)
     r2 = torch.randn(B, cout, L_out, generator=g)
     film = torch.randn(B, 2 * cout, generator=g).to(DEV)
@@ -259,7 +264,7 @@ def test_conv_register_streamed_every_shape(geom):
         def run(tile):
             y = E.new_act(B, cout, L_out, DEV)
             d = E.conv_desc(cw, xa, y, res1=r1a, s1=0.7, film=film.data_ptr(), film_bs=2 * cout, res2=r2a,
-                            s2=0.5, n_frames=T, out_len=L_out, valid_len=L_out - 2)
+                            s2=0.5, n_frames=U, out_len=L_out, valid_len=L_out - 2)
             d.tile = tile
             rc = lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
             torch.cuda.synchronize()
@@ -267,6 +272,12 @@ def test_conv_register_streamed_every_shape(geom):
 
         rc, ref = run(-1)
         assert rc == 0
+        if prec == 1 and rout == 1:   # the chunked kernel itself against torch fp32
+            want = _ref(w, bias, x, frame, kt, 0.25, None, 1.0)
+            want[:, :, L_out - 2:] = 0.0
+            want = film.cpu()[:, :cout, None] * ((want + r1) * 0.7) + film.cpu()[:, cout:, None]
+            want = (want + r2) * 0.5
+            assert ((ref - want).norm() / want.norm()).item() < 1e-5
         for t in range(16):
             if not lib.ou_conv_tile_ok(kt, t | RS_BIT):
                 continue

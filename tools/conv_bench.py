@@ -31,6 +31,9 @@ LAYERS = {
     "L4k3": (512, 512, 1, 3, 800, 1, True),
     "L4k5": (512, 512, 1, 5, 800, 1, False),
     "D3": (512, 256, 5, 3, 800, 1, False),     # down-sampling conv, rate 5 (polyphase)
+    "D1": (128, 64, 4, 3, 16000, 1, False),    # down-sampling conv, rate 4 (level 1 -> 2)
+    "D2": (256, 128, 4, 3, 4000, 1, False),    # down-sampling conv, rate 4 (level 2 -> 3)
+    "CD1": (128, 64, 4, 1, 16000, 1, False),   # conditioner down conv (no FIR), rate 4
     "U3": (1280, 512, 1, 3, 800, 5, True),     # up-sampling conv, rate 5
     "GI": (1536, 512, 1, 1, 800, 1, False),    # GRU input projection
     "U2": (512, 256, 1, 3, 4000, 4, True),     # up-sampling conv, rate 4 (level 3 -> 2)
@@ -94,7 +97,7 @@ def main():
             tiles = [a.tile] if a.tile is not None else [t | k for t in range(lib.ou_conv_num_tiles())
                                                           if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))
                                                           for k in (0, 1 << 12, 2 << 12, 3 << 12)]
-            if a.tile is None and d.frame == 1 and d.cin % 16 == 0:   # register-streamed kernel
+            if a.tile is None and d.cin % 16 == 0:   # register-streamed kernel
                 tiles += [t | E.RS_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | E.RS_BIT)]
                 if a.rdiag:
                     tiles += [t | v for t in tiles if t & E.RS_BIT for v in (1 << 8, 2 << 8, 3 << 8)]
