@@ -719,8 +719,10 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     const int s0 = wk * NS / WK, s1 = (wk + 1) * NS / WK;
     const half8_t* ap = (const half8_t*)d.w + mt * (a_mt_stride / 4) + lane;
     half8_t ra[D][2];
+    // a wave with no steps (NS < WK) still issues its prologue loads: clamp
+    // every step index into [s0, NS), never below its range (s0 < NS always)
     auto load_a = [&](int s, half8_t (&dst)[2]) {
-        const int sc = min(s, s1 - 1);
+        const int sc = max(s0, min(s, s1 - 1));
         const int g = sc / KT, k = sc - (sc / KT) * KT;
         const half8_t* p = ap + ((int64_t)(2 * g) * KT + k) * 64;
         dst[0] = p[0];
@@ -797,7 +799,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             load_a(s + j + D - 1, ra[(j + D - 1) % D]);
-            const int st = min(s + j, s1 - 1);
+            const int st = max(s0, min(s + j, s1 - 1));
             const bool live = s + j < s1;
             const int g = st / KT, k = st - (st / KT) * KT;
             half8_t a0 = ra[j][0], a1 = ra[j][1];

@@ -80,6 +80,13 @@ def overlap_enabled():
     return os.environ.get("OUHIP_OVERLAP", "1") != "0"
 
 
+def st_lane_enabled():
+    """OUHIP_ST_LANE=0 keeps the conditioner's st_convs on its own lane."""
+    import os
+
+    return os.environ.get("OUHIP_ST_LANE", "1") != "0"
+
+
 def split_amax_enabled():
     import os
 
@@ -1125,9 +1132,14 @@ class Engine:
         bufs["TB"] = [new_act(B, self.c_dec[l].C, Ts[min(n_lvl - 1 - l, len(rates))], dev) for l in range(n_lvl)]
         return bufs
 
-    def rec_cond(self, prog, bufs, x: Act, need_aux=False, after_level=None):
+    def rec_cond(self, prog, bufs, x: Act, need_aux=False, after_level=None, st_lane=None):
         """ConditionerNetwork.forward (condition.py:346-377).  ``after_level(l,
-        cond_l)`` runs right after decoder level l has produced its condition."""
+        cond_l)`` runs right after decoder level l has produced its condition.
+        With ``st_lane`` (recording on a side lane) the strided st_convs, which
+        only feed the bottleneck level's residual, are recorded on lane
+        ``st_lane`` instead, each behind a signal that its encoder level is
+        done, and the bottleneck block waits for their sum: they run beside the
+        next encoder levels instead of in line."""
         rates = list(self.ccfg["rate_factors"])
         nr = len(rates)
         n_lvl = len(self.c_enc)
@@ -1152,10 +1164,23 @@ class Engine:
                           e_out=bufs[f"E{i+1}"])
                 if i < nr - 1:
                     prev = bufs["XMEL"] if nsum == 0 else bufs["SUM"]
+                    if st_lane is not None:
+                        side = _LANE
+                        ev = prog.signal()
+                        set_lane(prog, st_lane)
+                        prog.wait(ev)
                     prog.add(L.OP_CONV, conv_desc(self.c_st[i], bufs[f"V{i}"], bufs["SUM"],
                                                   n_frames=U, res1=prev, s1=1.0))
+                    if st_lane is not None:
+                        set_lane(prog, side)
                     nsum += 1
             else:
+                if st_lane is not None and nsum:
+                    side = _LANE
+                    set_lane(prog, st_lane)
+                    ev = prog.signal()
+                    set_lane(prog, side)
+                    prog.wait(ev)
                 n_out = nsum + 1
                 nf = np.float32(1.0 / math.sqrt(n_out + 1))
                 rec_block(prog, bw, bufs[f"E{i}"], bufs["OUT"], bufs["LA"], bufs["LB"],

@@ -110,7 +110,7 @@ class EnhancePlan(_PlanBase):
 
     def __init__(self, eng, batch, mix_len, n_steps, epsilon, keep_rms=False,
                  use_aux_signal=False, warm_start=None, diff=None, ensemble=None,
-                 ensemble_mode=None, slot=0, arena=None):
+                 ensemble_mode=None, slot=0, arena=None, st_lane=True):
         # arena: record every buffer into this Arena (engine.Arena; the caller
         # owns it and retries with a bigger one on ArenaFull)
         if arena is not None:
@@ -185,7 +185,8 @@ class EnhancePlan(_PlanBase):
                 p.add(L.OP_CONV, E.conv_desc(eng.s_sc[l], cond, self.SC[l]))
                 ev_cond[l] = p.signal()
         conds, yaux = eng.rec_cond(p, cb, self.XN, need_aux=use_aux_signal or warm_start is not None,
-                                   after_level=after_level)
+                                   after_level=after_level,
+                                   st_lane=0 if (self.overlap and st_lane and E.st_lane_enabled()) else None)
         if use_aux_signal or warm_start is not None:
             self.AUXT = new_act(B, yaux.C, Tp, dev)
             self.SIG = new_act(B, 1, Tp, dev)

@@ -233,6 +233,9 @@ RS_GEOMS = [
     (128, 64, 4, 3, 1, 2003, 2),
     (64, 32, 2, 1, 1, 999, 1),
     (256, 128, 4, 3, 1, 401, 1),
+    # fewer K steps than K-split waves (16 channels x 1 tap: one step)
+    (32, 16, 1, 1, 2, 440, 2),
+    (32, 16, 1, 3, 1, 300, 1),
 ]
 
 
