@@ -678,24 +678,29 @@ struct RCfg {
     static_assert(WM * WK == 4, "4 waves per workgroup");
 };
 
-// LDS bytes of the register-streamed kernel at cin input channels
+// LDS bytes of the register-streamed kernel for chunks of cec K channels
 template <int KT, int WM, int WK, int NR, int P>
-int rlds_bytes(int cin)
+int rlds_bytes(int cec)
 {
     using R = RCfg<KT, WM, WK, NR>;
-    const int x = R::W * (cin + 8) * (P == 1 ? 2 : 1) * 2;
+    const int x = R::W * (cec + 8) * (P == 1 ? 2 : 1) * 2;
     return std::max(x, R::RED * 4);
 }
 
+
 template <int KT, int WM, int WK, int NR, int P>
-__global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride)
+__global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride, int PC, int CCH)
 {
     using R = RCfg<KT, WM, WK, NR>;
     constexpr int W = R::W, D = R::RING;
     OU_DYNAMIC_LDS(float4, lds4);
     _Float16* xs = (_Float16*)lds4;
-    // K channels: the frame view's cin * R (phase-major: ph * cin + ci)
-    const int cin = d.cin, RF = d.frame, CE = cin * RF, SX = CE + 8, HALF = CE / 2, plane = W * SX;
+    // K channels: the frame view's cin * R (phase-major: ph * cin + ci), in
+    // chunks of PC phases x CCH channels (PC == 1 or CCH == cin, so a chunk is
+    // the contiguous K range [p0 cin + c0, + CEC)); one chunk when the whole
+    // window fits LDS
+    const int cin = d.cin, RF = d.frame, CEC = PC * CCH, SX = CEC + 8, HALF = CEC / 2, plane = W * SX;
+    const int nchc = cin / CCH, nchunks = (RF / PC) * nchc;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave % WM, wk = wave / WM;
     const int h = lane >> 5, l32 = lane & 31;
@@ -705,118 +710,122 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     const int mt = min(mtu, mtiles - 1);
     const int diag = (d.tile >> 8) & 3;   // diagnostics (tools/conv_bench.py --rdiag): 1 no input loads, 2 no K loop
 
-    // ---- K loop: steps s = (16-channel group g, tap k), s = g * KT + k;
-    // wave wk owns steps [s0, s1).  A fragments (hi | lo) stream from the
-    // packed global order [m-tile][g][hi | lo][tap][lane][8] through a D-deep
-    // ring whose first D - 1 steps are issued before the input staging, so
-    // their L2 latency overlaps it.
     floatx16 acc[1][NR], accx[NR];
 #pragma unroll
     for (int nr = 0; nr < NR; ++nr)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[0][nr][r] = 0.f, accx[nr][r] = 0.f;
-    const int NS = (CE / 16) * KT;
+    // ---- per chunk, steps s = (16-channel group g of the chunk, tap k),
+    // s = g * KT + k; wave wk owns steps [s0, s1).  A fragments (hi | lo)
+    // stream from the packed global order [m-tile][G][hi | lo][tap][lane][8]
+    // (G = the chunk's first 16-group + g) through a D-deep ring whose first
+    // D - 1 steps are issued before the chunk's staging, so their L2 latency
+    // overlaps it.
+    const int NS = (CEC / 16) * KT;
     const int s0 = wk * NS / WK, s1 = (wk + 1) * NS / WK;
-    const half8_t* ap = (const half8_t*)d.w + mt * (a_mt_stride / 4) + lane;
+    const half8_t* ap0 = (const half8_t*)d.w + mt * (a_mt_stride / 4) + lane;
     half8_t ra[D][2];
-    // a wave with no steps (NS < WK) still issues its prologue loads: clamp
-    // every step index into [s0, NS), never below its range (s0 < NS always)
-    auto load_a = [&](int s, half8_t (&dst)[2]) {
-        const int sc = max(s0, min(s, s1 - 1));
-        const int g = sc / KT, k = sc - (sc / KT) * KT;
-        const half8_t* p = ap + ((int64_t)(2 * g) * KT + k) * 64;
-        dst[0] = p[0];
-        if constexpr (P == 1) dst[1] = p[KT * 64];
-    };
-#pragma unroll
-    for (int j = 0; j < D - 1; ++j) load_a(s0 + j, ra[j]);
-    // ---- stage the input window: item = (8-channel group g, frame w); 8
-    // loads, consecutive lanes = consecutive frames; then even channels to the
-    // h = 0 half of the row, odd channels to the h = 1 half
     const float* xb = d.x + (int64_t)b * d.x_bstride;
     const int64_t xc = d.x_cstride;
     const float scale = d.in_scale ? d.in_scale[b] : 1.f, slope = d.slope;
     constexpr float xsc = 1.f / (1 << kSplitShift);
-    // item = (8 input channels, sample s of the window): consecutive lanes
-    // load consecutive samples (coalesced for any R); sample s is frame s / R,
-    // phase s % R, i.e. K channels ph * cin + 8 g .. + 7 of row s / R
-    const int WS = W * RF;                                 // window samples
-    const int t0 = (n0 - d.pad) * RF + d.shift;            // first window sample
     const int in_len = d.in_len;
-    const int NI = (cin / 8) * WS;
+    const int WS = W * PC;                                 // window samples of one chunk, per channel
+    const int NI = (CCH / 8) * WS;
     bool ovf = false;
-    // up to kStageItems items per thread in flight at once: the window is one
-    // L2 / HBM round trip for cin * W * R <= 8 * 256 * kStageItems
-    constexpr int IPT = kStageItems;
-    for (int base = 0; base < NI; base += IPT * 256) {
-        float v[IPT][8];
-#pragma unroll
-        for (int it = 0; it < IPT; ++it) {
-            const int item = min(base + tid + 256 * it, NI - 1);
-            const int g = item / WS, sm = item - g * WS;
-            const int t = t0 + sm;
-            const int tc = min(max(t, 0), in_len - 1);
-            const float* src = xb + (int64_t)(8 * g) * xc + tc;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) v[it][i] = (diag & 1) ? 0.f : src[i * xc];
-            if (t != tc) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) v[it][i] = 0.f;
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < IPT; ++it) {
-            const int item = base + tid + 256 * it;
-            if (item >= NI) break;
-            const int g = item / WS, sm = item - g * WS;
-            const int w = sm / RF, ph = sm - w * RF;
-            float x[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float q = v[it][i] * scale;
-                x[i] = (q >= 0.f ? q : q * slope) * xsc;
-            }
-            half4_t he, le, ho, lo;
-            split4r<P>(x[0], x[2], x[4], x[6], he, le, ovf);
-            split4r<P>(x[1], x[3], x[5], x[7], ho, lo, ovf);
-            _Float16* dst = xs + w * SX + (ph * cin + 8 * g) / 2;
-            *(half4_t*)dst = he;
-            *(half4_t*)(dst + HALF) = ho;
-            if constexpr (P == 1) {
-                *(half4_t*)(dst + plane) = le;
-                *(half4_t*)(dst + plane + HALF) = lo;
-            }
-        }
-    }
-    __syncthreads();
-
     const _Float16* xp = xs + l32 * SX + h * HALF;
-    // branch-free blocks of D steps: steps past s1 (the last block's padding)
-    // multiply a zeroed A fragment, so the scheduler can hoist every LDS read
-    const int nblk = (diag & 2) ? 0 : (s1 - s0 + D - 1) / D;
-    for (int blk = 0; blk < nblk; ++blk) {
-        const int s = s0 + blk * D;
+    for (int q = 0; q < nchunks; ++q) {
+        const int p0 = (q / nchc) * PC, c0 = (q - (q / nchc) * nchc) * CCH;
+        const half8_t* ap = ap0 + (int64_t)((p0 * cin + c0) / 16) * 2 * KT * 64;
+        // a wave with no steps (NS < WK) still issues its prologue loads: clamp
+        // every step index into [s0, NS), never below its range (s0 < NS always)
+        auto load_a = [&](int s, half8_t (&dst)[2]) {
+            const int sc = max(s0, min(s, s1 - 1));
+            const int g = sc / KT, k = sc - (sc / KT) * KT;
+            const half8_t* pp = ap + ((int64_t)(2 * g) * KT + k) * 64;
+            dst[0] = pp[0];
+            if constexpr (P == 1) dst[1] = pp[KT * 64];
+        };
 #pragma unroll
-        for (int j = 0; j < D; ++j) {
-            load_a(s + j + D - 1, ra[(j + D - 1) % D]);
-            const int st = max(s0, min(s + j, s1 - 1));
-            const bool live = s + j < s1;
-            const int g = st / KT, k = st - (st / KT) * KT;
-            half8_t a0 = ra[j][0], a1 = ra[j][1];
-            if (!live) a0 = half8_t{}, a1 = half8_t{};
-            half8_t bq[NR], bl[NR];
+        for (int j = 0; j < D - 1; ++j) load_a(s0 + j, ra[j]);
+        if (q > 0) __syncthreads();   // every wave is done reading the previous chunk
+        // ---- stage the chunk: item = (8 channels c0 + 8 g .., sample j of the
+        // chunk's window): consecutive lanes load consecutive samples of PC
+        // phases (the whole frame when PC = R); sample j is frame j / PC, phase
+        // p0 + j % PC, i.e. chunk K channels (j % PC) cin + 8 g .. + 7 of row j / PC
+        const int t0 = (n0 - d.pad) * RF + d.shift + p0;   // first sample of frame 0, phase p0
+        // up to kStageItems items per thread in flight at once
+        constexpr int IPT = kStageItems;
+        for (int base = 0; base < NI; base += IPT * 256) {
+            float v[IPT][8];
 #pragma unroll
-            for (int nr = 0; nr < NR; ++nr) {
-                const _Float16* q = xp + (nr * 32 + k) * SX + 8 * g;
-                bq[nr] = *(const half8_t*)q;
-                if constexpr (P == 1) bl[nr] = *(const half8_t*)(q + plane);
+            for (int it = 0; it < IPT; ++it) {
+                const int item = min(base + tid + 256 * it, NI - 1);
+                const int g = item / WS, sm = item - g * WS;
+                const int w = sm / PC, pl = sm - w * PC;
+                const int t = t0 + w * RF + pl;
+                const int tc = min(max(t, 0), in_len - 1);
+                const float* src = xb + (int64_t)(c0 + 8 * g) * xc + tc;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[it][i] = (diag & 1) ? 0.f : src[i * xc];
+                if (t != tc) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[it][i] = 0.f;
+                }
             }
 #pragma unroll
-            for (int nr = 0; nr < NR; ++nr) {
-                acc[0][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq[nr], acc[0][nr], 0, 0, 0);
+            for (int it = 0; it < IPT; ++it) {
+                const int item = base + tid + 256 * it;
+                if (item >= NI) break;
+                const int g = item / WS, sm = item - g * WS;
+                const int w = sm / PC, pl = sm - w * PC;
+                float x[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float qv = v[it][i] * scale;
+                    x[i] = (qv >= 0.f ? qv : qv * slope) * xsc;
+                }
+                half4_t he, le, ho, lo;
+                split4r<P>(x[0], x[2], x[4], x[6], he, le, ovf);
+                split4r<P>(x[1], x[3], x[5], x[7], ho, lo, ovf);
+                _Float16* dst = xs + w * SX + (pl * cin + 8 * g) / 2;
+                *(half4_t*)dst = he;
+                *(half4_t*)(dst + HALF) = ho;
                 if constexpr (P == 1) {
-                    accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bl[nr], accx[nr], 0, 0, 0);
-                    accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bq[nr], accx[nr], 0, 0, 0);
+                    *(half4_t*)(dst + plane) = le;
+                    *(half4_t*)(dst + plane + HALF) = lo;
+                }
+            }
+        }
+        __syncthreads();
+
+        // branch-free blocks of D steps: steps past s1 (the last block's padding)
+        // multiply a zeroed A fragment, so the scheduler can hoist every LDS read
+        const int nblk = (diag & 2) ? 0 : (s1 - s0 + D - 1) / D;
+        for (int blk = 0; blk < nblk; ++blk) {
+            const int s = s0 + blk * D;
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                load_a(s + j + D - 1, ra[(j + D - 1) % D]);
+                const int st = max(s0, min(s + j, s1 - 1));
+                const bool live = s + j < s1;
+                const int g = st / KT, k = st - (st / KT) * KT;
+                half8_t a0 = ra[j][0], a1 = ra[j][1];
+                if (!live) a0 = half8_t{}, a1 = half8_t{};
+                half8_t bq[NR], bl[NR];
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr) {
+                    const _Float16* qq = xp + (nr * 32 + k) * SX + 8 * g;
+                    bq[nr] = *(const half8_t*)qq;
+                    if constexpr (P == 1) bl[nr] = *(const half8_t*)(qq + plane);
+                }
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr) {
+                    acc[0][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq[nr], acc[0][nr], 0, 0, 0);
+                    if constexpr (P == 1) {
+                        accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bl[nr], accx[nr], 0, 0, 0);
+                        accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bq[nr], accx[nr], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -1832,13 +1841,39 @@ int lds_bytes_kt(int tile)
 #define OU_RTILES(X) X(0, 2, 2, 1) X(1, 2, 2, 2) X(2, 4, 1, 1) X(3, 1, 4, 1) X(4, 4, 1, 2) X(5, 1, 4, 2)
 [[maybe_unused]] constexpr int kNumRTiles = 6;
 
+// K chunking of the register-streamed kernel: the whole window (pc = R
+// phases x cch = cin channels) when it fits LDS, else chunks of at most half
+// the LDS (two workgroups per CU) -- pc phases of every channel, or for R = 1
+// cch channels.  Returns false when no chunking fits.
+template <int KT, int WM, int WK, int NR, int P>
+bool rchunks(int cin, int rf, int* pc, int* cch)
+{
+    if (rlds_bytes<KT, WM, WK, NR, P>(cin * rf) <= kMaxLds) {
+        *pc = rf, *cch = cin;
+        return true;
+    }
+    int best = 0;
+    if (rf > 1) {
+        for (int q = 1; q < rf; ++q)
+            if (rf % q == 0 && (q * cin) % 16 == 0 && rlds_bytes<KT, WM, WK, NR, P>(q * cin) <= kMaxLds / 2)
+                best = q;
+        *pc = best, *cch = cin;
+    } else {
+        for (int c = 16; c < cin; c += 16)
+            if (cin % c == 0 && rlds_bytes<KT, WM, WK, NR, P>(c) <= kMaxLds / 2) best = c;
+        *pc = 1, *cch = best;
+    }
+    return best > 0;
+}
+
 template <int KT, int WM, int WK, int NR, int P>
 int launch_r(const ou_conv_desc& d, hipStream_t s)
 {
     using R = RCfg<KT, WM, WK, NR>;
-    const int lds = rlds_bytes<KT, WM, WK, NR, P>(d.cin * d.frame);
-    if (lds > kMaxLds)
-        return ou_fail(-2, "conv: register-streamed tile needs %d B of LDS at %d K channels", lds, d.cin * d.frame);
+    int pc = 0, cch = 0;
+    if (!rchunks<KT, WM, WK, NR, P>(d.cin, d.frame, &pc, &cch))
+        return ou_fail(-2, "conv: no register-streamed K chunking for cin %d x frame %d", d.cin, d.frame);
+    const int lds = rlds_bytes<KT, WM, WK, NR, P>(pc * cch);
     auto kern = conv_rkernel<KT, WM, WK, NR, P>;
     static bool attr = false;   // opt in to the full 160 KiB once
     if (!attr) {
@@ -1851,7 +1886,7 @@ int launch_r(const ou_conv_desc& d, hipStream_t s)
     const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
     const int64_t a_mt_stride = (int64_t)cin_pad * KT * 32;
     dim3 grid((d.n_frames + R::BN - 1) / R::BN, (mtiles + WM - 1) / WM, d.batch);
-    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, d, mtiles, a_mt_stride);
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, d, mtiles, a_mt_stride, pc, cch);
     return ou_check_launch("conv");
 }
 

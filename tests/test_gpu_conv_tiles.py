@@ -233,6 +233,12 @@ RS_GEOMS = [
     (128, 64, 4, 3, 1, 2003, 2),
     (64, 32, 2, 1, 1, 999, 1),
     (256, 128, 4, 3, 1, 401, 1),
+    # K chunked through LDS: the conditioner's st_convs (rates 160 / 20),
+    # the rate-5 down conv, a frame-1 conv over 2048 channels
+    (512, 32, 160, 1, 1, 6401, 1),
+    (512, 128, 20, 1, 1, 2001, 2),
+    (512, 256, 5, 3, 1, 1003, 1),
+    (64, 2048, 1, 1, 1, 100, 1),
     # fewer K steps than K-split waves (16 channels x 1 tap: one step)
     (32, 16, 1, 1, 2, 440, 2),
     (32, 16, 1, 3, 1, 300, 1),

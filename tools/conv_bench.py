@@ -34,6 +34,9 @@ LAYERS = {
     "D1": (128, 64, 4, 3, 16000, 1, False),    # down-sampling conv, rate 4 (level 1 -> 2)
     "D2": (256, 128, 4, 3, 4000, 1, False),    # down-sampling conv, rate 4 (level 2 -> 3)
     "CD1": (128, 64, 4, 1, 16000, 1, False),   # conditioner down conv (no FIR), rate 4
+    "ST0": (512, 32, 160, 1, 800, 1, False),   # conditioner st_convs (level -> bottleneck)
+    "ST1": (512, 64, 80, 1, 800, 1, False),
+    "ST2": (512, 128, 20, 1, 800, 1, False),
     "U3": (1280, 512, 1, 3, 800, 5, True),     # up-sampling conv, rate 5
     "GI": (1536, 512, 1, 1, 800, 1, False),    # GRU input projection
     "U2": (512, 256, 1, 3, 4000, 4, True),     # up-sampling conv, rate 4 (level 3 -> 2)
