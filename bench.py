@@ -439,7 +439,7 @@ def main():
             if args.traffic_json and os.path.exists(args.traffic_json):
                 with open(args.traffic_json) as fh:
                     pmc = json.load(fh)
-                rows = [r for k, r in pmc.get("kernels", {}).items() if k in ("conv_kernel", "block_kernel")]
+                rows = [r for k, r in pmc.get("kernels", {}).items() if k in ("conv_kernel", "conv_rkernel", "block_kernel")]
                 if rows and pmc.get("config", "c2") == args.config and pmc.get("enhances_profiled"):
                     # bytes of every conv-stack dispatch of one enhance, per
                     # recorded conv op (K-slice ops dispatch twice)
@@ -461,7 +461,7 @@ def main():
             out["roofline"] = {
                 **rl, "traffic": traffic,
                 "traffic_source": tsrc,
-                "kernel": "conv stack: ou_conv (conv_kernel) + fused ConvBlock ou_block (block_kernel), "
+                "kernel": "conv stack: ou_conv (conv_kernel, conv_rkernel) + fused ConvBlock ou_block (block_kernel), "
                           "all launches of one enhance",
                 "launches": prof["n_conv"],
                 "fused_block_launches": prof["n_block"],
