@@ -65,6 +65,9 @@ def cpu_model():
 # on request (--config) with the same harness.  Batch is per GPU for c3 and the
 # whole-node batch for c4 (32 clips sharded over the ranks: 32/N per rank).
 CONFIGS = {
+    "c1": dict(arch="pp16", batch=1, seconds=4.0, n_steps=None,
+               workload="UNIVERSE++ 16 kHz enhance(), batch=1, one 4 s clip, 8 diffusion steps (BASELINE.json "
+                        "configs[0]: the reference's CPU-only case; here on the GPU, the oracle's CPU time beside it)"),
     "c2": dict(arch="pp16", batch=1, seconds=8.0, n_steps=None,
                workload="UNIVERSE++ 16 kHz enhance(), batch=1, 8 s clip, 8 diffusion steps (BASELINE.json configs[1])"),
     "c3": dict(arch="orig16", batch=8, seconds=8.0, n_steps=60,
@@ -119,7 +122,7 @@ def available_cpus():
 
 # CPU sample per config: (clip seconds at B=1, clip seconds at the config's B).
 # Bounded so each leg is a few seconds of oracle work (c2: the full 8 s clip).
-CPU_SAMPLE = {"c2": (8.0, 8.0), "c3": (1.0, 0.25), "c4": (2.0, 0.1), "c5": (8.0, 8.0)}
+CPU_SAMPLE = {"c1": (4.0, 4.0), "c2": (8.0, 8.0), "c3": (1.0, 0.25), "c4": (2.0, 0.1), "c5": (8.0, 8.0)}
 
 
 def cpu_baseline(model, cfg, C, config_name):

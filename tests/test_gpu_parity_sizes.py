@@ -197,6 +197,15 @@ def test_c2_size_enhance_vs_oracle():
     assert rel_rms(out, ref) < 1e-3 and si_sdr(out, ref) > 60
 
 
+def test_c1_size_enhance_vs_oracle():
+    """BASELINE configs[0]: PP16, one 4 s clip (the reference's CPU-only
+    plumbing case), 8 steps, the HIP path against the fp32 oracle on the same
+    noise."""
+    m, out, ref = _vs_oracle("pp16", 1, 4.0)
+    assert out.shape == ref.shape == (1, 64000)
+    assert rel_rms(out, ref) < 1e-3 and si_sdr(out, ref) > 60
+
+
 def test_c3_shape_enhance_vs_oracle():
     """BASELINE configs[2]: ORIG16 full width, batch 8, 60 steps (0.25 s clips
     so the oracle finishes in seconds)."""
