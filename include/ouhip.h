@@ -276,6 +276,18 @@ int ou_signal_median(const float* x, float* y, int ensemble, int batch, int64_t 
 int ou_resample(const float* x, int64_t x_bstride, float* y, int64_t y_bstride, int batch, int n_in,
                 int n_out, const float* kernel, int phases, int taps, int orig, int width, void* stream);
 
+/* FLAC input decoding for the CLI (host code): the
+ * reference reads .wav/.mp3/.flac with torchaudio.load (bin/enhance.py:33,
+ * 61-64); libFLAC / torchaudio are absent here.  ou_flac_info parses
+ * STREAMINFO (frames = total samples per channel; counted by a decode pass
+ * when STREAMINFO leaves it 0).  ou_flac_decode writes planar float32
+ * out[c * frames + i] = sample / 2^(bps-1) (torchaudio.load's scaling) and
+ * returns the frames decoded, or < 0 (ou_last_error) on a malformed stream or
+ * a CRC-8 / CRC-16 mismatch. */
+int ou_flac_info(const uint8_t* data, int64_t n, int32_t* sample_rate, int32_t* channels,
+                 int32_t* bits_per_sample, int64_t* frames);
+int64_t ou_flac_decode(const uint8_t* data, int64_t n, float* out, int64_t frames);
+
 /* Alias-free Snake of the signal-decoupling layer (universe_gan.py:119-151;
  * bigvgan/snake.py:131-157, alias_free_act.py:8-30): torchaudio-style 2x
  * sinc up-sampling, Snake x + sin^2(a x)/(a + 1e-9), 2x down-sampling.  The

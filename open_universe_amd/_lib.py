@@ -188,6 +188,9 @@ EXPORTS = {
     "ou_block": (c_int, [POINTER(BlockDesc), c_void_p]),
     "ou_resample": (c_int, [fp, c_int64, fp, c_int64, c_int, c_int, c_int, fp, c_int, c_int, c_int, c_int,
                             c_void_p]),
+    "ou_flac_info": (c_int, [c_void_p, c_int64, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32),
+                             POINTER(c_int64)]),
+    "ou_flac_decode": (c_int64, [c_void_p, c_int64, c_void_p, c_int64]),
     "ou_program_create": (c_void_p, []),
     "ou_program_destroy": (None, [c_void_p]),
     "ou_program_add": (c_int, [c_void_p, c_int, c_void_p, c_size_t]),

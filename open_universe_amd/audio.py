@@ -6,10 +6,12 @@ The reference CLI reads files with ``torchaudio.load``, resamples with
 
 * ``resample`` runs on the GPU (``ou_resample``, csrc/ou_audio.hip) with
   torchaudio's default polyphase windowed-sinc table (``dsp.sinc_resample_kernel``);
-* ``load_audio`` / ``save_audio`` read and write WAV (torchaudio is not in this
-  image; mp3/flac decoding is out of scope) with torchaudio's normalisation of
-  integer PCM to float32 in [-1, 1).
+* ``load_audio`` reads WAV (scipy) and FLAC (``ou_flac_decode``, a native
+  decoder in csrc/ou_flac.cpp: libFLAC and torchaudio are not in this image)
+  with torchaudio's normalisation of integer PCM to float32 in [-1, 1);
+  ``save_audio`` writes WAV.  mp3 stays out of scope (no decoder here).
 """
+import ctypes
 import math
 
 import numpy as np
@@ -49,10 +51,32 @@ def resample(x: torch.Tensor, orig_freq: int, new_freq: int) -> torch.Tensor:
     return y.reshape(shape[:-1] + (n_out,))
 
 
+def load_flac(path):
+    """(channels, frames) float32 tensor and the sample rate of a FLAC file,
+    scaled as ``torchaudio.load`` scales integer PCM (sample / 2^(bps-1))."""
+    lib = L.load()
+    with open(path, "rb") as fh:
+        data = fh.read()
+    buf = ctypes.create_string_buffer(data, len(data))
+    fs, ch, bps, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+    L.check(lib.ou_flac_info(buf, len(data), ctypes.byref(fs), ctypes.byref(ch), ctypes.byref(bps),
+                             ctypes.byref(n)), f"flac {path}")
+    out = np.zeros((ch.value, n.value), dtype=np.float32)
+    got = lib.ou_flac_decode(buf, len(data), out.ctypes.data, n.value)
+    if got < 0:
+        L.check(int(got), f"flac {path}")
+    if got != n.value:
+        raise L.OuHipError(f"flac {path}: decoded {got} frames, STREAMINFO says {n.value}")
+    return torch.from_numpy(out), int(fs.value)
+
+
 def load_audio(path):
     """(channels, frames) float32 tensor and the sample rate, as
-    ``torchaudio.load(path)`` returns them for a WAV file."""
+    ``torchaudio.load(path)`` returns them for a WAV or FLAC file."""
     from scipy.io import wavfile
+
+    if str(path).lower().endswith(".flac"):
+        return load_flac(path)
 
     fs, data = wavfile.read(str(path))
     if data.dtype == np.int16:

@@ -1,12 +1,13 @@
 #!/usr/bin/env python
-"""Enhance a WAV file or a folder of WAV files (mirrors the reference's
+"""Enhance a WAV / FLAC file or a folder of them (mirrors the reference's
 open_universe/bin/enhance.py:1-192): same positional arguments, ``--model``,
 ``--model-strict``, ``--seed``, ``--device`` and the ``enhance()`` options
 added from the model's signature (``inference_utils.add_enhance_arguments``).
 The folder structure is kept.
 
 Differences: audio is resampled to ``model.fs`` and back on the GPU
-(``audio.resample``); only WAV is read; the model must be a local checkpoint
+(``audio.resample``); WAV and FLAC are read (FLAC by the native decoder,
+``audio.load_flac``), mp3 is not; the model must be a local checkpoint
 (the Hugging Face hub needs the network).  Files are enhanced in groups of
 ``--chunk`` with ``--streams`` clips in flight (Universe.enhance_many; the
 noise of each file is drawn in file order from the one seeded generator).  Under torchrun (WORLD_SIZE > 1)
@@ -27,7 +28,7 @@ from open_universe_amd import inference_utils
 from open_universe_amd.audio import load_audio, resample, save_audio
 from open_universe_amd.sharding import dist_env, shard_utterances
 
-AUDIO_SUFFIXES = [".wav"]
+AUDIO_SUFFIXES = [".wav", ".flac"]
 
 
 def find_files(path):

@@ -20,6 +20,7 @@ cc() {   # cc <src> <obj> [extra flags...]
 for s in ou_gru.hip ou_misc.hip ou_program.hip ou_audio.hip ou_block.hip; do
   cc "$s" "${s%.hip}.o"
 done
+cc ou_flac.cpp ou_flac.o   # host-only (FLAC input decoding for the CLI)
 if [[ "${OUHIP_CFLAGS:-}" == *OU_CONV_STAMPS* ]]; then
   cc ou_conv.hip ou_conv.o
 else
