@@ -287,6 +287,13 @@ int ou_resample(const float* x, int64_t x_bstride, float* y, int64_t y_bstride, 
 int ou_flac_info(const uint8_t* data, int64_t n, int32_t* sample_rate, int32_t* channels,
                  int32_t* bits_per_sample, int64_t* frames);
 int64_t ou_flac_decode(const uint8_t* data, int64_t n, float* out, int64_t frames);
+/* FLAC output (a .flac input is written back as .flac, as torchaudio.save
+ * does): x planar float32 [channels][frames], PCM of bps = 16 or 24 bits
+ * (round(x * 2^(bps-1)), clamped), FIXED-2 / VERBATIM subframes, CRCs set.
+ * Returns the bytes written (<= ou_flac_encode_bound) or < 0. */
+int64_t ou_flac_encode_bound(int channels, int64_t frames, int bps);
+int64_t ou_flac_encode(const float* x, int channels, int64_t frames, int sample_rate, int bps, uint8_t* out,
+                       int64_t capacity);
 
 /* Alias-free Snake of the signal-decoupling layer (universe_gan.py:119-151;
  * bigvgan/snake.py:131-157, alias_free_act.py:8-30): torchaudio-style 2x

@@ -191,6 +191,8 @@ EXPORTS = {
     "ou_flac_info": (c_int, [c_void_p, c_int64, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32),
                              POINTER(c_int64)]),
     "ou_flac_decode": (c_int64, [c_void_p, c_int64, c_void_p, c_int64]),
+    "ou_flac_encode_bound": (c_int64, [c_int, c_int64, c_int]),
+    "ou_flac_encode": (c_int64, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p, c_int64]),
     "ou_program_create": (c_void_p, []),
     "ou_program_destroy": (None, [c_void_p]),
     "ou_program_add": (c_int, [c_void_p, c_int, c_void_p, c_size_t]),

@@ -9,7 +9,8 @@ The reference CLI reads files with ``torchaudio.load``, resamples with
 * ``load_audio`` reads WAV (scipy) and FLAC (``ou_flac_decode``, a native
   decoder in csrc/ou_flac.cpp: libFLAC and torchaudio are not in this image)
   with torchaudio's normalisation of integer PCM to float32 in [-1, 1);
-  ``save_audio`` writes WAV.  mp3 stays out of scope (no decoder here).
+  ``save_audio`` writes WAV, or 24-bit FLAC for a .flac path (``ou_flac_encode``).
+  mp3 stays out of scope (no decoder here).
 """
 import ctypes
 import math
@@ -91,11 +92,30 @@ def load_audio(path):
     return torch.from_numpy(np.ascontiguousarray(x)), int(fs)
 
 
+def save_flac(path, x: torch.Tensor, fs: int, bits: int = 24):
+    """Write (channels, frames) or (frames,) as a FLAC file of ``bits``-bit
+    PCM (``ou_flac_encode``)."""
+    lib = L.load()
+    a = x.detach().to("cpu", torch.float32).numpy()
+    a = np.ascontiguousarray(a[None] if a.ndim == 1 else a)
+    ch, n = a.shape
+    cap = lib.ou_flac_encode_bound(ch, n, bits)
+    buf = (ctypes.c_uint8 * cap)()
+    got = lib.ou_flac_encode(a.ctypes.data, ch, n, int(fs), bits, buf, cap)
+    if got < 0:
+        L.check(int(got), f"flac {path}")
+    with open(path, "wb") as fh:
+        fh.write(bytes(buf)[:got])
+
+
 def save_audio(path, x: torch.Tensor, fs: int):
-    """Write (channels, frames) or (frames,) as a 32-bit float WAV (what
-    ``torchaudio.save`` writes for a float32 tensor)."""
+    """Write (channels, frames) or (frames,): a 32-bit float WAV (what
+    ``torchaudio.save`` writes for a float32 tensor), or 24-bit FLAC for a
+    ``.flac`` path."""
     from scipy.io import wavfile
 
+    if str(path).lower().endswith(".flac"):
+        return save_flac(path, x, fs)
     a = x.detach().to("cpu", torch.float32).numpy()
     if a.ndim == 2:
         a = a.T if a.shape[0] > 1 else a[0]

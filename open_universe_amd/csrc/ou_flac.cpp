@@ -13,6 +13,8 @@
 // stereo decorrelation modes, and both checksums (header CRC-8, frame
 // CRC-16): a damaged stream fails loudly instead of decoding to noise.
 #include <cstdint>
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -272,7 +274,141 @@ int64_t decode(const uint8_t* d, int64_t n, const StreamInfo& si, float* out, in
     return done;
 }
 
+
+// ---------------------------------------------------------------------------
+// Encoder (the CLI writes a .flac output for a .flac input, as torchaudio.save
+// does): PCM of bps bits (x * 2^(bps-1), rounded, clamped), blocks of 4096
+// frames, independent channels, each subframe FIXED order 2 with one Rice
+// partition, or VERBATIM when that is not smaller; STREAMINFO carries the
+// total and a zero MD5 ("not computed", allowed by RFC 9639).
+struct BitOut {
+    std::vector<uint8_t> b;
+    uint64_t acc = 0;
+    int nacc = 0;
+    void put(uint64_t v, int k)
+    {
+        for (int i = k - 1; i >= 0; --i) {
+            acc = (acc << 1) | ((v >> i) & 1);
+            if (++nacc == 8) { b.push_back((uint8_t)acc); acc = 0; nacc = 0; }
+        }
+    }
+    void zeros(uint64_t q) { for (uint64_t i = 0; i < q; ++i) put(0, 1); }
+    void align() { while (nacc) put(0, 1); }
+};
+
+constexpr int kEncBlock = 4096;
+
+void put_utf8(BitOut& o, uint32_t n)
+{
+    if (n < 0x80) { o.put(n, 8); return; }
+    int nb = 2;
+    while (nb < 7 && n >= (1u << (5 * nb + 1))) ++nb;
+    o.put(((0xFFu << (8 - nb)) & 0xFF) | (n >> (6 * (nb - 1))), 8);
+    for (int i = nb - 2; i >= 0; --i) o.put(0x80 | ((n >> (6 * i)) & 0x3F), 8);
+}
+
+void enc_subframe(BitOut& o, const int32_t* s, int n, int bps)
+{
+    // FIXED order 2 residual and its Rice cost for the best parameter
+    std::vector<uint32_t> u;
+    uint64_t sum = 0;
+    if (n > 2) {
+        u.resize(n - 2);
+        for (int i = 2; i < n; ++i) {
+            const int64_t r = (int64_t)s[i] - (2 * (int64_t)s[i - 1] - s[i - 2]);
+            const uint64_t z = r >= 0 ? (uint64_t)r << 1 : ((uint64_t)(-r) << 1) - 1;
+            u[i - 2] = z > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)z;
+            sum += u[i - 2];
+        }
+    }
+    int k = 0;
+    if (!u.empty()) {
+        const uint64_t mean = sum / u.size();
+        while (k < 30 && (1ull << (k + 1)) <= mean) ++k;
+    }
+    uint64_t bits = 2 * (uint64_t)bps + 2 + 4 + 5;
+    for (uint32_t v : u) bits += (v >> k) + 1 + k;
+    const bool fixed = n > 2 && bits < (uint64_t)n * bps;
+    o.put(0, 1);
+    o.put(fixed ? 8 + 2 : 1, 6);
+    o.put(0, 1);   // no wasted bits
+    if (!fixed) {
+        for (int i = 0; i < n; ++i) o.put((uint32_t)s[i], bps);
+        return;
+    }
+    o.put((uint32_t)s[0], bps);
+    o.put((uint32_t)s[1], bps);
+    o.put(1, 2);   // 5-bit Rice parameters
+    o.put(0, 4);   // one partition
+    o.put(k, 5);
+    for (uint32_t v : u) {
+        o.zeros(v >> k);
+        o.put(1, 1);
+        o.put(v, k);
+    }
+}
+
 }  // namespace
+
+extern "C" int64_t ou_flac_encode_bound(int channels, int64_t frames, int bps)
+{
+    const int64_t blocks = (frames + kEncBlock - 1) / kEncBlock;
+    return 42 + blocks * (20 + (int64_t)channels * 8) + (int64_t)channels * frames * ((bps + 7) / 8);
+}
+
+extern "C" int64_t ou_flac_encode(const float* x, int channels, int64_t frames, int sample_rate, int bps,
+                                  uint8_t* out, int64_t capacity)
+{
+    if (!x || !out || channels < 1 || channels > 8 || frames < 1 || (bps != 16 && bps != 24) ||
+        sample_rate < 1 || sample_rate >= (1 << 20))
+        return ou_fail(-1, "flac encode: bad args");
+    BitOut o;
+    o.b.reserve((size_t)std::min<int64_t>(capacity, ou_flac_encode_bound(channels, frames, bps)));
+    for (const char* m = "fLaC"; *m; ++m) o.put((uint8_t)*m, 8);
+    o.put(0x80, 8);   // last metadata block, STREAMINFO
+    o.put(34, 24);
+    const int first = (int)std::min<int64_t>(frames, kEncBlock);
+    o.put(frames <= kEncBlock ? first : kEncBlock, 16);
+    o.put(first, 16);
+    o.put(0, 24);
+    o.put(0, 24);
+    o.put(sample_rate, 20);
+    o.put(channels - 1, 3);
+    o.put(bps - 1, 5);
+    o.put((uint64_t)frames, 36);
+    for (int i = 0; i < 16; ++i) o.put(0, 8);
+    const double full = (double)(1 << (bps - 1));
+    const int32_t lo = -(1 << (bps - 1)), hi = (1 << (bps - 1)) - 1;
+    std::vector<int32_t> s(kEncBlock);
+    uint32_t fno = 0;
+    for (int64_t t0 = 0; t0 < frames; t0 += kEncBlock, ++fno) {
+        const int n = (int)std::min<int64_t>(kEncBlock, frames - t0);
+        const size_t start = o.b.size();
+        o.put(0x3FFE, 14);
+        o.put(0, 2);
+        o.put(n == kEncBlock ? 12 : 7, 4);   // 4096 from the table, else 16-bit n - 1
+        o.put(0, 4);                         // sample rate from STREAMINFO
+        o.put(channels - 1, 4);
+        o.put(bps == 16 ? 4 : 6, 3);
+        o.put(0, 1);
+        put_utf8(o, fno);
+        if (n != kEncBlock) o.put(n - 1, 16);
+        o.put(crc8(o.b.data() + start, (int64_t)(o.b.size() - start)), 8);
+        for (int c = 0; c < channels; ++c) {
+            for (int i = 0; i < n; ++i) {
+                const double v = std::nearbyint((double)x[(int64_t)c * frames + t0 + i] * full);
+                s[i] = (int32_t)std::max<double>(lo, std::min<double>(hi, v));
+            }
+            enc_subframe(o, s.data(), n, bps);
+        }
+        o.align();
+        const uint16_t crc = crc16(o.b.data() + start, (int64_t)(o.b.size() - start));
+        o.put(crc, 16);
+    }
+    if ((int64_t)o.b.size() > capacity) return ou_fail(-2, "flac encode: output needs %lld bytes", (long long)o.b.size());
+    std::memcpy(out, o.b.data(), o.b.size());
+    return (int64_t)o.b.size();
+}
 
 extern "C" int ou_flac_info(const uint8_t* data, int64_t n, int32_t* sample_rate, int32_t* channels,
                             int32_t* bits_per_sample, int64_t* frames)

@@ -107,3 +107,38 @@ def test_cli_lists_flac_inputs(tmp_path):
     from open_universe_amd.bin import enhance as cli
 
     assert ".flac" in cli.AUDIO_SUFFIXES
+
+
+@pytest.mark.parametrize("ch,n,bits", [(1, 1, 16), (1, 4096, 24), (2, 10000, 16), (2, 12345, 24)])
+def test_encoder_round_trip(tmp_path, ch, n, bits):
+    """ou_flac_encode (the CLI's .flac output) -> ou_flac_decode: the PCM the
+    encoder quantised comes back exactly (block sizes from the table and
+    explicit 16-bit ones; FIXED-2 and VERBATIM subframes)."""
+    import torch
+
+    rng = np.random.default_rng(n)
+    t = np.arange(n)
+    x = np.stack([0.5 * np.sin(2 * np.pi * 0.013 * (c + 1) * t) for c in range(ch)])
+    if n > 100:
+        x[:, 50:100] = rng.uniform(-1.2, 1.2, (ch, 50))   # noise burst + clipping: VERBATIM blocks
+    x = x.astype(np.float32)
+    p = tmp_path / "o.flac"
+    audio.save_audio(p, torch.from_numpy(x), 22050)
+    y, fs = audio.load_audio(p)
+    full = float(1 << (bits - 1)) if bits == 24 else None
+    q = np.clip(np.rint(x.astype(np.float64) * (1 << (bits - 1))), -(1 << (bits - 1)), (1 << (bits - 1)) - 1)
+    if bits == 24:   # save_audio writes 24-bit
+        assert fs == 22050 and y.shape == (ch, n)
+        np.testing.assert_array_equal(y.numpy(), (q / full).astype(np.float32))
+    else:
+        from open_universe_amd import _lib as LL
+        import ctypes
+
+        lib = LL.load()
+        a = np.ascontiguousarray(x)
+        cap = lib.ou_flac_encode_bound(ch, n, 16)
+        buf = (ctypes.c_uint8 * cap)()
+        got = lib.ou_flac_encode(a.ctypes.data, ch, n, 22050, 16, buf, cap)
+        assert 0 < got <= cap
+        y16, _ = _decode(tmp_path, bytes(buf)[:got], "o16.flac")
+        np.testing.assert_array_equal(y16, (q / 32768.0).astype(np.float32))

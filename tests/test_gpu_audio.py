@@ -76,3 +76,26 @@ def test_enhance_cli_end_to_end(tmp_path):
     a, _ = load_audio(outs[0])
     b, _ = load_audio(outs[1])
     assert torch.equal(a, b)
+
+
+def test_enhance_cli_flac_in_flac_out(tmp_path):
+    """A .flac input (decoded by ou_flac_decode) is enhanced and written back
+    as .flac (ou_flac_encode), as the reference does through torchaudio."""
+    import torch
+
+    from open_universe_amd.bin import enhance as cli
+    from test_api_surface import _write_ckpt
+
+    ckpt, _, _, _ = _write_ckpt(str(tmp_path), with_ema=False)
+    src = tmp_path / "noisy"
+    src.mkdir()
+    rng = np.random.default_rng(3)
+    save_audio(src / "c.flac", torch.from_numpy((rng.standard_normal(20000) * 0.1).astype(np.float32)), 24000)
+    x, fs = load_audio(src / "c.flac")
+    assert fs == 24000 and x.shape == (1, 20000)
+    out = tmp_path / "enh"
+    assert cli.main([str(src), str(out), "--model", ckpt, "--n_steps", "2", "--seed", "7"]) == 0
+    assert (out / "c.flac").read_bytes()[:4] == b"fLaC"
+    y, fs_out = load_audio(out / "c.flac")
+    assert fs_out == 24000 and y.shape[0] == 1 and abs(y.shape[-1] - 20000) <= 3
+    assert torch.isfinite(y).all() and y.abs().max() > 0
