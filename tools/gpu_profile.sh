@@ -24,6 +24,8 @@ python3 "$ROOT/tools/pmc_summary.py" --tag "$TAG" --enhances 2 --out "$O/pmc_$TA
     "$(find "$O/pmcf_$TAG" -name '*counter_collection.csv' | head -n1)" \
     "$(find "$O/pmcw_$TAG" -name '*counter_collection.csv' | head -n1)" > /dev/null
 rc=$?
+[ "$rc" -eq 0 ] && python3 "$ROOT/tools/trace_gaps.py" "$(find "$O/kt_$TAG" -name '*kernel_trace.csv' | head -n1)" \
+    > "$O/trace_gaps_$TAG.txt"
 cat "$O/bench_$TAG.json"
 find "$O/kt_$TAG" -name '*kernel_stats.csv' -exec head -n 12 {} \;
 exit $rc
