@@ -51,6 +51,16 @@ F16_PEAK_TF = 2516.6   # dense F16/BF16 MFMA peak; split-f16 spends 3 MFMAs per 
 HBM_PEAK = 8000.0      # GB/s
 
 
+def lib_sha16():
+    """Hash of the libouhip.so this process loads (ties PMC counters to a build)."""
+    import hashlib
+
+    from open_universe_amd import _lib as L
+
+    with open(L.LIB_PATH, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -73,27 +83,30 @@ CONFIGS = {
     "c3": dict(arch="orig16", batch=8, seconds=8.0, n_steps=60,
                workload="UNIVERSE (original) 16 kHz enhance(), batch=8, 8 s clips, 60 diffusion steps "
                         "(BASELINE.json configs[2])"),
-    "c4": dict(arch="pp24", batch=32, seconds=10.0, n_steps=None, node_batch=True,
+    # c4 runs the damped synthetic family (utils/synthetic.py RC_DAMP): with
+    # g ~ 1 on the anti-aliased rate changes PP24's activations reach 7.7e6 in
+    # the reference itself and the split-f16 operands would fall back to f32
+    "c4": dict(arch="pp24", batch=32, seconds=10.0, n_steps=None, node_batch=True, damped=True,
                workload="UNIVERSE++ 24 kHz enhance(), batch=32 per node sharded over the GPUs, 10 s clips, "
-                        "8 diffusion steps (BASELINE.json configs[3])"),
+                        "8 diffusion steps (BASELINE.json configs[3]); damped synthetic weights"),
     "c5": dict(arch="pp16", batch=1, seconds=60.0, n_steps=None, conv_prec="f16",
                workload="UNIVERSE++ 16 kHz enhance(), batch=1, 60 s long-form clip, 8 diffusion steps, fp16 conv "
                         "operands, whole sampler captured in one hipGraph (BASELINE.json configs[4])"),
 }
 
 
-def build_model(device, nch=None, seed=0, arch="pp16"):
+def build_model(device, nch=None, seed=0, arch="pp16", damped=False):
     import torch
 
     from open_universe_amd.configs import get_config
     from open_universe_amd.networks.universe import Universe, UniverseGAN
-    from open_universe_amd.utils.synthetic import synth_state_dict
+    from open_universe_amd.utils.synthetic import RC_DAMP, synth_state_dict
 
     cfg = get_config(arch, nch)
     cls = Universe if cfg["_target_"].endswith(".Universe") else UniverseGAN
     m = cls(**{k: v for k, v in cfg.items() if k != "_target_"})
-    m.load_state_dict(synth_state_dict([(k, v.shape) for k, v in m.state_dict().items()], seed),
-                      strict=False)
+    m.load_state_dict(synth_state_dict([(k, v.shape) for k, v in m.state_dict().items()], seed,
+                                       RC_DAMP if damped else 1.0), strict=False)
     return cfg, m.to(device).eval()
 
 
@@ -331,7 +344,7 @@ def main():
     dev = torch.device("cuda", gpu)
     if C.get("conv_prec") and "OUHIP_CONV_PREC" not in os.environ:
         os.environ["OUHIP_CONV_PREC"] = C["conv_prec"]
-    cfg, model = build_model(dev, arch=C["arch"])
+    cfg, model = build_model(dev, arch=C["arch"], damped=C.get("damped", False))
     fs = int(cfg["fs"])
     T = int(args.seconds * fs)
     n_clips = args.warmup + args.steps
@@ -356,8 +369,8 @@ def main():
     prec = model._get_engine().conv_prec
     # the strictly-f32 figure: a second timed pass with f32 conv operands
     f32 = None
-    if prec != 0 and not args.no_f32_pass and args.config == "c2":
-        _, m32 = build_model(dev, arch=C["arch"])
+    if prec != 0 and not args.no_f32_pass and args.config in ("c2", "c4"):
+        _, m32 = build_model(dev, arch=C["arch"], damped=C.get("damped", False))
         m32._conv_prec = 0
         with torch.no_grad():
             e32 = timed_loop(lambda i: m32.enhance(clips[i % len(clips)], rng=rng, **ekw),
@@ -414,7 +427,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": dtype,
-            "data": "synthetic (16 kHz harmonic+noise clips, seeded synthetic weights)",
+            "data": "synthetic (harmonic+noise clips, seeded synthetic weights%s)"
+                    % (", damped family" if C.get("damped") else ""),
             "config": {"workload": C["workload"],
                        "model": {"pp16": "UniverseGAN PP16 (42.85 M params)", "orig16": "Universe ORIG16 (43.0 M params)",
                                  "pp24": "UniverseGAN PP24 (107.5 M params)"}[C["arch"]],
@@ -443,14 +457,23 @@ def main():
                 with open(args.traffic_json) as fh:
                     pmc = json.load(fh)
                 rows = [r for k, r in pmc.get("kernels", {}).items() if k in ("conv_kernel", "conv_rkernel", "block_kernel")]
+                lib_now = lib_sha16()
+                if pmc.get("lib_sha16") != lib_now:
+                    # counters of another build of the kernels: not quoted
+                    rows = []
+                    tsrc = (f"null: {os.path.relpath(args.traffic_json, HERE)} was counted on libouhip.so "
+                            f"{pmc.get('lib_sha16')}, this run loads {lib_now} (re-run tools/gpu_profile.sh)")
+                elif pmc.get("config", "c2") != args.config:
+                    tsrc = f"null: the PMC passes profiled --config {pmc.get('config', 'c2')}, not {args.config}"
                 if rows and pmc.get("config", "c2") == args.config and pmc.get("enhances_profiled"):
                     # bytes of every conv-stack dispatch of one enhance, per
                     # recorded conv op (K-slice ops dispatch twice)
                     tot = sum(r["traffic_bytes_per_launch"] * r["dispatches"] for r in rows)
                     traffic = round(tot / pmc["enhances_profiled"] / prof["n_conv"])
                     per = "conv-stack op (ou_conv incl. both launches of K-slice ops, ou_block)"
-                    tsrc = (f"{os.path.relpath(args.traffic_json, HERE)} ({pmc.get('tag', '')}): "
-                            f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes per {per}")
+                    tsrc = (f"{os.path.relpath(args.traffic_json, HERE)} ({pmc.get('tag', '')}, libouhip.so "
+                            f"{lib_now}, the library this run loaded): rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
+                            f"bytes per {per}")
             if t_hbm > t_mfma:
                 rl = {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK, "peak_basis": "HBM3E",
                       "unit": "GB/s", "frac": round(gbps / HBM_PEAK, 4),

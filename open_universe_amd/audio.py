@@ -71,6 +71,32 @@ def load_flac(path):
     return torch.from_numpy(out), int(fs.value)
 
 
+def audio_info(path):
+    """(channels, frames, sample rate) of a WAV or FLAC file without decoding
+    it (torchaudio.info's num_channels / num_frames / sample_rate)."""
+    if str(path).lower().endswith(".flac"):
+        lib = L.load()
+        with open(path, "rb") as fh:
+            data = fh.read()
+        buf = ctypes.create_string_buffer(data, len(data))
+        fs, ch, bps, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        L.check(lib.ou_flac_info(buf, len(data), ctypes.byref(fs), ctypes.byref(ch), ctypes.byref(bps),
+                                 ctypes.byref(n)), f"flac {path}")
+        return int(ch.value), int(n.value), int(fs.value)
+    from scipy.io import wavfile
+
+    fs, data = wavfile.read(str(path), mmap=True)
+    return (data.shape[1] if data.ndim > 1 else 1), int(data.shape[0]), int(fs)
+
+
+def resampled_len(n, orig_freq, new_freq):
+    """Output length of ``resample`` (ceil(new * n / orig) in lowest terms)."""
+    if orig_freq == new_freq:
+        return n
+    g = math.gcd(int(orig_freq), int(new_freq))
+    return int(math.ceil((new_freq // g) * n / (orig_freq // g)))
+
+
 def load_audio(path):
     """(channels, frames) float32 tensor and the sample rate, as
     ``torchaudio.load(path)`` returns them for a WAV or FLAC file."""

@@ -9,10 +9,17 @@ Differences: audio is resampled to ``model.fs`` and back on the GPU
 (``audio.resample``); WAV and FLAC are read (FLAC by the native decoder,
 ``audio.load_flac``), mp3 is not; the model must be a local checkpoint
 (the Hugging Face hub needs the network).  Files are enhanced in groups of
-``--chunk`` with ``--streams`` clips in flight (Universe.enhance_many; the
-noise of each file is drawn in file order from the one seeded generator).  Under torchrun (WORLD_SIZE > 1)
-each rank enhances its share of the files on ``cuda:LOCAL_RANK``
-(``sharding.shard_utterances``, balanced by file size) -- no collectives.
+``--chunk`` with ``--streams`` clips in flight (Universe.enhance_many).  Under
+torchrun (WORLD_SIZE > 1) each rank enhances its share of the files on
+``cuda:LOCAL_RANK`` (``sharding.shard_utterances``, balanced by file size) --
+no collectives.
+
+Noise: as in the reference (bin/enhance.py:71-73,147-148,173-189), one
+generator seeded with ``--seed`` draws every file's noise in the order
+``rglob`` lists the files (suffix matched case-sensitively).  A rank draws and
+discards the noise of the files other ranks enhance (``Universe.skip_noise``,
+from the file headers), so every file gets the same noise -- and the same
+output -- whatever the world size.
 
     python -m open_universe_amd.bin.enhance noisy/ enhanced/ --model exp/ckpt.ckpt
     python -m torch.distributed.run --nproc-per-node 8 -m open_universe_amd.bin.enhance noisy/ out/ --model ...
@@ -25,17 +32,18 @@ from pathlib import Path
 import torch
 
 from open_universe_amd import inference_utils
-from open_universe_amd.audio import load_audio, resample, save_audio
+from open_universe_amd.audio import audio_info, load_audio, resample, resampled_len, save_audio
 from open_universe_amd.sharding import dist_env, shard_utterances
 
 AUDIO_SUFFIXES = [".wav", ".flac"]
 
 
 def find_files(path):
-    """(files, root, is_dir) as bin/enhance.py:46-58."""
+    """(files, root, is_dir) as bin/enhance.py:46-58: rglob order, suffix
+    matched case-sensitively (the order fixes which noise each file gets)."""
     if not path.is_dir():
         return [path], path.parent, False
-    return sorted(p for p in path.rglob("*") if p.suffix.lower() in AUDIO_SUFFIXES), path, True
+    return [p for p in path.rglob("*") if p.suffix in AUDIO_SUFFIXES], path, True
 
 
 def main(argv=None):
@@ -59,7 +67,7 @@ def main(argv=None):
     torch.cuda.set_device(torch.device(device))
     model = inference_utils.load_model(args.model, device=device, strict=args.model_strict)
     rng = torch.Generator(device=device)
-    rng.manual_seed(args.seed + rank)
+    rng.manual_seed(args.seed)
 
     inference_utils.add_enhance_arguments(model, parser)
     args = parser.parse_args(argv)
@@ -68,10 +76,25 @@ def main(argv=None):
     enhance_kwargs = dict(groups.get("enhance", {}))
     enhance_kwargs["rng"] = rng
 
-    files, root, is_dir = find_files(args.input)
+    all_files, root, is_dir = find_files(args.input)
+    mine = list(range(len(all_files)))
     if world > 1:
-        mine = shard_utterances([p.stat().st_size for p in files], world)[rank]
-        files = [files[i] for i in mine]
+        mine = shard_utterances([p.stat().st_size for p in all_files], world)[rank]
+    files = [all_files[i] for i in mine]
+    # the files before each of mine (in the global order) that other ranks
+    # enhance: their noise is drawn and discarded right before mine
+    skip_before, prev = [], -1
+    for i in mine:
+        skip_before.append(all_files[prev + 1:i])
+        prev = i
+    noise_kw = {k: enhance_kwargs.get(k) for k in ("n_steps", "target", "use_aux_signal", "ensemble",
+                                                  "warm_start")}
+
+    def skip(paths):
+        for p in paths:
+            ch, n, fs = audio_info(p)
+            model.skip_noise((ch, resampled_len(n, fs, model.fs)), rng, **noise_kw)
+
     def out_path(path):
         if is_dir:
             return args.output / path.relative_to(root)
@@ -92,9 +115,13 @@ def main(argv=None):
         with torch.no_grad():
             xs = [resample(a.to(device), fs, model.fs) for a, fs in loaded]
             if many_ok:
-                ys = model.enhance_many(xs, streams=args.streams, **many_kw)
+                ys = model.enhance_many(xs, streams=args.streams, pre_noise=lambda j: skip(skip_before[i + j]),
+                                        **many_kw)
             else:
-                ys = [model.enhance(x, **enhance_kwargs) for x in xs]
+                ys = []
+                for j, x in enumerate(xs):
+                    skip(skip_before[i + j])
+                    ys.append(model.enhance(x, **enhance_kwargs))
             ys = [resample(y, model.fs, fs) for y, (_, fs) in zip(ys, loaded)]
         for path, y, (_, fs) in zip(group, ys, loaded):
             out = out_path(path)

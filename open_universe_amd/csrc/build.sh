@@ -9,11 +9,15 @@ OUT="${1:-$HERE/../libouhip.so}"
 ARCH="${OUHIP_ARCH:-gfx950}"
 OBJDIR="$HERE/build${OUHIP_BUILD_TAG:-}"
 mkdir -p "$OBJDIR"
-rm -f "$OBJDIR"/*.o
+# OUHIP_INCREMENTAL=1 (development): keep objects newer than their source and
+# the shared headers; the default rebuilds everything
+[ "${OUHIP_INCREMENTAL:-0}" = 1 ] || rm -f "$OBJDIR"/*.o
 CFLAGS=(--offload-arch="$ARCH" -O3 -fPIC -std=c++17 -Wall -Wno-unused-function)
 pids=()
 cc() {   # cc <src> <obj> [extra flags...]
   local src="$1" obj="$2"; shift 2
+  if [ -f "$OBJDIR/$obj" ] && [ "$OBJDIR/$obj" -nt "$HERE/$src" ] && [ "$OBJDIR/$obj" -nt "$HERE/ou_common.h" ] \
+     && [ "$OBJDIR/$obj" -nt "$HERE/../../include/ouhip.h" ]; then return 0; fi
   /opt/rocm/bin/hipcc "${CFLAGS[@]}" ${OUHIP_CFLAGS:-} "$@" -c "$HERE/$src" -o "$OBJDIR/$obj" &
   pids+=($!)
 }

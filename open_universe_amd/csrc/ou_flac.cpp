@@ -46,6 +46,13 @@ struct Bits {
         if (k == 32) return (int32_t)v;
         return (int32_t)(v << (32 - k)) >> (32 - k);
     }
+    int64_t get_signed64(int k)   // k <= 33 (a 32-bit stream's side channel)
+    {
+        if (k <= 32) return get_signed(k);
+        const uint64_t hi = get(k - 32), lo = get(32);
+        const uint64_t v = (hi << 32) | lo;
+        return (int64_t)(v << (64 - k)) >> (64 - k);
+    }
     uint32_t unary()   // count of 0 bits before the next 1
     {
         uint32_t q = 0;
@@ -120,7 +127,7 @@ int parse_header(const uint8_t* d, int64_t n, StreamInfo& si)
 }
 
 // residual of one subframe into r[order ..] (r[0 .. order) holds the warm-up)
-bool residual(Bits& b, int bsize, int order, int32_t* r)
+bool residual(Bits& b, int bsize, int order, int64_t* r)
 {
     const int method = (int)b.get(2);
     if (method > 1) return false;
@@ -140,7 +147,7 @@ bool residual(Bits& b, int bsize, int order, int32_t* r)
             for (int j = 0; j < cnt; ++j) {
                 const uint32_t q = b.unary();
                 const uint32_t u = (q << k) | b.get((int)k);
-                r[i++] = (int32_t)(u >> 1) ^ -(int32_t)(u & 1);
+                r[i++] = (int64_t)((int32_t)(u >> 1) ^ -(int32_t)(u & 1));
             }
         }
         if (b.bad) return false;
@@ -148,38 +155,39 @@ bool residual(Bits& b, int bsize, int order, int32_t* r)
     return true;
 }
 
-bool subframe(Bits& b, int bsize, int bps, int32_t* s)
+// samples are int64: the side channel of a 32-bit stereo stream needs 33 bits
+bool subframe(Bits& b, int bsize, int bps, int64_t* s)
 {
     if (b.get(1) != 0) return false;
     const int type = (int)b.get(6);
     int wasted = 0;
     if (b.get(1)) wasted = (int)b.unary() + 1;
     const int eb = bps - wasted;
-    if (eb <= 0 || eb > 32) return false;
+    if (eb <= 0 || eb > 33) return false;
     if (type == 0) {   // CONSTANT
-        const int32_t v = b.get_signed(eb);
+        const int64_t v = b.get_signed64(eb);
         for (int i = 0; i < bsize; ++i) s[i] = v;
     } else if (type == 1) {   // VERBATIM
-        for (int i = 0; i < bsize; ++i) s[i] = b.get_signed(eb);
+        for (int i = 0; i < bsize; ++i) s[i] = b.get_signed64(eb);
     } else if (type >= 8 && type <= 12) {   // FIXED, order 0..4
         const int order = type - 8;
         if (order > bsize) return false;
-        for (int i = 0; i < order; ++i) s[i] = b.get_signed(eb);
+        for (int i = 0; i < order; ++i) s[i] = b.get_signed64(eb);
         if (!residual(b, bsize, order, s)) return false;
         for (int i = order; i < bsize; ++i) {
             int64_t p = 0;
             switch (order) {
             case 1: p = s[i - 1]; break;
-            case 2: p = 2 * (int64_t)s[i - 1] - s[i - 2]; break;
-            case 3: p = 3 * (int64_t)s[i - 1] - 3 * (int64_t)s[i - 2] + s[i - 3]; break;
-            case 4: p = 4 * (int64_t)s[i - 1] - 6 * (int64_t)s[i - 2] + 4 * (int64_t)s[i - 3] - s[i - 4]; break;
+            case 2: p = 2 * s[i - 1] - s[i - 2]; break;
+            case 3: p = 3 * s[i - 1] - 3 * s[i - 2] + s[i - 3]; break;
+            case 4: p = 4 * s[i - 1] - 6 * s[i - 2] + 4 * s[i - 3] - s[i - 4]; break;
             }
-            s[i] = (int32_t)(p + s[i]);
+            s[i] = p + s[i];
         }
     } else if (type >= 32) {   // LPC, order 1..32
         const int order = type - 31;
         if (order > bsize) return false;
-        for (int i = 0; i < order; ++i) s[i] = b.get_signed(eb);
+        for (int i = 0; i < order; ++i) s[i] = b.get_signed64(eb);
         const int prec = (int)b.get(4) + 1;
         if (prec == 16) return false;   // 0b1111 is invalid
         const int shift = b.get_signed(5);
@@ -190,13 +198,13 @@ bool subframe(Bits& b, int bsize, int bps, int32_t* s)
         for (int i = order; i < bsize; ++i) {
             int64_t acc = 0;
             for (int j = 0; j < order; ++j) acc += (int64_t)c[j] * s[i - 1 - j];
-            s[i] = (int32_t)((acc >> shift) + s[i]);
+            s[i] = (acc >> shift) + s[i];
         }
     } else {
         return false;   // reserved subframe type
     }
     if (wasted)
-        for (int i = 0; i < bsize; ++i) s[i] = (int32_t)((uint32_t)s[i] << wasted);
+        for (int i = 0; i < bsize; ++i) s[i] = (int64_t)((uint64_t)s[i] << wasted);
     return !b.bad;
 }
 
@@ -206,10 +214,15 @@ const int kSizes[8] = {0, 8, 12, -1, 16, 20, 24, 32};
 int64_t decode(const uint8_t* d, int64_t n, const StreamInfo& si, float* out, int64_t cap)
 {
     int64_t off = si.first_frame, done = 0;
-    std::vector<int32_t> ch[8];
+    std::vector<int64_t> ch[8];
     while (off + 2 <= n) {
-        if (d[off] != 0xFF || (d[off + 1] & 0xFE) != 0xF8)
+        if (d[off] != 0xFF || (d[off + 1] & 0xFE) != 0xF8) {
+            // bytes after the last frame (an ID3v1 'TAG' block, padding):
+            // libFLAC / torchaudio.load stop there once every sample is in
+            if ((si.total > 0 && done >= si.total) || (n - off >= 3 && std::memcmp(d + off, "TAG", 3) == 0))
+                break;
             return ou_fail(-2, "flac: lost frame sync at byte %lld", (long long)off);
+        }
         Bits b{d + off, n - off};
         b.get(16);
         const int bs_code = (int)b.get(4), sr_code = (int)b.get(4);

@@ -649,11 +649,12 @@ class ConvTuner:
         self.path = path
         self.timed = 0   # geometries tuned by timing (not reused from another length)
         self.by_geom = {}   # geometry -> frame-count buckets cached
-        for kk in self.cache:
-            self.by_geom.setdefault(kk[:-1], set()).add(kk[-1])
         if path and os.path.exists(path):
             with open(path) as fh:
                 self.cache = {tuple(json.loads(k)): v for k, v in json.load(fh).items()}
+        # persisted geometries seed the nearest-length reuse too
+        for kk in self.cache:
+            self.by_geom.setdefault(kk[:-1], set()).add(kk[-1])
 
     def _save(self):
         import json

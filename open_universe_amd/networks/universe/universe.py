@@ -84,6 +84,7 @@ class Universe(nn.Module):
         self.ema = None  # EMA weights are applied at load time (inference only)
         self._engine = None
         self._plans = collections.OrderedDict()   # LRU of recorded plans, see _plan()
+        self._inflight = set()   # plan keys submitted by enhance_many and not yet checked
         self._conv_prec = None   # None: OUHIP_CONV_PREC; 0 after a split-f16 range error
 
     def init_losses(self, score_model, condition_model, losses, training):
@@ -132,8 +133,13 @@ class Universe(nn.Module):
             self._plans.move_to_end(key)
             return plan
         cap = max(1, int(os.environ.get("OUHIP_MAX_PLANS", "8")))
+        # plans enhance_many has queued and not yet synchronised are pinned:
+        # their kernels may still read the buffers an eviction would free
         while len(self._plans) >= cap:
-            self._plans.popitem(last=False)
+            victim = next((k for k in self._plans if k not in self._inflight), None)
+            if victim is None:
+                break
+            del self._plans[victim]
         plan = self._plans[key] = make()
         return plan
 
@@ -158,7 +164,13 @@ class Universe(nn.Module):
                     return build(ar)
                 except E.ArenaFull as e:
                     size = max(2 * ar.nbytes, int(e.args[0] * 1.5))
-                    for k in [k for k, p in self._plans.items() if getattr(p, "arena", None) is ar]:
+                    old = [k for k, p in self._plans.items() if getattr(p, "arena", None) is ar]
+                    if any(k in self._inflight for k in old):
+                        # plans of this slot are still queued on its stream:
+                        # their kernels read the arena being replaced
+                        torch.cuda.synchronize(eng.device)
+                        self._inflight.clear()
+                    for k in old:
                         del self._plans[k]
                     arenas[slot] = None
                     del ar
@@ -169,6 +181,7 @@ class Universe(nn.Module):
     def invalidate(self):
         """Drop the packed device weights (call after changing parameters)."""
         self._engine, self._plans = None, collections.OrderedDict()
+        self._inflight = set()
 
     def _apply(self, fn, *args, **kwargs):
         self.invalidate()
@@ -202,6 +215,39 @@ class Universe(nn.Module):
         net = self._edm_model(w_in * x, self.edm_kwargs["noise"] * sigma, cond)
         est = w_skip * x + w_out * net
         return (est - x) / sigma[:, None, None] ** 2
+
+    # ------------------------------------------------------------------ noise
+    def noise_shapes(self, mix_shape, n_steps: Optional[int] = None, target=None, use_aux_signal=False,
+                     ensemble=None, warm_start=None, **_):
+        """The shapes of the ``torch.randn(..., generator=rng)`` draws one
+        ``enhance(mix, ...)`` makes, in draw order (universe.py:39-41,322-343:
+        x0, then one z per intermediate step; the known-answer mode also draws
+        the score noise of every step, :278-298).  Drawing and discarding
+        these advances ``rng`` exactly as that enhance would (bin/enhance.py
+        keeps a multi-rank run's noise assignment equal to the 1-rank run's)."""
+        if n_steps is None:
+            n_steps = self.diff_kwargs.n_steps
+        shape = tuple(mix_shape)
+        if len(shape) == 1:
+            shape = (1, 1) + shape
+        elif len(shape) == 2:
+            shape = (shape[0], 1, shape[1])
+        B, T = shape[0] * (ensemble or 1), shape[-1]
+        Tp = T + self.tot_ds - T % self.tot_ds
+        if target is not None:
+            return [(B, 1, Tp)] * (2 * int(n_steps))
+        if use_aux_signal:
+            return []
+        n_start = 0 if warm_start is None else int(warm_start)
+        return [(B, 1, Tp)] * (1 + (int(n_steps) - 1 - n_start))
+
+    def skip_noise(self, mix_shape, rng, **enhance_kwargs):
+        """Advance ``rng`` past the noise of an ``enhance`` of ``mix_shape``
+        without running it (the draws are made and discarded)."""
+        if rng is None:
+            return
+        for shp in self.noise_shapes(mix_shape, **enhance_kwargs):
+            torch.randn(shp, generator=rng, device=rng.device, dtype=torch.float32)
 
     # ------------------------------------------------------------------ enhance
     def enhance(
@@ -272,14 +318,17 @@ class Universe(nn.Module):
         return x
 
     def enhance_many(self, mixes, n_steps: Optional[int] = None, epsilon: Optional[float] = None,
-                     rng: Optional[torch.Generator] = None, keep_rms: Optional[bool] = False, streams: int = 2):
+                     rng: Optional[torch.Generator] = None, keep_rms: Optional[bool] = False, streams: int = 2,
+                     pre_noise=None):
         """Enhance a sequence of clips (each a (T,), (B, T) or (B, 1, T) device
         tensor, as ``enhance`` takes them) with up to ``streams`` enhances in
         flight at once, on their own HIP streams and plans.  At batch 1 one
         enhance leaves most of the chip idle while its GRUs run (a serial
         801-step chain per clip); a second clip's convolutions fill it.  Each
         clip's result equals ``enhance`` of that clip with the noise drawn in
-        clip order from ``rng``.  Returns the list of outputs."""
+        clip order from ``rng``; ``pre_noise(i)``, if given, runs right before
+        clip i draws its noise (the CLI discards other ranks' draws there).
+        Returns the list of outputs."""
         from ...plan import EnhancePlan
         from ... import engine as E
 
@@ -287,10 +336,15 @@ class Universe(nn.Module):
             epsilon = self.diff_kwargs.epsilon
         if n_steps is None:
             n_steps = self.diff_kwargs.n_steps
+        mixes = list(mixes)
+        if not mixes:
+            return []
         S = max(1, min(int(streams), E.MAX_SLOTS))
         eng = self._get_engine()
-        if not hasattr(self, "_streams") or len(self._streams) < S:
+        streams_dev = getattr(self, "_streams_dev", None)
+        if not hasattr(self, "_streams") or len(self._streams) < S or streams_dev != eng.device:
             self._streams = [torch.cuda.Stream(device=eng.device) for _ in range(S)]
+            self._streams_dev = eng.device
         main = torch.cuda.current_stream(eng.device)
         shapes, outs, pending = [], [], []
         for i, mix in enumerate(mixes):
@@ -309,6 +363,9 @@ class Universe(nn.Module):
                                                                       keep_rms=bool(keep_rms),
                                                                       diff=dict(self.diff_kwargs), slot=slot,
                                                                       arena=ar, st_lane=False))
+            self._inflight.add(key)
+            if pre_noise is not None:
+                pre_noise(i)
             st = self._streams[slot]
             st.wait_stream(main)   # the input was produced on the caller's stream
             with torch.cuda.stream(st):
@@ -322,7 +379,10 @@ class Universe(nn.Module):
         for st in self._streams[:S]:
             main.wait_stream(st)
         try:
-            plan.check()   # synchronises; the status word is shared by the engine's plans
+            try:
+                plan.check()   # synchronises; the status word is shared by the engine's plans
+            finally:
+                self._inflight.clear()
         except L.OuRangeError:
             # as enhance(): a split-f16 input left its range -> f32 operands,
             # same noise, every clip of the call

@@ -10,6 +10,14 @@ shipping any weight file.
 Scales are chosen so activations stay O(1) through the network: weight-normed
 layers get ``g ~ 1`` (unit-norm rows, the reference's ``cond_weight_norm``,
 ``blocks.py:40-46``), plain layers get ``1/sqrt(fan_in)``.
+
+The "damped" family (``rc_gain=RC_DAMP``) also scales ``g`` of every
+rate-change conv: the binomial anti-alias FIRs are normalised to unit RMS, not
+unit DC gain (``blocks.py:66-72``), so with ``g ~ 1`` each anti-aliased rate
+change amplifies by 4-9x and the reference's own PP24 activations reach 7.7e6
+(golden ``pp24.npz`` ``enh_peak_activation``), beyond what trained weights
+produce and beyond the split-f16 operand range.  At ``RC_DAMP`` they stay O(10)
+(``pp24d.npz``), the regime trained models run in.
 """
 import math
 import zlib
@@ -24,10 +32,14 @@ def _gen(name, seed):
     return g
 
 
-def synth_tensor(name, shape, seed=0):
+RC_DAMP = 0.25   # rate-change conv weight_g scale of the damped family
+
+
+def synth_tensor(name, shape, seed=0, rc_gain=1.0):
     """Synthetic value for one state-dict entry, or ``None`` for deterministic
     buffers that the module computes itself (FIR taps, mel filterbank, STFT
-    window, resampling kernels)."""
+    window, resampling kernels).  ``rc_gain`` scales the weight-norm gain of
+    the rate-change convs (the damped family, see the module doc)."""
     shape = tuple(int(s) for s in shape)
     g = _gen(name, seed)
     leaf = name.rsplit(".", 1)[-1]
@@ -46,7 +58,8 @@ def synth_tensor(name, shape, seed=0):
     if leaf == "alpha":  # Snake log-alpha (bigvgan/snake.py:44)
         return 0.3 * torch.randn(shape, generator=g)
     if leaf == "weight_g":
-        return 1.0 + 0.2 * (2.0 * torch.rand(shape, generator=g) - 1.0)
+        v = 1.0 + 0.2 * (2.0 * torch.rand(shape, generator=g) - 1.0)
+        return v * rc_gain if (rc_gain != 1.0 and "rate_change_conv" in name) else v
     if leaf == "weight_v":
         return torch.randn(shape, generator=g)
     if "prelu" in name and leaf == "weight" and n == 1:
@@ -66,26 +79,26 @@ def synth_tensor(name, shape, seed=0):
     return 0.1 * torch.randn(shape, generator=g)
 
 
-def fill_module_(module, seed=0, skip_prefixes=("loss_",)):
+def fill_module_(module, seed=0, skip_prefixes=("loss_",), rc_gain=1.0):
     """Overwrite a module's parameters/buffers in place with synthetic values."""
     sd = module.state_dict()
     new = {}
     for name, t in sd.items():
         if name.startswith(tuple(skip_prefixes)):
             continue
-        v = synth_tensor(name, t.shape, seed)
+        v = synth_tensor(name, t.shape, seed, rc_gain)
         if v is not None:
             new[name] = v.to(t.dtype)
     module.load_state_dict(new, strict=False)
     return module
 
 
-def synth_state_dict(spec, seed=0):
+def synth_state_dict(spec, seed=0, rc_gain=1.0):
     """spec: iterable of (name, shape) -> {name: tensor} (deterministic buffers
     are omitted; the consumer recomputes them)."""
     out = {}
     for name, shape in spec:
-        v = synth_tensor(name, shape, seed)
+        v = synth_tensor(name, shape, seed, rc_gain)
         if v is not None:
             out[name] = v
     return out

@@ -33,7 +33,8 @@ def golden_state_dict(d, seed=0):
 
     spec = [(n, [int(s) for s in sh.split(",") if s != ""])
             for n, sh in zip(d["manifest_names"], d["manifest_shapes"])]
-    return synth_state_dict([(n, s) for n, s in spec if not n.startswith("loss_")], seed)
+    rc_gain = float(d["synth_rc_gain"]) if "synth_rc_gain" in d else 1.0   # the damped family (pp24d)
+    return synth_state_dict([(n, s) for n, s in spec if not n.startswith("loss_")], seed, rc_gain)
 
 
 def rel_rms(a, b):

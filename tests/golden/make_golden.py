@@ -33,7 +33,7 @@ sys.path.insert(0, REPO)
 REF = "/root/reference/open_universe"
 
 from open_universe_amd.configs import get_config  # noqa: E402
-from open_universe_amd.utils.synthetic import fill_module_, synth_audio  # noqa: E402
+from open_universe_amd.utils.synthetic import RC_DAMP, fill_module_, synth_audio  # noqa: E402
 from oracle import ou_oracle  # noqa: E402  (only for the torchaudio restatement)
 
 
@@ -226,12 +226,12 @@ def full_model_config(name, n_channels=None):
     return cfg
 
 
-def build_ref_model(name, n_channels=None, seed=0):
+def build_ref_model(name, n_channels=None, seed=0, rc_gain=1.0):
     cfg = to_attr(full_model_config(name, n_channels))
     cls = _REGISTRY[cfg["_target_"].rsplit(".", 1)[-1]]
     args = {k: v for k, v in cfg.items() if k != "_target_"}
     model = cls(**args)
-    fill_module_(model, seed=seed)
+    fill_module_(model, seed=seed, rc_gain=rc_gain)
     model.eval()
     return model
 
@@ -253,12 +253,20 @@ def tensors(d):
 # (model, n_channels, samples, tag): reduced-width variants and full width.
 # Full-width ORIG16 / PP24 at short T cover the real channel widths (48..768,
 # GRU H = 384) and, for ORIG16, the 60-step sampler of BASELINE configs[2].
+# "pp24d": PP24 full width with the damped synthetic family (rate-change conv
+# gains scaled by RC_DAMP): activations stay O(10), so the HIP path runs its
+# production split-f16 operands where the undamped "pp24" reruns in f32.
 CASES = (("pp16", None, 3360, "pp16"),
          ("pp16", 4, 4000, "pp16_c4"),
          ("orig16", 4, 3360, "orig16_c4"),
          ("pp24", 4, 5040, "pp24_c4"),
          ("orig16", None, 3360, "orig16"),
-         ("pp24", None, 5040, "pp24"))
+         ("pp24", None, 5040, "pp24"),
+         ("pp24", None, 5040, "pp24d"))
+RC_GAIN = {"pp24d": RC_DAMP}
+# full-width aux-signal / warm-start outputs (the signal-decoupling layer at its
+# real 32 / 48 channels over the 2x-upsampled signal)
+AUX_TAGS = ("pp16_c4", "pp16", "pp24d")
 
 # Standalone torch.nn.GRU layers, the module the reference calls
 # (score.py:84-90 one layer, condition.py:173-179 two layers), at the hidden
@@ -268,13 +276,14 @@ GRU_CASES = (("h384_b8", 384, 1, 8, 33), ("h384_b32", 384, 1, 32, 17),
 
 
 def make_model_case(name, nch, T, tag):
-    model = build_ref_model(name, nch)
+    model = build_ref_model(name, nch, rc_gain=RC_GAIN.get(tag, 1.0))
     names, shapes, order = manifest(model)
     fs = model.fs
     d = {}
     d["manifest_names"] = np.array(names)
     d["manifest_shapes"] = np.array([",".join(map(str, s)) for s in shapes])
     d["param_order"] = np.array(order)
+    d["synth_rc_gain"] = np.float64(RC_GAIN.get(tag, 1.0))   # the synthetic family (conftest.golden_state_dict)
 
     B = 2
     mix = torch.stack([torch.from_numpy(synth_audio(T, fs, i)[0]) for i in range(B)])[:, None]
@@ -331,6 +340,8 @@ def make_model_case(name, nch, T, tag):
             d["enh_sigmed3_out"] = model.enhance(mix, rng=rng, ensemble=3, ensemble_stat="signal_median")
             rng = torch.Generator().manual_seed(9)
             d["enh_sigmed4_out"] = model.enhance(mix, rng=rng, ensemble=4, ensemble_stat="signal_median")
+
+        if tag in AUX_TAGS:
             rng = torch.Generator().manual_seed(4)
             d["enh_aux_out"] = model.enhance(mix, rng=rng, use_aux_signal=True)
             rng = torch.Generator().manual_seed(6)

@@ -142,3 +142,31 @@ def test_load_model_lightning_checkpoint_with_pickled_hparams(tmp_path):
     model = load_model(path)
     for p, e in zip(model.model_parameters(), ema):
         torch.testing.assert_close(p.detach(), e)
+
+
+@pytest.mark.parametrize("shape", [(3000,), (2, 3000), (1, 1, 3200)])
+@pytest.mark.parametrize("kw", [{}, {"n_steps": 3}, {"warm_start": 2}, {"ensemble": 2},
+                                {"use_aux_signal": True}, {"n_steps": 4, "target": True}])
+def test_noise_shapes_match_the_oracle_draws(shape, kw):
+    """Universe.noise_shapes (what bin/enhance.py discards for other ranks'
+    files) lists exactly the randn draws of one enhance, in order: checked
+    against the oracle's restatement of universe.py:231-375 (reduced width)."""
+    from oracle import ou_oracle
+
+    m = _build("pp16", 4)
+    sd = synth_state_dict([(k, v.shape) for k, v in m.state_dict().items()], 0)
+    m.load_state_dict(sd, strict=False)
+    orc = ou_oracle.Oracle({k: v for k, v in m.state_dict().items()}, get_config("pp16", 4))
+    drawn = []
+
+    def noise_fn(s):
+        drawn.append(tuple(s))
+        return torch.zeros(s)
+
+    mix = torch.randn(shape, generator=torch.Generator().manual_seed(0)) * 0.1
+    okw = dict(kw)
+    if okw.get("target"):
+        okw["target"] = mix.reshape(-1, 1, shape[-1]).clone()
+    with torch.no_grad():
+        orc.enhance(mix, noise_fn=noise_fn, **okw)
+    assert m.noise_shapes(mix.shape, **kw) == drawn

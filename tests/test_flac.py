@@ -91,6 +91,41 @@ def test_block_size_and_sample_size_codes(tmp_path, bps):
     np.testing.assert_array_equal(y, x.astype(np.float32) / float(1 << (bps - 1)))
 
 
+@pytest.mark.parametrize("mode", [8, 9, 10])
+def test_32_bit_stereo_side_channel_needs_33_bits(tmp_path, mode):
+    """RFC 9639: the side channel of a 32-bit stream is a 33-bit signal;
+    channels at opposite full scale make it use the 33rd bit."""
+    n = 256
+    lo, hi = -(1 << 31), (1 << 31) - 1
+    left = np.where(np.arange(n) % 2 == 0, hi, lo).astype(np.int64)
+    # frame 2: near opposite full scale but smooth, so a FIXED predictor's
+    # residuals stay small (RFC 9639 keeps residuals within 32 bits) while
+    # its 33-bit warm-up sample and predictions do not
+    ramp = hi - (np.arange(n) % 64) * 1000
+    x = np.concatenate([np.stack([left, -left - 1]), np.stack([ramp, -ramp - 1])], axis=1)
+    frames = [{"n": n, "mode": mode, "sub": [{"kind": "verbatim"}] * 2},
+              {"n": n, "mode": mode, "sub": [{"kind": ("fixed", 1)}] * 2}]
+    y, _ = _decode(tmp_path, fw.encode(x, 48000, 32, frames))
+    np.testing.assert_array_equal(y, x.astype(np.float32) / float(1 << 31))
+
+
+@pytest.mark.parametrize("tail", [b"TAG" + bytes(125), bytes(64)])
+def test_trailing_bytes_after_last_frame(tmp_path, tail):
+    """An ID3v1 tag or padding after the last frame is ignored once every
+    sample STREAMINFO announced is decoded (as libFLAC does); the same bytes
+    before the end of the samples are still a lost frame sync."""
+    rng = np.random.default_rng(3)
+    frames = _mono_frames(256)[:3]
+    x = _signal(rng, 1, 768, 16)
+    data = fw.encode(x, 16000, 16, frames)
+    y, _ = _decode(tmp_path, data + tail)
+    np.testing.assert_array_equal(y, x.astype(np.float32) / 32768.0)
+    if tail[:3] != b"TAG":   # padding where a frame should start
+        cut = data[: len(data) - 10]
+        with pytest.raises(L.OuHipError, match="flac"):
+            _decode(tmp_path, cut + tail)
+
+
 def test_damaged_stream_fails_loudly(tmp_path):
     rng = np.random.default_rng(1)
     frames = _mono_frames(256)[:3]

@@ -99,3 +99,38 @@ def test_enhance_cli_flac_in_flac_out(tmp_path):
     y, fs_out = load_audio(out / "c.flac")
     assert fs_out == 24000 and y.shape[0] == 1 and abs(y.shape[-1] - 20000) <= 3
     assert torch.isfinite(y).all() and y.abs().max() > 0
+
+
+@pytest.mark.parametrize("streams", [2, 1])
+def test_enhance_cli_outputs_independent_of_world_size(tmp_path, monkeypatch, streams):
+    """Every file's noise comes from the one --seed generator in the
+    reference's file order (bin/enhance.py:71-73,147-148,173-189), whatever
+    the world size: rank 0 and rank 1 of WORLD_SIZE=2 (both on cuda:0 here)
+    together write outputs bit-identical to the single-rank run."""
+    from scipy.io import wavfile
+
+    from open_universe_amd.bin import enhance as cli
+    from test_api_surface import _write_ckpt
+
+    ckpt, _, _, _ = _write_ckpt(str(tmp_path), with_ema=False)
+    src = tmp_path / "noisy"
+    src.mkdir()
+    rng = np.random.default_rng(5)
+    lens = {"w0.wav": (16000, 9000), "w1.wav": (48000, 30000), "w2.wav": (16000, 4000), "w3.wav": (8000, 7000),
+            "w4.wav": (16000, 12000)}
+    for name, (fs, n) in lens.items():
+        wavfile.write(src / name, fs, (rng.standard_normal(n) * 0.1).astype(np.float32))
+    common = ["--model", ckpt, "--n_steps", "3", "--seed", "11", "--device", "cuda:0", "--streams", str(streams),
+              "--chunk", "2"]
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    assert cli.main([str(src), str(tmp_path / "one")] + common) == 0
+    for r in (0, 1):
+        monkeypatch.setenv("RANK", str(r))
+        monkeypatch.setenv("LOCAL_RANK", "0")
+        monkeypatch.setenv("WORLD_SIZE", "2")
+        assert cli.main([str(src), str(tmp_path / "two")] + common) == 0
+    for name in lens:
+        a, _ = load_audio(tmp_path / "one" / name)
+        b, _ = load_audio(tmp_path / "two" / name)
+        assert torch.equal(a, b), name

@@ -175,6 +175,72 @@ def test_full_width_pp24_enhance():
     assert rel_rms(out, d["enh_out"]) < 1e-3 and si_sdr(out, d["enh_out"]) > 60
 
 
+def test_full_width_pp24_damped_split_f16_vs_reference():
+    """PP24 at full width with the damped synthetic family (pp24d: the
+    reference's activations stay below 2^15): the production split-f16
+    operands on the 48..768-channel geometries at rates 3 and 8 -- no f32
+    rerun -- against the reference's networks and enhance."""
+    d, cfg, m = _golden_model("pp24d", "pp24")
+    assert float(d["enh_peak_activation"]) < 2.0**15
+    with torch.no_grad():
+        conds, y_hat, h = m.condition_model(_t(d["cond_in"]).to(DEV), train=True)
+        for i, c in enumerate(conds):
+            assert rel_rms(c.cpu(), d[f"cond_out{i}"]) < 1e-4, i
+        conds = [_t(d[f"cond_out{i}"]).to(DEV) for i in range(5)]
+        sc = m.get_score_model()(_t(d["score_x"]).to(DEV), _t(d["score_sigma"]).to(DEV), conds)
+        assert rel_rms(sc.cpu(), d["score_out"]) < 1e-4
+        mix = _t(d["enh_mix"]).to(DEV)
+        out = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
+        assert m._get_engine().conv_prec == 1   # split-f16 ran it, no f32 rerun
+        assert rel_rms(out, d["enh_out"]) < 1e-3 and si_sdr(out, d["enh_out"]) > 60
+        out2 = m.enhance(mix, n_steps=3, rng=torch.Generator().manual_seed(7), keep_rms=True).cpu()
+        assert rel_rms(out2, d["enh2_out"]) < 1e-3 and si_sdr(out2, d["enh2_out"]) > 60
+    assert m._get_engine().conv_prec == 1
+
+
+@pytest.mark.parametrize("tag,name", [("pp16", "pp16"), ("pp24d", "pp24")])
+def test_full_width_aux_and_warm_start_vs_reference(tag, name):
+    """use_aux_signal and warm_start at full width (T = 3,360 / 5,040): the
+    ou_snake_aa kernel over the 32- / 48-channel decoder output upsampled 2x,
+    then the 1-channel conv, and the warm-started sampler, against the
+    reference (universe.py:317-331, universe_gan.py:147-151)."""
+    d, cfg, m = _golden_model(tag, name)
+    mix = _t(d["enh_mix"]).to(DEV)
+    with torch.no_grad():
+        aux = m.enhance(mix, rng=torch.Generator().manual_seed(4), use_aux_signal=True).cpu()
+        assert aux.shape == d["enh_aux_out"].shape
+        assert rel_rms(aux, d["enh_aux_out"]) < 1e-4
+        warm = m.enhance(mix, rng=torch.Generator().manual_seed(6), warm_start=4).cpu()
+        assert rel_rms(warm, d["enh_warm_out"]) < 1e-3 and si_sdr(warm, d["enh_warm_out"]) > 60
+    assert m._get_engine().conv_prec == 1
+
+
+def test_c4_real_shape_damped_split_f16_item0_vs_oracle():
+    """BASELINE configs[3] at its real shape: PP24 full width, batch 32, 10 s
+    clips, damped synthetic weights, split-f16 operands.  The whole batch runs
+    on the GPU; item 0 is compared with the fp32 oracle on the same noise
+    slice (the oracle at B = 32 x 10 s would take minutes)."""
+    from open_universe_amd.utils.synthetic import RC_DAMP
+
+    cfg = get_config("pp24", None)
+    m = UniverseGAN(**{k: v for k, v in cfg.items() if k != "_target_"})
+    m.load_state_dict(synth_state_dict([(k, v.shape) for k, v in m.state_dict().items()], 0, RC_DAMP),
+                      strict=False)
+    m = m.to(DEV).eval()
+    mix = _clips(32, 10.0, cfg["fs"], base=31)
+    with torch.no_grad():
+        out = m.enhance(mix.to(DEV), rng=torch.Generator().manual_seed(2024)).cpu()
+        eng = m._get_engine()
+        assert eng.conv_prec == 1 and int(eng.status.abs().sum()) == 0
+        assert out.shape == (32, 240000) and torch.isfinite(out).all()
+        nz = next(iter(m._plans.values())).NZ.cpu()   # (draws, 32, 1, Tp): the noise the GPU used
+        it = iter(range(nz.shape[0]))
+        ref = _oracle(m, cfg).enhance(mix[:1], noise_fn=lambda shp: nz[next(it), :1].reshape(shp))
+    assert rel_rms(out[:1], ref) < 1e-3 and si_sdr(out[:1], ref) > 60
+    # the other items are not copies of item 0
+    assert rel_rms(out[1:2], out[:1]) > 0.1
+
+
 # ------------------------------------------- BASELINE shapes vs the oracle
 def _vs_oracle(name, B, seconds, n_steps=None, seed=0, conv_prec=None):
     cfg, m = _synth_model(name, seed)

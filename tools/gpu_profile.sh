@@ -21,6 +21,7 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmcf_$TA
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmcw_$TAG" -o pmc -- \
     python3 "$B" --steps 1 --warmup 1 --no-cpu-baseline --no-profile --no-f32-pass --no-queued > /dev/null 2> "$O/pmcw_$TAG.err" &&
 python3 "$ROOT/tools/pmc_summary.py" --tag "$TAG" --enhances 2 --out "$O/pmc_$TAG.json" \
+    --lib "$ROOT/open_universe_amd/libouhip.so" \
     "$(find "$O/pmcf_$TAG" -name '*counter_collection.csv' | head -n1)" \
     "$(find "$O/pmcw_$TAG" -name '*counter_collection.csv' | head -n1)" > /dev/null
 rc=$?

@@ -23,6 +23,13 @@ def short(name):
     return name.split("::")[-1].replace("void ", "").strip()
 
 
+def lib_hash(path):
+    import hashlib
+
+    with open(path, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
 def read(path, counter):
     per = collections.defaultdict(float)  # (dispatch, kernel) -> value
     with open(path) as fh:
@@ -45,6 +52,7 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--enhances", type=int, default=None, help="enhance() calls in the profiled run")
     ap.add_argument("--config", default="c2", help="bench.py --config of the profiled run")
+    ap.add_argument("--lib", default=None, help="the libouhip.so the profiled run loaded (its hash is recorded)")
     a = ap.parse_args()
     f, w = read(a.fetch, "FETCH_SIZE"), read(a.write, "WRITE_SIZE")
     rows = {}
@@ -58,6 +66,9 @@ def main():
     out = {"tag": a.tag, "config": a.config, "correction": "FETCH_SIZE x2 (gfx950), KiB->bytes", "kernels": rows}
     if a.enhances:
         out["enhances_profiled"] = a.enhances
+    if a.lib:
+        # bench.py quotes these counters only for the same library build
+        out["lib_sha16"] = lib_hash(a.lib)
     txt = json.dumps(out, indent=1)
     print(txt)
     if a.out:
