@@ -16,7 +16,7 @@ resampler is therefore pinned to that restatement, not to torchaudio bytes.
 Weights: ``open_universe_amd.utils.synthetic.synth_tensor`` keyed by parameter
 name (the trained HF checkpoint is unavailable offline).
 
-Usage:  python tests/golden/make_golden.py [tag ...]   (tags: CASES, gru, manifests; none = all)
+Usage:  python tests/golden/make_golden.py [tag ...]   (tags: CASES, gru, manifests, metrics; none = all)
 """
 import importlib.util
 import math
@@ -156,8 +156,29 @@ def install_stubs():
     tat.MelSpectrogram = MelSpectrogram
     tat.Resample = Resample
     ta.transforms = tat
+    taf = types.ModuleType("torchaudio.functional")
+
+    def spectrogram(waveform, pad, window, n_fft, hop_length, win_length, power, normalized, center=True,
+                    pad_mode="reflect", onesided=True, return_complex=None):
+        """torchaudio.functional.spectrogram restated from its documented
+        algorithm (the metrics' STFT, metrics/lsd.py:101-126)."""
+        if pad > 0:
+            waveform = torch.nn.functional.pad(waveform, (pad, pad), "constant")
+        shape = waveform.size()
+        waveform = waveform.reshape(-1, shape[-1])
+        spec = torch.stft(waveform, n_fft=n_fft, hop_length=hop_length, win_length=win_length, window=window,
+                          center=center, pad_mode=pad_mode, normalized=False, onesided=onesided,
+                          return_complex=True)
+        spec = spec.reshape(shape[:-1] + spec.shape[-2:])
+        if normalized == "window" or normalized is True:
+            spec = spec / window.pow(2.0).sum().sqrt()
+        return spec.abs().pow(power) if power is not None else spec
+
+    taf.spectrogram = spectrogram
+    ta.functional = taf
     sys.modules["torchaudio"] = ta
     sys.modules["torchaudio.transforms"] = tat
+    sys.modules["torchaudio.functional"] = taf
 
 
 def _load(modname, path):
@@ -378,10 +399,46 @@ def make_gru_cases():
     return tensors(d)
 
 
+def make_metric_cases():
+    """F4: the reference's own log_spectral_distance (metrics/lsd.py:26-140)
+    with the wrapper's 25 ms / 10 ms frames at fs (metrics/wrapper.py:130-151),
+    LSD and SI-LSD, on random pairs and on enhanced-vs-clean pairs (the pp16_c4
+    fixture's enhance output against its clean target), at 16 and 24 kHz, in
+    float64 and float32 (the reference computes in the input dtype)."""
+    lsd_mod = _load("ouref.metrics.lsd", REF + "/metrics/lsd.py")
+    d = {}
+    g = torch.Generator().manual_seed(77)
+    pp = np.load(os.path.join(HERE, "pp16_c4.npz"))
+    for fs in (16000, 24000):
+        n = int(0.75 * fs)
+        clean = torch.from_numpy(np.stack([synth_audio(n, fs, 40 + i)[1] for i in range(3)])).double()
+        noisy = clean + 0.05 * torch.randn(clean.shape, generator=g, dtype=torch.float64)
+        scaled = 0.3 * clean + 0.01 * torch.randn(clean.shape, generator=g, dtype=torch.float64)
+        pairs = {"noisy": (clean, noisy), "scaled": (clean, scaled)}
+        if fs == 16000:
+            tgt = torch.from_numpy(pp["enh_tgt"][:, 0]).double()
+            pairs["enhanced"] = (tgt, torch.from_numpy(pp["enh_out"]).double())
+        for name, (ref, deg) in pairs.items():
+            key = f"fs{fs}_{name}"
+            d[f"{key}_ref"] = ref
+            d[f"{key}_deg"] = deg
+            for dt, sfx in ((torch.float64, "f64"), (torch.float32, "f32")):
+                r, x = ref.to(dt), deg.to(dt)
+                kw = dict(n_fft=int(0.025 * fs), hop_length=int(0.01 * fs))
+                d[f"{key}_lsd_{sfx}"] = lsd_mod.log_spectral_distance(x, r, **kw)
+                d[f"{key}_silsd_{sfx}"] = lsd_mod.log_spectral_distance(x, r, scale_invariant=True, **kw)
+    return tensors(d)
+
+
 def main():
     torch.set_num_threads(8)
     load_reference()
     want = set(sys.argv[1:])
+    if "metrics" in want:
+        np.savez_compressed(os.path.join(HERE, "metrics.npz"), **make_metric_cases())
+        want.discard("metrics")
+        if not want:
+            return
     for name, nch, T, tag in CASES:
         if want and tag not in want:
             continue

@@ -117,3 +117,27 @@ def test_resample_table_matches_oracle(orig, new):
     ko, wo, o, n = O._sinc_resample_kernel(orig, new)
     assert width == wo and k.shape == (n, 2 * width + o)
     np.testing.assert_array_equal(k, ko.reshape(n, -1).numpy())
+
+
+def test_lsd_and_si_lsd_vs_reference_fixtures():
+    """F4 pinned to the reference: tests/golden/metrics.npz holds the outputs
+    of the reference's own log_spectral_distance (metrics/lsd.py:26-140, loaded
+    by path in make_golden.py; torchaudio.functional.spectrogram restated) with
+    the wrapper's 25 ms / 10 ms frames (metrics/wrapper.py:130-151) on random,
+    rescaled and enhanced-vs-clean pairs at 16 and 24 kHz.  The restatement
+    computes in float64: equal to the float64 reference to 1e-9, and to the
+    float32 reference (the dtype the reference keeps) to 1e-4 relative."""
+    from conftest import load_golden
+
+    d = load_golden("metrics")
+    keys = sorted({k.rsplit("_", 1)[0] for k in d if k.endswith("_ref")})
+    assert len(keys) == 5
+    for key in keys:
+        fs = int(key.split("_")[0][2:])
+        ref, deg = torch.from_numpy(d[f"{key}_ref"]), torch.from_numpy(d[f"{key}_deg"])
+        got = metrics.lsd(ref, deg, fs=fs).numpy()
+        got_si = metrics.si_lsd(ref, deg, fs=fs).numpy()
+        np.testing.assert_allclose(got, d[f"{key}_lsd_f64"], rtol=1e-9, err_msg=key)
+        np.testing.assert_allclose(got_si, d[f"{key}_silsd_f64"], rtol=1e-9, err_msg=key)
+        np.testing.assert_allclose(got, d[f"{key}_lsd_f32"], rtol=1e-4, err_msg=key)
+        np.testing.assert_allclose(got_si, d[f"{key}_silsd_f32"], rtol=1e-4, err_msg=key)
