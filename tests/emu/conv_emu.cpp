@@ -2,7 +2,11 @@
 // source compiled for the host against tests/emu/hip/hip_runtime.h, under
 // AddressSanitizer.  Exits nonzero (ASan report / EMU message) on the first
 // out-of-bounds global, buffer or LDS access.  See tests/test_emu_bounds.py.
+#ifdef OU_EMU_CONV_SRC   // a modified copy of the kernel source (tests/test_emu_kernels.py)
+#include OU_EMU_CONV_SRC
+#else
 #include "../../open_universe_amd/csrc/ou_conv.hip"
+#endif
 
 #include <memory>
 
@@ -72,29 +76,52 @@ int main(int argc, char** argv)
         {642, 1, 160, 4, 1600, 1, 1, false, false, false, false},   // STFT as a framed GEMM
         {128, 256, 1, 3, 41, 2, 4, true, false, false, false},      // transposed conv, 4 phases
         {160, 96, 1, 3, 67, 1, 5, false, false, false, false},      // M = 800, partial m-groups
+        // register-streamed kernel (tile bit 14) shapes, run with its tiles
+        // only (kFirstRsGeom on): ragged 16-channel up
+        // conv (3 steps < 4 K waves: the b31c724 fault), 1 step, deep k3 / k5,
+        // frame views with and without the folded FIR, the conditioner's
+        // st_convs whose windows exceed LDS (K chunked by phases / channels)
+        {32, 16, 1, 3, 301, 1, 2, true, false, false, false},
+        {16, 16, 1, 1, 100, 2, 1, false, false, false, false},
+        {512, 512, 1, 3, 41, 1, 1, false, false, false, false},
+        {256, 256, 1, 5, 70, 1, 1, true, true, true, false},
+        {256, 128, 4, 3, 148, 1, 1, false, false, false, false},
+        {512, 256, 5, 1, 205, 1, 1, false, false, false, false},
+        {512, 32, 160, 1, 1760, 1, 1, true, false, false, false},
+        {512, 64, 80, 1, 880, 1, 1, false, false, false, false},
+        {512, 128, 20, 1, 220, 1, 1, false, false, false, false},
     };
     const int only = argc > 1 ? std::atoi(argv[1]) : -1;
     int n = 0;
+    constexpr int kFirstRsGeom = 10;   // geometries from here on: register-streamed tiles only
+    int nrs = 0;
+    const bool rs_only = std::getenv("OUHIP_EMU_RS_ONLY") != nullptr;   // register-streamed tiles only
     for (int gi = 0; gi < (int)(sizeof(geoms) / sizeof(geoms[0])); ++gi) {
         if (only >= 0 && gi != only) continue;
         const Geom& g = geoms[gi];
-        for (int t = 0; t < ou_conv_num_tiles(); ++t) {
-            if (!ou_conv_tile_ok(g.kt, t)) continue;
-            for (int tpw = 0; tpw < 6; ++tpw) {   // 3: warp-specialised, 4: split-f16, 5: f16
+        for (int t = 0; t < std::max(ou_conv_num_tiles(), 16); ++t) {
+            // 3: warp-specialised, 4: split-f16, 5: f16, 6 / 7: register-streamed
+            // kernel (tile bit 14) split-f16 / f16
+            for (int tpw = 0; tpw < 8; ++tpw) {
                 if (tpw == 3 && g.rout != 1) continue;   // warp-specialised: plain convs only
-                const int v = tpw >= 4 ? 2048 : tpw == 3 ? 1024 : tpw << 8;
-                if (!ou_conv_tile_ok(g.kt, t | v)) continue;
+                if (tpw >= 6 && (t >= 16 || g.cin % 16)) continue;   // register-streamed: cin % 16 == 0
+                if (tpw < 6 && (rs_only || gi >= kFirstRsGeom || t >= ou_conv_num_tiles() || !ou_conv_tile_ok(g.kt, t)))
+                    continue;
+                const int v = tpw >= 6 ? (2048 | (1 << 14)) : tpw >= 4 ? 2048 : tpw == 3 ? 1024 : tpw << 8;
+                if (!ou_conv_tile_ok(g.kt, tpw >= 6 ? (t | (1 << 14)) : (t | v))) continue;
                 if (std::getenv("OUHIP_EMU_VERBOSE")) std::fprintf(stderr, "geom %d tile %d tpw %d\n", gi, t, tpw);
-                const int rc = run(g, t | v | (tpw == 5 ? 4096 : 0));
+                const int rc = run(g, t | v | ((tpw == 5 || tpw == 7) ? 4096 : 0));
                 if (rc == -2 && tpw == 3) continue;   // warp-specialised form refused for this geometry
+                if (rc != 0 && tpw >= 6) continue;    // register-streamed form refused (window / LDS)
                 if (rc != 0) {
                     std::fprintf(stderr, "geom %d tile %d tpw %d: ou_conv returned %d\n", gi, t, tpw, rc);
                     return 2;
                 }
                 ++n;
+                nrs += tpw >= 6;
             }
         }
     }
-    std::printf("ok: %d launches bounds-checked\n", n);
+    std::printf("ok: %d launches bounds-checked (%d register-streamed)\n", n, nrs);
     return 0;
 }

@@ -43,6 +43,11 @@ struct float4 {
     const float& operator[](int i) const { return (&x)[i]; }
 };
 inline float4 make_float4(float a, float b, float c, float d) { return {a, b, c, d}; }
+// IEEE round-to-nearest arithmetic (the host's default mode)
+inline float __fadd_rn(float a, float b) { return a + b; }
+inline float __fsub_rn(float a, float b) { return a - b; }
+inline float __fmul_rn(float a, float b) { return a * b; }
+inline float __fdiv_rn(float a, float b) { return a / b; }
 inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 inline uint32_t __float_as_uint(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 #ifdef OU_EMU_FIBERS

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.skipif(not os.path.exists(CLANG), reason="ROCm clang++ 
 
 
 def _build(src, out, *flags):
-    cmd = [CLANG, "-std=c++17", *flags, "-I", EMU, "-x", "c++", os.path.join(EMU, src), "-o", out]
+    cmd = [CLANG, "-std=c++17", "-Wno-psabi", *flags, "-I", EMU, "-x", "c++", os.path.join(EMU, src), "-o", out]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
 
@@ -34,9 +34,65 @@ ASAN = ("-O0", "-g0", "-fsanitize=address", "-fno-omit-frame-pointer")
 
 
 def test_conv_tiles_in_bounds(tmp_path):
+    """Every ou_conv tile of the chunked kernel, and every register-streamed
+    (conv_rkernel, tile bit 14) shape on ragged / 1-step / deep / frame-view /
+    K-chunked (st_conv) geometries, split-f16 and f16."""
     exe = str(tmp_path / "conv_emu")
     _build("conv_emu.cpp", exe, *ASAN)
+    out = _run([exe])
+    assert "ok:" in out and "(0 register-streamed)" not in out
+
+
+def test_fused_block_in_bounds(tmp_path):
+    """ou_block at 32 / 64 / 128 channels, split-f16 and f16, every epilogue
+    the dispatcher instantiates (FiLM, input_cond, cond_out, res2, kEpiIn,
+    kEpiHead, kEpiDown at rates 2 and 4) and ragged lengths."""
+    exe = str(tmp_path / "block_emu")
+    _build("block_emu.cpp", exe, *ASAN)
     assert "ok:" in _run([exe])
+
+
+def _mutant(tmp_path, src, old, new):
+    """A copy of csrc/<src> with one edit, laid out so its relative includes
+    resolve (ou_common.h beside it, include/ouhip.h two levels up)."""
+    import shutil
+
+    d = tmp_path / "m" / "a" / "csrc"
+    d.mkdir(parents=True)
+    (tmp_path / "m" / "include").mkdir()
+    shutil.copy(os.path.join(ROOT, "open_universe_amd", "csrc", "ou_common.h"), d)
+    shutil.copy(os.path.join(ROOT, "include", "ouhip.h"), tmp_path / "m" / "include")
+    text = open(os.path.join(ROOT, "open_universe_amd", "csrc", src)).read()
+    assert old in text, old
+    (d / src).write_text(text.replace(old, new, 1))
+    return str(d / src)
+
+
+def _must_fail(cmd, env=None):
+    e = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", **(env or {}))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=e)
+    assert r.returncode != 0 and "AddressSanitizer" in r.stderr, (r.stdout[-1000:], r.stderr[-2000:])
+
+
+def test_emulator_catches_the_reverted_rkernel_clamp(tmp_path):
+    """The round-2 GPU fault (commit b31c724): a conv_rkernel wave with no K
+    steps read the weight ring below its range.  With the clamp reverted the
+    emulator must report it."""
+    src = _mutant(tmp_path, "ou_conv.hip", "const int sc = max(s0, min(s, s1 - 1));",
+                  "const int sc = min(s, s1 - 1);")
+    exe = str(tmp_path / "conv_emu_rev")
+    _build("conv_emu.cpp", exe, *ASAN, f'-DOU_EMU_CONV_SRC="{src}"')
+    _must_fail([exe, "10"], env={"OUHIP_EMU_RS_ONLY": "1"})
+
+
+def test_emulator_catches_an_unclamped_block_read(tmp_path):
+    """ou_block stages PReLU(h) over its halo with clamped frame indices; an
+    unclamped one reads before the tensor at the clip start."""
+    src = _mutant(tmp_path, "ou_block.hip", "            const int tc = min(max(t, 0), T - 1);\n",
+                  "            const int tc = t;\n")
+    exe = str(tmp_path / "block_emu_rev")
+    _build("block_emu.cpp", exe, *ASAN, f'-DOU_EMU_BLOCK_SRC="{src}"')
+    _must_fail([exe])
 
 
 def test_recorded_plan_convs_in_bounds(tmp_path):
