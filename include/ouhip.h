@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define OUHIP_ABI_VERSION 4
+#define OUHIP_ABI_VERSION 5
 
 int ou_abi_version(void);
 const char* ou_last_error(void);
@@ -168,9 +168,27 @@ typedef struct ou_gru_desc {
                                /* (skips the hand-off wait: wrong results)        */
     uint64_t* granules;        /* workspace: ou_gru_workspace_bytes()             */
     int32_t* status;           /* device int, set nonzero on spin timeout         */
+    int32_t ws_zeroed;         /* nonzero: the caller zeroed the workspace before */
+                               /* the first launch on it (per replay); launches   */
+                               /* leave it reusable, so no per-launch memset --   */
+                               /* needs steps >= 4 (the step tags of the previous */
+                               /* launch must not match a new launch's first two) */
+    int32_t _pad;
+    const void* w_hh16;        /* non-NULL: W_hh in f16 packed by                 */
+                               /* ou_gru_pack_cu16 (hidden 256, the f16 operand   */
+                               /* mode): one 1024-thread workgroup per (item,     */
+                               /* direction) holds it in registers and exchanges  */
+                               /* h through LDS -- no cross-CU hand-off; w_hh,    */
+                               /* granules and status are then unused             */
 } ou_gru_desc;
 
 int64_t ou_gru_workspace_bytes(int hidden, int batch);
+/* Pack w_hh [2][3H][H] (f32, host) for the single-CU f16 recurrence: per
+ * direction, wave w, lane l (unit pair p = l >> 3, k-slice q = l & 7): the f16
+ * weights W[g H + 16 w + 2 p + u][32 q + k], u < 2, g < 3, k < 32, in that
+ * order.  out: ou_gru_packed_cu16_bytes(hidden) bytes. */
+int ou_gru_pack_cu16(const float* w_hh, int hidden, void* out);
+int64_t ou_gru_packed_cu16_bytes(int hidden);
 int ou_gru(const ou_gru_desc* d, void* stream);
 
 /* ------------------------------------------------------------------------

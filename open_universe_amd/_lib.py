@@ -12,7 +12,7 @@ from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OUHIP_LIB", os.path.join(_HERE, "libouhip.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 fp = c_void_p  # device pointers are passed as integers
 
@@ -48,7 +48,8 @@ class GruDesc(ctypes.Structure):
         ("y", fp), ("y_bstride", c_int64), ("y_cstride", c_int64),
         ("res", fp), ("res_bstride", c_int64), ("res_cstride", c_int64),
         ("res_scale", c_float), ("hidden", c_int32), ("steps", c_int32), ("batch", c_int32),
-        ("flags", c_int32), ("granules", fp), ("status", fp),
+        ("flags", c_int32), ("granules", fp), ("status", fp), ("ws_zeroed", c_int32), ("_pad", c_int32),
+        ("w_hh16", fp),
     ]
 
 
@@ -167,6 +168,8 @@ EXPORTS = {
     "ou_conv_lds_info": (c_int, [c_int, c_int, POINTER(c_int), POINTER(c_int)]),
     "ou_gru_workspace_bytes": (c_int64, [c_int, c_int]),
     "ou_gru": (c_int, [POINTER(GruDesc), c_void_p]),
+    "ou_gru_pack_cu16": (c_int, [c_void_p, c_int, c_void_p]),
+    "ou_gru_packed_cu16_bytes": (c_int64, [c_int]),
     "ou_embed": (c_int, [POINTER(EmbedDesc), c_void_p]),
     "ou_head": (c_int, [POINTER(HeadDesc), c_void_p]),
     "ou_normalize": (c_int, [fp, fp, c_int, c_int64, c_float, c_float, c_void_p]),

@@ -62,6 +62,15 @@ constexpr int kStageShift = 6;   // activations are staged as x * 2^-6 (ou_conv'
 #ifndef OU_BLOCK_NT128
 #define OU_BLOCK_NT128 1
 #endif
+#ifndef OU_BLOCK_RING1
+#define OU_BLOCK_RING1 6   // weight-fragment ring depth (k-steps) of one-m-tile waves
+#endif
+#ifndef OU_BLOCK_FENCE
+#define OU_BLOCK_FENCE 1   // pin each ring load ahead of the step's LDS reads (128 ch: 36.6 -> 32.7 us)
+#endif
+#ifndef OU_BLOCK_HV_EARLY
+#define OU_BLOCK_HV_EARLY 0   // load the block residual before the conv3 MFMA stage
+#endif
 
 template <int C, int NT, int P>
 struct BCfg {
@@ -85,7 +94,7 @@ struct BCfg {
     static constexpr int B_OFF = NPL * PA;         // region B: conv2 input
     static constexpr int LDS_BYTES = 2 * (NPL * PA + NPL * PB);
     static constexpr int KS = C / 16;              // 16-channel k-steps per tap
-    static constexpr int RING = MR == 1 ? 6 : 4;   // weight-fragment ring depth (k-steps)
+    static constexpr int RING = MR == 1 ? OU_BLOCK_RING1 : 4;   // weight-fragment ring depth (k-steps)
     static_assert(C % 32 == 0 && WM * WN == WAVES && MT % WM == 0 && NT % WN == 0, "block tiling");
     static_assert((SX / 8) % 2 == 1, "LDS row stride must be an odd number of 16-B slots");
 };
@@ -130,6 +139,9 @@ __device__ __forceinline__ void stage_mma(const half8_t* __restrict__ wp, const 
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         if (s + D - 1 < NS) load_a(s + D - 1, ra[(s + D - 1) % D]);
+        // the fully unrolled loop otherwise lets the scheduler sink the ring
+        // loads next to their use (2-3 steps of latency cover instead of D - 1)
+        if constexpr (OU_BLOCK_FENCE) asm volatile("" ::: "memory");
         const int k = s / KS, ks = s - (s / KS) * KS;
         half8_t b[NR], bl[NR];
 #pragma unroll
@@ -473,14 +485,11 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
     __syncthreads();
 
     // ---- stage 3: conv3 (k3) over frames t0 - OFF + w, w < F + 2 OFF -> y
-    stage_mma<3, C, NT, P>((const half8_t*)d.w[2], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
-    {
-        const float un = d.w_unscale[2];
-        float bia[MR][16], hv[MR][NR][16], rv[MR][NR][16];
-#pragma unroll
-        for (int mr = 0; mr < MR; ++mr)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) bia[mr][r] = d.bias[2] ? d.bias[2][row(mr, r)] : 0.f;
+    // the block residual h (and res2) of this wave's output tiles: loaded
+    // before the conv3 MFMAs when OU_BLOCK_HV_EARLY (their latency then hides
+    // under the stage), else after it
+    float hv[MR][NR][16], rv[MR][NR][16];
+    auto load_res = [&]() {
 #pragma unroll
         for (int nr = 0; nr < NR; ++nr) {
             const int w = (wn * NR + nr) * 32 + l32;
@@ -506,6 +515,17 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
                         rv[mr][nr][r] = d.res2[(int64_t)b * d.r2_bstride + (int64_t)row(mr, r) * d.r2_cstride + tc];
             }
         }
+    };
+    if constexpr (OU_BLOCK_HV_EARLY && !(EPI & kEpiIn)) load_res();
+    stage_mma<3, C, NT, P>((const half8_t*)d.w[2], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
+    if constexpr (!(OU_BLOCK_HV_EARLY && !(EPI & kEpiIn))) load_res();
+    {
+        const float un = d.w_unscale[2];
+        float bia[MR][16];
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bia[mr][r] = d.bias[2] ? d.bias[2][row(mr, r)] : 0.f;
         if constexpr (EPI & kEpiHead) {
             // the score head on the block output: Y[w][c] = prelu2(prelu1(y))
             // (f32, region A, zero outside [0, T)), then one thread per frame

@@ -383,21 +383,52 @@ def prep_block(sd, p, kind, rate, antialias, device):
 class GruW:
     hidden: int
     layers: List  # per layer: (ConvW input projection, w_hh dev [2][3H][H], b_hh dev [2][3H])
+    w16: List = field(default_factory=list)   # per layer: ou_gru_pack_cu16 weights (f16 mode) or None
+
+
+def gru_cu16_enabled():
+    """OUHIP_GRU_CU16=1 runs the f16 operand mode's recurrence on the
+    single-CU f16 kernel (ou_gru_pack_cu16).  Off by default: measured
+    1.59 us per step against 0.79 us for the k-split kernel."""
+    import os
+
+    return os.environ.get("OUHIP_GRU_CU16", "0") == "1"
+
+
+def pack_gru_cu16(w_hh, hidden):
+    """w_hh [2][3H][H] f32 (host) -> the single-CU f16 recurrence's packing."""
+    import ctypes
+
+    lib = L.load()
+    n = lib.ou_gru_packed_cu16_bytes(hidden)
+    assert n > 0, hidden
+    w = np.ascontiguousarray(w_hh, dtype=np.float32)
+    out = np.empty(n // 2, dtype=np.float16)
+    L.check(lib.ou_gru_pack_cu16(w.ctypes.data_as(ctypes.c_void_p), hidden, out.ctypes.data_as(ctypes.c_void_p)),
+            "gru_pack_cu16")
+    return out
 
 
 def prep_gru(sd, p, num_layers, device):
-    layers = []
+    layers, w16 = [], []
     for l in range(num_layers):
         s, sr = f"_l{l}", f"_l{l}_reverse"
         w_ih = np.concatenate([_np(sd[p + ".weight_ih" + s]), _np(sd[p + ".weight_ih" + sr])], 0)
         b_ih = np.concatenate([_np(sd[p + ".bias_ih" + s]), _np(sd[p + ".bias_ih" + sr])], 0)
         proj = make_conv(ConvSpec(w_ih[:, :, None], w_ih.shape[1], 1, 0, 1, 1.0, b_ih,
                                   ref_macs=float(w_ih.size)), device)
-        w_hh = torch.stack([sd[p + ".weight_hh" + s], sd[p + ".weight_hh" + sr]]).float().contiguous().to(device)
+        w_hh = torch.stack([sd[p + ".weight_hh" + s], sd[p + ".weight_hh" + sr]]).detach().to(
+            "cpu", torch.float32).contiguous()
         b_hh = torch.stack([sd[p + ".bias_hh" + s], sd[p + ".bias_hh" + sr]]).float().contiguous().to(device)
-        layers.append((proj, w_hh, b_hh))
+        # the f16 operand mode (BASELINE configs[4]) runs the recurrence on f16
+        # weights in one CU per direction (ou_gru_pack_cu16, hidden 256)
+        cu16 = None
+        if proj.prec == 2 and w_hh.shape[-1] == 256 and gru_cu16_enabled():
+            cu16 = torch.from_numpy(pack_gru_cu16(w_hh.numpy(), 256)).to(device)
+        w16.append(cu16)
+        layers.append((proj, w_hh.to(device), b_hh))
     H = int(sd[p + ".weight_hh_l0"].shape[1])
-    return GruW(H, layers)
+    return GruW(H, layers, w16)
 
 
 # ---------------------------------------------------------------------------
@@ -597,6 +628,14 @@ def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film
 
 
 GRU_FLAGS = -1   # kernel default (XCD-local chains); see ou_gru_desc.flags
+_GRU_WS_ZEROED = False   # set by EnhancePlan: it zeroes the GRU workspaces once per replay
+
+
+def rec_gru_ws_zero(prog, granules):
+    """Zero a GRU hand-off workspace once per replay (OP_MEMSET); the GRU
+    launches recorded after it (with _GRU_WS_ZEROED) then skip their own
+    memset (ou_gru_desc.ws_zeroed)."""
+    prog.add(L.OP_MEMSET, L.MemsetArgs(ptr=granules.data_ptr(), bytes=granules.numel() * granules.element_size()))
 
 
 def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, res: Act = None,
@@ -617,6 +656,9 @@ def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, re
     d.hidden, d.steps, d.batch = gw.hidden, x.T, x.B
     d.granules, d.status = granules.data_ptr(), status.data_ptr()
     d.flags = GRU_FLAGS
+    d.ws_zeroed = 1 if _GRU_WS_ZEROED else 0
+    if gw.w16 and gw.w16[layer] is not None:
+        d.w_hh16 = gw.w16[layer].data_ptr()
     d._flops = 2.0 * 2 * 3 * H * H * x.T * x.B
     prog.add(L.OP_GRU, d)
     if _REC is not None:   # y now holds GRU values its amax row has not seen
@@ -646,6 +688,9 @@ class ConvTuner:
 
         self.cache = {}
         self.reps = reps
+        self.graph = os.environ.get("OUHIP_TUNE_GRAPH", "1") != "0"   # time candidates inside a hipGraph
+        if self.graph:
+            self.reps = max(reps, 8)
         self.path = path
         self.timed = 0   # geometries tuned by timing (not reused from another length)
         self.by_geom = {}   # geometry -> frame-count buckets cached
@@ -751,14 +796,32 @@ class ConvTuner:
             # best of two timed batches: a single short batch is noisy enough
             # to prefer a 35 % slower tile
             ms = float("inf")
-            for _ in range(2):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
+            if self.graph:
+                # device time as the plans run it: copies of the op in one
+                # hipGraph (eager back-to-back launches are host-bound below
+                # ~10 us and charge K-slice tiles a second host launch)
+                prog = L.Program()
                 for _ in range(self.reps):
-                    lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
-                e1.record()
-                e1.synchronize()
-                ms = min(ms, e0.elapsed_time(e1) / self.reps)
+                    prog.add(L.OP_CONV, d)
+                prog.capture()
+                prog.launch(stream)
+                for _ in range(2):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    prog.launch(stream)
+                    e1.record()
+                    e1.synchronize()
+                    ms = min(ms, e0.elapsed_time(e1) / self.reps)
+                del prog
+            else:
+                for _ in range(2):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(self.reps):
+                        lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
+                    e1.record()
+                    e1.synchronize()
+                    ms = min(ms, e0.elapsed_time(e1) / self.reps)
             if ms < best_ms:
                 best, best_ms = t, ms
         d.tile = -1

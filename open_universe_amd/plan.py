@@ -71,6 +71,7 @@ class _PlanBase:
                 init(self, *a, **k)
             finally:
                 E.end_record()
+                E._GRU_WS_ZEROED = False
                 E._LANE = 0
                 E._SLOT = 0
                 E._ARENA = None
@@ -154,6 +155,10 @@ class EnhancePlan(_PlanBase):
         cb = eng.alloc_cond(B, Tp, need_aux=use_aux_signal or warm_start is not None)
         self.cb = cb
         p = self.prog
+        # the GRU hand-off workspaces are zeroed once per replay; the GRU
+        # launches then skip their per-launch memsets (ou_gru_desc.ws_zeroed)
+        E.rec_gru_ws_zero(p, cb["gran"])
+        E._GRU_WS_ZEROED = True
         # ---- record ----
         mixact = Act(self.MIX)
         if keep_rms:
@@ -227,6 +232,7 @@ class EnhancePlan(_PlanBase):
                 coefs.append(c)
             self.WIN = torch.from_numpy(win).to(dev)
             self.sb = eng.alloc_score(B, Tp)
+            E.rec_gru_ws_zero(p, self.sb["gran"])   # lane 0, ahead of the first score GRU
             # initial sample (universe.py:322-331)
             if warm_start is None:
                 p.add(L.OP_SCALE, L.ScaleArgs(z=self.NZ.data_ptr(), y=self.X.ptr, n=B * Tp,

@@ -196,3 +196,19 @@ def test_numpy_block_packing_matches_c():
         a, ua = L.block_pack(w)
         b, ub = L.block_pack_np(w)
         assert ua == ub and np.array_equal(a, b)
+
+
+def test_gru_cu16_packing_matches_restatement():
+    """ou_gru_pack_cu16 (the single-CU f16 recurrence's weight order) against
+    a numpy restatement of the order include/ouhip.h documents."""
+    from open_universe_amd import engine as E
+
+    H = 256
+    w = np.random.default_rng(3).standard_normal((2, 3 * H, H)).astype(np.float32) * 0.06
+    got = E.pack_gru_cu16(w, H)
+    # [dir][wave 16][lane 64: p = l >> 3, q = l & 7][u 2][g 3][k 32]
+    d, wv, p, q, u, g, k = np.meshgrid(np.arange(2), np.arange(16), np.arange(8), np.arange(8), np.arange(2),
+                                        np.arange(3), np.arange(32), indexing="ij")
+    want = w[d, g * H + wv * 16 + 2 * p + u, 32 * q + k].astype(np.float16).reshape(-1)
+    assert got.dtype == np.float16 and got.shape == want.shape
+    np.testing.assert_array_equal(got, want)

@@ -60,9 +60,41 @@ def make(name, dev, seed=0):
     return d, (cw, x, y, r, ws)
 
 
+GRAPH_COPIES = 20
+
+
+def time_tile_graph(d, tile, reps, stream):
+    """Device time per launch: GRAPH_COPIES copies of the op captured in one
+    hipGraph (no host launch cost in the figure; K-slice tiles pay their
+    second launch as a graph node, as in the recorded plans)."""
+    import ctypes
+
+    lib = L.load()
+    d.tile = tile
+    if lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream)) != 0:
+        return None
+    prog = L.Program()
+    for _ in range(GRAPH_COPIES):
+        prog.add(L.OP_CONV, d)
+    prog.capture()
+    prog.launch(stream)
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(max(2, reps // 10)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        prog.launch(stream)
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1) / GRAPH_COPIES)
+    return best
+
+
 def time_tile(d, tile, reps, stream):
     import ctypes
 
+    if os.environ.get("CONV_BENCH_GRAPH", "1") == "1":
+        return time_tile_graph(d, tile, reps, stream)
     lib = L.load()
     d.tile = tile
     if lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream)) != 0:

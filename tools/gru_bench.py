@@ -20,8 +20,17 @@ def main():
     m.load_state_dict(synth_state_dict([(k, v.shape) for k, v in m.state_dict().items()]), strict=False)
     m = m.to(dev).eval()
     eng = m._get_engine()
-    T = 801
+    T = int(os.environ.get("GRU_T", "801"))
     stream = torch.cuda.current_stream().cuda_stream
+    gw = eng.s_gru
+    if os.environ.get("GRU_CU16") == "1":   # the single-CU f16 recurrence (f16 operand mode)
+        sd = {k: v.cpu() for k, v in m.state_dict().items()}
+        saved, E._PREP_PREC = E._PREP_PREC, 2
+        os.environ["OUHIP_GRU_CU16"] = "1"
+        try:
+            gw = E.prep_gru(sd, "_edm_model.encoder.gru", 1, dev)
+        finally:
+            E._PREP_PREC = saved
     for B in (1, 4, 8):
         x = E.Act(torch.randn(B, 512, T, device=dev) * 0.5)
         gi, y = E.new_act(B, 1536, T, dev), E.new_act(B, 512, T, dev)
@@ -30,7 +39,7 @@ def main():
         for flags in [int(f) for f in os.environ.get("GRU_FLAGS", "5,7,9,11,21,25").split(",")]:
             E.GRU_FLAGS = flags
             prog = L.Program()
-            E.rec_gru(prog, eng.s_gru, 0, x, gi, y, gran, eng.status)
+            E.rec_gru(prog, gw, 0, x, gi, y, gran, eng.status)
             prog.run(stream)
             torch.cuda.synchronize()
             ms = []
