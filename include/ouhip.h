@@ -47,7 +47,7 @@ const char* ou_last_error(void);
  *   xv[c'][t] = prelu(in_scale[b] * x[b][c'%cin][t*R + c'/cin + shift])  (0 outside [0,in_len))
  *   (phase-major frame view: channel c' = ph*cin + ci; W's channel axis, as
  *   packed by ou_conv_pack, follows the same order)
- *   acc[m][u] = sum_{c',k} W[m][c'][k] * xv[c'][u + k - pad]          u in [0, n_frames)
+ *   acc[m][u] = sum_{c',k} W[m][c'][k] * xv[c'][u + k - pad]     u in [f0, f0 + n_frames)
  *   m = ph*cout + co, t = u*rout + ph  (pixel shuffle; rout = 1 for plain convs)
  *   v = acc + bias[co];  v = t < valid_len ? v : 0
  *   v = (v + res1[b][co][t]) * s1;  v = film_g[b][co]*v + film_b[b][co];
@@ -94,7 +94,12 @@ typedef struct ou_conv_desc {
                                /* 2: f16 operands (the hi halves of the same     */
                                /*    packing), f32 accumulation                  */
     float w_unscale;           /* prec 1: power of two from ou_conv_pack_split   */
-    int32_t _reserved;
+    int32_t f0;                /* first output frame u computed: the launch      */
+                               /* covers u in [f0, f0 + n_frames), in the global */
+                               /* frame coordinates of x / y (zero padding only  */
+                               /* at the true ends); 0 = from the start.  The    */
+                               /* persistent / warp-specialised f32 kernels      */
+                               /* (tile bits 8-10) need f0 = 0                   */
     int32_t* status;           /* prec 1: set to 1 when a staged input exceeds   */
                                /* the split-f16 range, or NULL                   */
     float* amax_out;           /* [64] or NULL: running max |y| of the stored    */
@@ -168,6 +173,13 @@ typedef struct ou_gru_desc {
                                /* (skips the hand-off wait: wrong results)        */
     uint64_t* granules;        /* workspace: ou_gru_workspace_bytes()             */
     int32_t* status;           /* device int, set nonzero on spin timeout         */
+    int32_t t_begin, t_end;    /* steps [t_begin, t_end) of the T-step sequences  */
+                               /* (forward: time t, backward: T - 1 - t); 0, 0 =  */
+                               /* all.  A launch with t_begin > 0 starts from     */
+                               /* hstate; every launch leaves h of its last step  */
+                               /* there: the recurrence split over launches, each */
+                               /* ordered after the one before (k-split kernel)   */
+    float* hstate;             /* [B][2][H], or NULL (whole sequences only)       */
     int32_t ws_zeroed;         /* nonzero: the caller zeroed the workspace before */
                                /* the first launch on it (per replay); launches   */
                                /* leave it reusable, so no per-launch memset --   */
@@ -392,6 +404,16 @@ typedef struct ou_block_desc {
     int32_t rate, down_kt;
     float* e;                  /* [B][2C][ceil(length / rate)]                   */
     int64_t e_bstride, e_cstride;
+    /* Frame range (a chunk of a longer signal): outputs (y, cond_out, the
+     * head, e) are computed and stored for frames [f0, f1) only, reading h
+     * (x) wherever the convs' halos reach -- zero padding stays at [0,
+     * length).  f1 = 0: the whole signal.  With a rate-change conv f0 and f1
+     * are multiples of `rate`.  h frames outside [h0, h1) are read as zero
+     * (h1 = 0: no limit): a chunk's caller has produced h only there, and
+     * the frames it leaves out reach no stored output -- a workgroup past f1
+     * stages them but stores nothing they feed.                             */
+    int32_t f0, f1;
+    int32_t h0, h1;
 } ou_block_desc;
 
 /* 1 when ou_block handles this channel count and operand precision. */
@@ -477,7 +499,7 @@ typedef struct ou_finish_args {
     const float* mix_rms;
 } ou_finish_args;
 typedef struct ou_sync_args {
-    int32_t id;                /* lane (OU_OP_LANE) or event (SIGNAL / WAIT), 0..63 */
+    int32_t id;                /* lane 0..8 (OU_OP_LANE) or event 0..4095 */
     int32_t _pad;
 } ou_sync_args;
 typedef struct ou_ensemble_args {

@@ -37,7 +37,7 @@ class ConvDesc(ctypes.Structure):
         ("res1", fp), ("r1_bstride", c_int64), ("r1_cstride", c_int64), ("s1", c_float),
         ("film", fp), ("film_bstride", c_int64),
         ("res2", fp), ("r2_bstride", c_int64), ("r2_cstride", c_int64), ("s2", c_float),
-        ("tile", c_int32), ("prec", c_int32), ("w_unscale", c_float), ("_reserved", c_int32),
+        ("tile", c_int32), ("prec", c_int32), ("w_unscale", c_float), ("f0", c_int32),
         ("status", fp), ("amax_out", fp), ("amax_in", fp), ("ks_ws", fp), ("ks_ws_bytes", c_int64),
     ]
 
@@ -48,7 +48,8 @@ class GruDesc(ctypes.Structure):
         ("y", fp), ("y_bstride", c_int64), ("y_cstride", c_int64),
         ("res", fp), ("res_bstride", c_int64), ("res_cstride", c_int64),
         ("res_scale", c_float), ("hidden", c_int32), ("steps", c_int32), ("batch", c_int32),
-        ("flags", c_int32), ("granules", fp), ("status", fp), ("ws_zeroed", c_int32), ("_pad", c_int32),
+        ("flags", c_int32), ("granules", fp), ("status", fp), ("t_begin", c_int32), ("t_end", c_int32),
+        ("hstate", fp), ("ws_zeroed", c_int32), ("_pad", c_int32),
         ("w_hh16", fp),
     ]
 
@@ -141,6 +142,7 @@ class BlockDesc(ctypes.Structure):
         ("head", HeadDesc),
         ("w_down", fp), ("b_down", fp), ("slope_down", c_float), ("w_down_unscale", c_float),
         ("rate", c_int32), ("down_kt", c_int32), ("e", fp), ("e_bstride", c_int64), ("e_cstride", c_int64),
+        ("f0", c_int32), ("f1", c_int32), ("h0", c_int32), ("h1", c_int32),
     ]
 
 

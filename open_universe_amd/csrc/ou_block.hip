@@ -229,14 +229,14 @@ __device__ __forceinline__ void split4(float x0, float x1, float x2, float x3, h
 // 32 x 32 tiles, dealt over the 4 waves.
 template <int C, int P, int R, int KF, int F, int SX>
 __device__ __forceinline__ void down_stage(const ou_block_desc& d, const _Float16* xa, int pstride, int t0, int T,
-                                           int b, int wave, int lane)
+                                           int TS, int b, int wave, int lane)
 {
     constexpr int KT = KF * R, KS = C / 16, NS = KT * KS;
     constexpr int M4 = 2 * C / 32, NU = F / R, N4 = (NU + 31) / 32;
     constexpr int D = NS < 6 ? NS : 6;
     const int l32 = lane & 31, h = lane >> 5;
     const half8_t* wp = (const half8_t*)d.w_down;
-    const int TE = (T + R - 1) / R;
+    const int TE = (TS + R - 1) / R;   // e stored for output frames < ceil(TS / R)
     const int e0 = t0 / R;
     const float un = d.w_down_unscale;
     for (int tile = wave; tile < M4 * N4; tile += 4) {
@@ -303,7 +303,9 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
     const int l32 = lane & 31, h = lane >> 5;
     const int b = blockIdx.y;
     const int T = d.length;
-    const int t0 = blockIdx.x * F;
+    const int t0 = d.f0 + blockIdx.x * F;   // first output frame of the workgroup (global)
+    const int TS = d.f1 > 0 ? min(d.f1, T) : T;   // outputs stored for frames < TS
+    const int hlo = d.h0, hhi = d.h1 > 0 ? min(d.h1, T) : T;   // h frames the caller produced
     const float* __restrict__ hb = d.h + (int64_t)b * d.h_bstride;
     bool ovf = false;
 
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[it][i] = src[(int64_t)i * d.h_cstride];
             }
-            if (t != tc || (d.dbg & 1)) {
+            if (t != tc || t < hlo || t >= hhi || (d.dbg & 1)) {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[it][i] = 0.f;
             }
@@ -413,7 +415,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
                     o[r] = inside ? v : 0.f;
                 }
                 if constexpr (EPI & kEpiCond) {
-                    if (inside && t >= t0 && t < t0 + F) {
+                    if (inside && t >= t0 && t < t0 + F && t < TS) {
                         float* co = d.cond_out + (int64_t)b * d.co_bstride + t;
 #pragma unroll
                         for (int r = 0; r < 16; ++r) co[(int64_t)row(mr, r) * d.co_cstride] = o[r];
@@ -553,7 +555,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
             __syncthreads();
             for (int f = tid; f < F; f += K::NTH) {
                 const int t = t0 + f;
-                if (t >= T) break;
+                if (t >= TS) break;
                 float net = 0.f;
                 for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -588,7 +590,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
                 for (int nr = 0; nr < NR; ++nr) {
                     const int w = (wn * NR + nr) * 32 + l32;
                     const int t = t0 - OFF + w;
-                    const bool own = w >= OFF && w < OFF + F && t < T && !((d.dbg & 4) && !(d.dbg & 1024));
+                    const bool own = w >= OFF && w < OFF + F && t < TS && !((d.dbg & 4) && !(d.dbg & 1024));
                     float vv[16];
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
@@ -620,7 +622,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 :
                 }
             if constexpr (EPI & kEpiDown) {
                 __syncthreads();
-                down_stage<C, P, R, KF, F, SX>(d, xa, K::PA, t0, T, b, wave, lane);
+                down_stage<C, P, R, KF, F, SX>(d, xa, K::PA, t0, T, TS, b, wave, lane);
             }
         }
     }
@@ -640,7 +642,10 @@ int launch(const ou_block_desc& d, hipStream_t s)
     }
     constexpr int F = block_f<C, NT, P, EPI, R, KF>();
     static_assert(F > 0 && F % R == 0, "block: frames per workgroup");
-    dim3 grid((d.length + F - 1) / F, d.batch);
+    const int f1 = d.f1 > 0 ? min(d.f1, d.length) : d.length;
+    if (d.f0 < 0 || d.f0 >= f1 || d.f0 % R || (R > 1 && f1 % R && f1 != d.length))
+        return ou_fail(-1, "block: frame range [%d, %d) (rate %d, length %d)", d.f0, f1, R, d.length);
+    dim3 grid((f1 - d.f0 + F - 1) / F, d.batch);
     hipLaunchKernelGGL((block_kernel<C, NT, P, EPI, R, KF>), grid, dim3(K::NTH), K::LDS_BYTES, s, d);
     return ou_check_launch("block");
 }

@@ -227,7 +227,7 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
             for (int r = 0; r < 16; ++r) {
                 const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 const int t = u * rout + ph[r];
-                const bool ok = m < M && u < d.n_frames && t < ylen;
+                const bool ok = m < M && u < d.f0 + d.n_frames && t < ylen;
                 off[r] = ok ? t : -1;   // column; row offsets differ per tensor
             }
             if (has_r1) {
@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const int ks = ksmode == 1 ? (int)blockIdx.z - b * nks : 0;
     const int q0 = ksmode == 1 ? ks * nchunks / nks : 0;
     const int q1 = ksmode == 1 ? (ks + 1) * nchunks / nks : nchunks;
-    const int n0 = blockIdx.x * C::BN;
+    const int n0 = blockIdx.x * C::BN + d.f0;     // first output frame (global)
     const int mt0 = blockIdx.y * (WM * MR);       // first m-tile of the workgroup
     const int h = lane >> 5;
     const int l32 = lane & 31;
@@ -705,7 +705,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     const int wm = wave % WM, wk = wave / WM;
     const int h = lane >> 5, l32 = lane & 31;
     const int b = blockIdx.z;
-    const int n0 = blockIdx.x * R::BN;
+    const int n0 = blockIdx.x * R::BN + d.f0;   // first output frame (global)
     const int mtu = blockIdx.y * WM + wm;       // this wave's m-tile (rows past M: computed, not stored)
     const int mt = min(mtu, mtiles - 1);
     const int diag = (d.tile >> 8) & 3;   // diagnostics (tools/conv_bench.py --rdiag): 1 no input loads, 2 no K loop
@@ -2106,8 +2106,8 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     if (!dp) return ou_fail(-1, "conv: null descriptor");
     const ou_conv_desc& d = *dp;
     if (!d.x || !d.w || !d.y || d.m <= 0 || d.batch <= 0 || d.n_frames <= 0 || d.cin <= 0 ||
-        d.frame <= 0 || d.rout <= 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0)
-        return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d frame=%d)", d.m, d.rout, d.frame);
+        d.frame <= 0 || d.rout <= 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0 || d.f0 < 0)
+        return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d frame=%d f0=%d)", d.m, d.rout, d.frame, d.f0);
     if (d.tile >= 0 && (d.tile & kRsBit)) {   // register-streamed kernel (bits 0-7: RTILES shape)
         if ((d.tile & ~(kRsBit | 0x3ff)) || (d.tile & 0xff) >= kNumRTiles)
             return ou_fail(-2, "conv: bad register-streamed tile 0x%x", d.tile);
@@ -2138,6 +2138,8 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
         return ou_fail(-2, "conv: amax_out needs the one-tile kernel (tile 0x%x)", d.tile);
     if (d.prec != 0 && (ws || tpw > 1))
         return ou_fail(-2, "conv: the split-f16 form has one-tile workgroups only (tile 0x%x)", d.tile);
+    if (d.f0 != 0 && (ws || tpw > 1))
+        return ou_fail(-2, "conv: a frame offset (f0 %d) needs the one-tile kernel (tile 0x%x)", d.f0, d.tile);
     if (d.prec != 0 && !(d.w_unscale > 0.f))
         return ou_fail(-1, "conv: split-f16 needs the w_unscale of ou_conv_pack_split");
     const int lb = lds_bytes(d.kt, tile | (ws ? kWsBit : 0) | (d.prec != 0 ? kSplitBit : 0));

@@ -386,6 +386,9 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
         return (int)(((((int64_t)b * 2 + dir) * 2 + par) * H + lane * KPL) * 8);
     };
 
+    // steps [tb, te) of this launch (the recurrence may be split over
+    // launches: h of the step before tb comes from d.hstate)
+    const int tb = d.t_begin, te = d.t_end > 0 ? min(d.t_end, T) : T;
     float hp[NB];                            // h_{t-1} of unit j
     float gir[NB], giz[NB], gin[NB], rsd[NB];
     auto prefetch = [&](int step) {
@@ -403,19 +406,22 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
             }
         }
     };
+    auto hs_at = [&](int b, int u) -> float {   // h of unit u before step tb (written by the previous launch)
+        return tb > 0 ? d.hstate[((int64_t)b * 2 + dir) * H + u] : 0.f;
+    };
 #pragma unroll
-    for (int bb = 0; bb < NB; ++bb) hp[bb] = 0.f;
-    prefetch(0);
+    for (int bb = 0; bb < NB; ++bb) hp[bb] = hs_at(b0 + min(bb, nbh - 1), j);
+    prefetch(tb);
     OU_STAMP_INIT
 
-    for (int t = 0; t < T; ++t) {
+    for (int t = tb; t < te; ++t) {
         const int time = dir == 0 ? t : T - 1 - t;
         float h[NB][KPL];
-        if (t == 0) {
+        if (t == tb) {
 #pragma unroll
             for (int bb = 0; bb < NB; ++bb)
 #pragma unroll
-                for (int k = 0; k < KPL; ++k) h[bb][k] = 0.f;
+                for (int k = 0; k < KPL; ++k) h[bb][k] = hs_at(b0 + min(bb, nbh - 1), lane * KPL + k);
         } else {
             const uint32_t want = (uint32_t)t;   // tag of h_{t-1}
             const int par = (t - 1) & 1;
@@ -460,7 +466,7 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
         for (int bb = 0; bb < NB; ++bb) {
             cr[bb] = gir[bb]; cz[bb] = giz[bb]; cn[bb] = gin[bb]; cres[bb] = rsd[bb];
         }
-        if (t + 1 < T) prefetch(t + 1);
+        if (t + 1 < te) prefetch(t + 1);
 
         // partial dot products, value index (u * NB + b) * 3 + g
         float acc[NV];
@@ -529,6 +535,12 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
             }
         }
         OU_STAMP(3);
+    }
+    // h of the last step, for a launch that continues the recurrence
+    if (d.hstate && writer) {
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb)
+            if (bb < nbh) d.hstate[((int64_t)(b0 + bb) * 2 + dir) * H + j] = hp[bb];
     }
     // leave the placement slot zeroed for the next launch on this workspace:
     // every member of the chain has passed the placement handshake by now
@@ -808,6 +820,12 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
     if (!d.gi || !d.b_hh || !d.y || d.steps <= 0 || d.batch <= 0 || d.batch > 32768)
         return ou_fail(-1, "gru: invalid descriptor");
     hipStream_t s = (hipStream_t)stream;
+    const bool split = d.t_begin != 0 || (d.t_end != 0 && d.t_end != d.steps);
+    if (d.t_begin < 0 || (d.t_end != 0 && (d.t_end <= d.t_begin || d.t_end > d.steps)) || (split && !d.hstate))
+        return ou_fail(-1, "gru: bad step range [%d, %d) of %d (hstate %p)", d.t_begin, d.t_end, d.steps,
+                       (const void*)d.hstate);
+    if (split && (d.w_hh16 || d.hidden % 64 || (d.flags >= 0 && (d.flags & 32))))
+        return ou_fail(-2, "gru: a step range needs the k-split kernel (hidden %% 64 == 0, fp32 weights)");
     if (d.w_hh16) {   // single-CU recurrence on f16 weights (ou_gru_pack_cu16)
         if (d.hidden != kCuH) return ou_fail(-1, "gru: f16 single-CU recurrence needs hidden 256 (got %d)", d.hidden);
         hipLaunchKernelGGL(gru_cu_kernel, dim3(2 * d.batch), dim3(64 * kCuWaves), 0, s, d);
@@ -818,7 +836,9 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
     // step tags of a previous launch (>= steps - 1 >= 3) never match a new
     // launch's first polls (tags 1, 2): a workspace zeroed once per replay
     // serves every launch of it (ws_zeroed)
-    if (!d.ws_zeroed || d.steps < 4)
+    // a launch continuing a split recurrence (t_begin > 0) starts from hstate:
+    // the tags the previous launches left are all older than the ones it polls
+    if ((!d.ws_zeroed && d.t_begin == 0) || d.steps < 4)
         OU_HIP_CHECK(hipMemsetAsync(d.granules, 0, ou_gru_workspace_bytes(d.hidden, d.batch), s), "gru: memset");
     // k-split kernel (default for H % 64 == 0; flags bit5 selects the
     // workgroup-gather kernel below)

@@ -6,6 +6,8 @@
 // an ou_program; replays run natively (no per-op Python), and
 // ou_program_capture() turns the list into a single hipGraph so a replay is
 // one host call regardless of the ~500 kernels inside.
+#include <cstdio>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -37,6 +39,7 @@ struct ou_program {
 // so one capture stream suffices.
 namespace {
 constexpr int kMaxDev = 64, kMaxSide = 8;
+constexpr int kMaxEvents = 4096;   // a chunked enhance signals ~10 events per diffusion step
 hipStream_t g_cap[kMaxDev];
 hipStream_t g_side[kMaxDev][kMaxSide];
 
@@ -98,7 +101,8 @@ static int validate_lanes(const ou_program* p, int* n_lanes, int* n_events)
             continue;
         }
         const int v = ((const ou_sync_args*)o.desc.data())->id;
-        if (v < 0 || v > 63) return ou_fail(-1, "program: sync id %d out of range", v);
+        if (v < 0 || v >= (o.kind == OU_OP_LANE ? kMaxSide + 1 : kMaxEvents))
+            return ou_fail(-1, "program: sync id %d out of range", v);
         if (o.kind == OU_OP_LANE) {
             if (v >= nl) {
                 nl = v + 1;
@@ -170,8 +174,14 @@ static int run_lanes(ou_program* p, hipStream_t s0)
             if ((rc = shared_stream(&g_side[dev][l - 1], &side[l - 1]))) return rc;
     }
     hipStream_t cur = s0;
+    static const bool trace = std::getenv("OUHIP_PROG_TRACE") != nullptr;   // diagnostics
     for (size_t i = 0; i < p->ops.size(); ++i) {
         const auto& o = p->ops[i];
+        if (trace) {
+            std::fprintf(stderr, "[prog] op %zu kind %d id %d\n", i, o.kind,
+                         is_sync(o.kind) ? ((const ou_sync_args*)o.desc.data())->id : -1);
+            std::fflush(stderr);
+        }
         if (is_sync(o.kind)) {
             const int v = ((const ou_sync_args*)o.desc.data())->id;
             if (o.kind == OU_OP_LANE) cur = v == 0 ? s0 : side[v - 1];
@@ -286,6 +296,36 @@ int ou_program_run(ou_program* p, void* stream)
     return run_lanes(p, (hipStream_t)stream);
 }
 
+// Side lanes that wait on each other's events (directly or around a cycle
+// of side lanes) crash the HIP runtime's stream capture (seen on ROCm 7.2:
+// a segfault inside the capture): refuse such a program before capturing.
+static int check_side_cycles(const ou_program* p)
+{
+    constexpr int N = kMaxSide + 1;
+    bool edge[N][N] = {};
+    std::vector<int> ev_lane;
+    int lane = 0;
+    for (const auto& o : p->ops) {
+        if (!is_sync(o.kind)) continue;
+        const int v = ((const ou_sync_args*)o.desc.data())->id;
+        if (o.kind == OU_OP_LANE) lane = v;
+        else if (o.kind == OU_OP_SIGNAL) {
+            if ((int)ev_lane.size() <= v) ev_lane.resize(v + 1, -1);
+            ev_lane[v] = lane;
+        } else if (v < (int)ev_lane.size() && ev_lane[v] > 0 && lane > 0 && ev_lane[v] != lane)
+            edge[lane][ev_lane[v]] = true;   // side lane `lane` waits on side lane ev_lane[v]
+    }
+    // reachability (Floyd-Warshall over <= 9 lanes)
+    for (int k = 1; k < N; ++k)
+        for (int i = 1; i < N; ++i)
+            for (int j = 1; j < N; ++j)
+                if (edge[i][k] && edge[k][j]) edge[i][j] = true;
+    for (int i = 1; i < N; ++i)
+        if (edge[i][i]) return ou_fail(-1, "program: side lane %d waits on itself through other side lanes "
+                                           "(route cross-lane edges through lane 0 for a hipGraph)", i);
+    return 0;
+}
+
 int ou_program_capture(ou_program* p)
 {
     if (!p) return ou_fail(-1, "program_capture: null");
@@ -298,6 +338,7 @@ int ou_program_capture(ou_program* p)
                  "begin capture");
     int nl = 1, ne = 0;
     int rc = validate_lanes(p, &nl, &ne);
+    if (rc == 0) rc = check_side_cycles(p);
     if (rc == 0) rc = ensure_sync(p, nl, ne);
     if (rc) {
         hipGraph_t g0 = nullptr;

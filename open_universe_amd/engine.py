@@ -12,6 +12,7 @@ The layer walk mirrors the reference modules it replaces:
   ConditionerNetwork       networks/universe/condition.py:68-377
   Universe.enhance         networks/universe/universe.py:231-375
 """
+import ctypes
 import math
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -62,7 +63,7 @@ _REC = None
 # slot * MAX_LANES + lane of their engine
 _LANE = 0
 _SLOT = 0
-MAX_LANES = 2
+MAX_LANES = 4   # 0 main (and the chunked pass's GRU), 1 conditioner, 2-3 the chunked pass's convs
 MAX_SLOTS = 2   # a third stream measured slower: the box gives a process 4 hardware queues
 
 
@@ -493,7 +494,25 @@ def new_act(B, C, T, device):
 
 def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=None,
               valid_len=None, in_scale=0, res1: Act = None, s1=1.0, film=0, film_bs=0,
-              res2: Act = None, s2=1.0, batch=None):
+              res2: Act = None, s2=1.0, batch=None, rng=None):
+    """ou_conv descriptor.  rng = (a, b): output frames [a, b) only (a chunk
+    of the signal, in the frame coordinates of the whole op): the launch
+    keeps the tile of the whole op -- the same K order per output frame, so
+    chunks and the whole op agree bit for bit wherever both compute -- and
+    reads x only up to the last sample those frames need (the rest reads as
+    zero: a chunk's caller has produced x only there).  Its FLOP / byte
+    counts stay the whole op's (rec_block scales them by the chunk's share)."""
+    if rng is not None:
+        full = conv_desc(cw, x, y, in_len=in_len, n_frames=n_frames, out_len=out_len, valid_len=valid_len,
+                         in_scale=in_scale, res1=res1, s1=s1, film=film, film_bs=film_bs, res2=res2, s2=s2,
+                         batch=batch)
+        a, b = max(0, rng[0]), min(full.n_frames, rng[1])
+        assert 0 <= a < b, ("conv chunk", rng, full.n_frames)
+        d = L.ConvDesc.from_buffer_copy(full)
+        d._flops, d._bytes, d._full = full._flops, full._bytes, full   # add_conv pins the tile
+        d.in_len = max(1, min(d.in_len, (b - cw.pad + cw.kt - 1) * cw.frame + cw.shift))
+        d.f0, d.n_frames = a, b - a
+        return d
     d = L.ConvDesc()
     d.x, d.x_bstride, d.x_cstride = x.ptr, x.bs, x.cs
     d.cin, d.in_len = cw.cin, x.T if in_len is None else in_len
@@ -511,6 +530,7 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
     if n_frames is None:
         n_frames = -(-d.in_len // cw.frame) if cw.rout == 1 else x.T
     d.n_frames = n_frames
+    d.f0 = 0
     d.batch = x.B if batch is None else batch
     d.y, d.y_bstride, d.y_cstride = y.ptr, y.bs, y.cs
     d.rout = cw.rout
@@ -524,6 +544,7 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
         d.res2, d.r2_bstride, d.r2_cstride, d.s2 = res2.ptr, res2.bs, res2.cs, s2
     d.tile = -1
     d._flops = 2.0 * cw.ref_macs * n_frames * d.batch
+    assert d.n_frames > 0
     # algorithmic HBM bytes: input, output and residuals once each (f32), plus
     # the logical f32 weights -- no halo or tile re-reads
     act = cw.cin * d.in_len + cw.cout * d.out_len * (1 + (res1 is not None) + (res2 is not None))
@@ -542,37 +563,107 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
 
 def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film_bs=0,
               sc: Act = None, res2: Act = None, s2=1.0, cond_out: Act = None, skip_tail=False,
-              x_in=None, head=None, e_out: Act = None):
+              x_in=None, head=None, e_out: Act = None, rng=None, e_rng=None, share=1.0):
     """ConvBlock main stage (blocks.py:393-407):
        cond_out = conv1(h); c = (cond_out + sc)/sqrt2; c = film(c); c = conv3(conv2(c));
        out = (h + c)/sqrt2 [; out = (out + res2) * s2]
     and, for a down block given ``e_out``, its rate-change conv e_out =
     rate_conv(out) (blocks.py:268-275): fused into the block where ou_block
-    has the stage, else its own launch."""
+    has the stage, else its own launch.
+
+    rng = (lo, hi): block outputs for frames [lo, hi) only (a chunk of the
+    signal; for a down block the rate conv runs over e frames e_rng, or
+    [lo / rate, ceil(hi / rate)) where it is fused).  Returns the h frames [a, b) the chunk reads, which
+    the caller must have produced.  share: the chunk's share of the whole
+    op (rec_block's ops count that fraction of its algorithmic FLOPs and
+    bytes: chunked plans recompute halo frames, which are not counted)."""
+    T = h.T
     c1_out = cond_out if cond_out is not None else tA
-    d1 = conv_desc(bw.conv1, h, c1_out, res1=sc, s1=NF2, film=film, film_bs=film_bs)
+    if rng is None:
+        r1 = r2 = r3 = e_rng = hn = None
+    else:
+        r3 = (max(0, rng[0]), min(T, rng[1]))
+        assert r3[0] < r3[1], rng
+        if e_out is not None:
+            r = bw.rate
+            if bw.fused is not None and bw.down is not None and out.ptr != h.ptr:
+                # the fused rate-change conv covers e frames [lo / rate, ceil(hi / rate))
+                assert r3[0] % r == 0 and (r3[1] % r == 0 or r3[1] == T), ("rate-change range", r3, r)
+                e_rng = (r3[0] // r, -(-r3[1] // r))
+            else:
+                lo_, hi_ = need(bw.rate_conv, e_rng, T)
+                assert r3[0] <= lo_ and hi_ <= r3[1], ("rate-change conv reads past the block range", r3, e_rng)
+        r2 = need(bw.conv3, r3, T)
+        r1 = need(bw.conv2, r2, T)
+        hn = need(bw.conv1, r1, T)
+    d1 = conv_desc(bw.conv1, h, c1_out, res1=sc, s1=NF2, film=film, film_bs=film_bs, rng=r1)
     if skip_tail:
-        prog.add(L.OP_CONV, d1)
+        add_conv(prog, d1, share)
         return
-    d2 = conv_desc(bw.conv2, c1_out, tB)
-    d3 = conv_desc(bw.conv3, tB, out, res1=h, s1=NF2, res2=res2, s2=s2)
-    d_rc = conv_desc(bw.rate_conv, out, e_out) if e_out is not None else None
+    d2 = conv_desc(bw.conv2, c1_out, tB, rng=r2)
+    d3 = conv_desc(bw.conv3, tB, out, res1=h, s1=NF2, res2=res2, s2=s2, rng=r3)
+    d_rc = conv_desc(bw.rate_conv, out, e_out, rng=e_rng) if e_out is not None else None
     if bw.fused is not None and out.ptr != h.ptr:
         fuse_rc = d_rc is not None and bw.down is not None
         descs = (d1, d2, d3) + ((x_in[4],) if x_in is not None else ()) + ((d_rc,) if fuse_rc else ())
-        prog.add(L.OP_BLOCK, block_desc(bw, h, out, descs, sc=sc, film=film, film_bs=film_bs,
-                                        cond_out=cond_out, res2=res2, s2=s2,
-                                        x_in=x_in[:4] if x_in is not None else None, head=head,
-                                        e_out=e_out if fuse_rc else None))
+        bd = block_desc(bw, h, out, descs, sc=sc, film=film, film_bs=film_bs,
+                        cond_out=cond_out, res2=res2, s2=s2,
+                        x_in=x_in[:4] if x_in is not None else None, head=head,
+                        e_out=e_out if fuse_rc else None)
+        if rng is not None:
+            # the kernel's internal window: the stored frames, the rate-change
+            # conv's taps and the head's taps, each through the conv chain
+            vin = r3
+            if fuse_rc:
+                vin = span_union(vin, need(bw.rate_conv, e_rng, T))
+            if head is not None:
+                vin = span_union(vin, (max(0, r3[0] - 1), min(T, r3[1] + 1)))   # head conv k3 (score.py:259)
+            hn = need(bw.conv1, need(bw.conv2, need(bw.conv3, vin, T), T), T)
+            bd.f0, bd.f1 = r3
+            bd.h0, bd.h1 = hn
+        prog.add(L.OP_BLOCK, scaled(bd, share))
         if d_rc is not None and not fuse_rc:
-            prog.add(L.OP_CONV, d_rc)
-        return True
+            add_conv(prog, d_rc, share)
+        return hn if rng is not None else True
     assert x_in is None and head is None, "input / head fusion needs the fused block"
-    prog.add(L.OP_CONV, d1)
-    prog.add(L.OP_CONV, d2)
-    prog.add(L.OP_CONV, d3)
+    add_conv(prog, d1, share)
+    add_conv(prog, d2, share)
+    add_conv(prog, d3, share)
     if d_rc is not None:
-        prog.add(L.OP_CONV, d_rc)
+        add_conv(prog, d_rc, share)
+    return hn
+
+
+def add_conv(prog, d, share=1.0):
+    """Record an ou_conv; a chunk (conv_desc rng) gets the tile of its whole op."""
+    full = getattr(d, "_full", None)
+    if full is not None and d.tile < 0:
+        if full.tile < 0:
+            full.tile = L.TUNER(full) if L.TUNER is not None else L.load().ou_conv_pick_tile(ctypes.byref(full))
+        d.tile = full.tile
+    prog.add(L.OP_CONV, scaled(d, share))
+
+
+def need(cw: ConvW, rng, in_len):
+    """Input samples [a, b) (clipped to [0, in_len)) that output frames rng
+    of conv ``cw`` read: frame u reads frame-view frames u - pad .. u - pad +
+    kt - 1 of ``frame`` samples each, from sample ``shift`` on (ou_conv_desc)."""
+    a = (rng[0] - cw.pad) * cw.frame + cw.shift
+    b = (rng[1] - cw.pad + cw.kt - 1) * cw.frame + cw.shift
+    return (max(0, a), min(in_len, b))
+
+
+def span_union(p, q):
+    return (min(p[0], q[0]), max(p[1], q[1]))
+
+
+def scaled(d, share):
+    """Scale a descriptor's algorithmic FLOP / byte counts (d._flops,
+    d._bytes: the roofline accounting) by ``share``."""
+    if share != 1.0:
+        d._flops = getattr(d, "_flops", 0.0) * share
+        d._bytes = getattr(d, "_bytes", 0.0) * share
+    return d
 
 
 def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film_bs=0, cond_out: Act = None,
@@ -639,14 +730,24 @@ def rec_gru_ws_zero(prog, granules):
 
 
 def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, res: Act = None,
-            res_scale=1.0):
+            res_scale=1.0, steps=None, hstate=None, proj_rng=None, share=1.0):
+    """Bidirectional GRU layer (input projection + recurrence, gru.py via
+    score.py:117-125).  steps = (t0, t1): only the recurrence steps [t0, t1)
+    of both directions (forward frames t0 .. t1 - 1, backward T - t1 .. T - 1
+    - t0), continuing from / leaving h in ``hstate`` [B][2][H]; the input
+    projection is then the caller's (proj_rng: record it for frames proj_rng
+    only, with no recurrence)."""
     proj, w_hh, b_hh = gw.layers[layer]
     H = gw.hidden
     assert gi.C == 6 * H and gi.T == x.T and y.C == 2 * H and y.T == x.T and y.B == x.B
     if res is not None:
         assert res.C == 2 * H and res.T == x.T
     assert granules.numel() * 8 >= L.load().ou_gru_workspace_bytes(H, x.B)
-    prog.add(L.OP_CONV, conv_desc(proj, x, gi))
+    if proj_rng is not None:
+        add_conv(prog, conv_desc(proj, x, gi, rng=proj_rng), share)
+        return
+    if steps is None:
+        prog.add(L.OP_CONV, conv_desc(proj, x, gi))
     d = L.GruDesc()
     d.gi, d.gi_bstride = gi.ptr, gi.bs
     d.w_hh, d.b_hh = w_hh.data_ptr(), b_hh.data_ptr()
@@ -657,9 +758,12 @@ def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, re
     d.granules, d.status = granules.data_ptr(), status.data_ptr()
     d.flags = GRU_FLAGS
     d.ws_zeroed = 1 if _GRU_WS_ZEROED else 0
+    if steps is not None:
+        assert hstate is not None and hstate.numel() >= x.B * 2 * H and 0 <= steps[0] < steps[1] <= x.T
+        d.t_begin, d.t_end, d.hstate = steps[0], steps[1], hstate.data_ptr()
     if gw.w16 and gw.w16[layer] is not None:
         d.w_hh16 = gw.w16[layer].data_ptr()
-    d._flops = 2.0 * 2 * 3 * H * H * x.T * x.B
+    d._flops = 2.0 * 2 * 3 * H * H * (x.T if steps is None else steps[1] - steps[0]) * x.B
     prog.add(L.OP_GRU, d)
     if _REC is not None:   # y now holds GRU values its amax row has not seen
         _REC["slots"].pop(y.ptr, None)
@@ -1037,7 +1141,7 @@ class Engine:
         self.sdl_b = float(sd[p + ".conv.bias"].reshape(-1)[0])
 
     # -------------------------------------------------------------- buffers
-    def alloc_score(self, B, T):
+    def alloc_score(self, B, T, chunked=False):
         dev = self.device
         Ts = level_lengths(T, self.rates)
         n_lvl = len(self.s_enc)
@@ -1050,6 +1154,15 @@ class Engine:
         H = self.s_gru.hidden
         bufs["GI"] = new_act(B, 6 * H, Ts[len(self.rates)], dev)
         bufs["gran"] = zeros((L.load().ou_gru_workspace_bytes(H, B) // 8,), dtype=torch.int64, device=dev)
+        if chunked:
+            # the chunked pass: GRU state between step segments, and a conv1
+            # temp for the unfused decoder levels below the top (whose E / V
+            # buffers hold the up-conv sum / the skip other chunks still read)
+            bufs["HS"] = empty((B, 2, H), dtype=torch.float32, device=dev)
+            for i in range(n_lvl - 1):
+                if self.s_dec[n_lvl - 1 - i].fused is None:
+                    li = min(i, len(self.rates))
+                    bufs[f"X{i}"] = new_act(B, Cs[li], Ts[li], dev)
         return bufs
 
     def score_levels(self):
@@ -1111,6 +1224,202 @@ class Engine:
                     prog.add(L.OP_HEAD, head)
                 return None
         return h
+
+    # ------------------------------------------------- chunked score pass
+    def chunk_plan(self, B, T, force=False):
+        """Split points of the chunked score pass for a (B, T) plan, or None
+        when it does not apply.  The pass cuts the bottleneck GRU (both
+        directions at once) into step segments [0, s1), [s1, s2), [s2, T4)
+        and runs the convs around it in chunks on two side lanes while the
+        recurrence runs on a third: the encoder outside-in (the forward
+        direction consumes frames from the left end, the backward one from
+        the right), the decoder middle-out (frame t has both directions once
+        max(t, T4 - 1 - t) steps are done).  Chunks recompute the convs' halo
+        frames; tiles are pinned to the whole ops', so every chunk computes
+        the bits the unchunked pass computes (tests/test_gpu_chunked.py).
+        Off unless OUHIP_CHUNK=1 or ``force``; OUHIP_CHUNK_SPLIT="f1,f2" sets
+        s1 / T4 and s2 / T4."""
+        import os
+
+        if not force:
+            if os.environ.get("OUHIP_CHUNK", "0") != "1":
+                return None
+            if B > int(os.environ.get("OUHIP_CHUNK_MAX_BATCH", "4")):
+                return None   # wide batches fill the chip without it
+        nr, n_lvl = len(self.rates), len(self.s_enc)
+        Ts = level_lengths(T, self.rates)
+        T4 = Ts[nr]
+        gw = self.s_gru
+        if (T4 < 96 or _REC is not None or gw.hidden % 64 or (GRU_FLAGS >= 0 and GRU_FLAGS & 32)
+                or any(w is not None for w in (gw.w16 or []))):
+            return None
+        b0, bl = self.s_enc[0], self.s_dec[-1]
+        if not (fuse_ends_enabled() and self.s_in_fusable and b0.fused is not None and b0.C == 32
+                and bl.fused is not None and bl.C == 32):
+            return None
+        if any(bw.fused is None and bw.conv1.prec == 0 for bw in self.s_enc + self.s_dec):
+            return None   # f32 tiles may be persistent (no frame offset)
+        f1, f2 = (float(v) for v in os.environ.get("OUHIP_CHUNK_SPLIT", "0.25,0.7").split(","))
+        h = T4 // 2
+        s1 = max(8, min(h - 8, int(round(f1 * T4))))
+        s2 = max(h + 8, min(T4 - 8, int(round(f2 * T4))))
+        D = math.prod(self.rates)
+        # middle decoder chunks: level-4 frames [m0, m1) = [T4 - s2 + g, s2 - g)
+        # with the smallest margin g whose chunks read only finished GRU frames
+        for g in range(0, s2 - h):
+            m0, m1 = T4 - s2 + g, s2 - g
+            if m1 - m0 < 4:
+                return None
+            q = [self._dec_ranges(T, (m0 * D, h * D))[0], self._dec_ranges(T, (h * D, min(Ts[0], m1 * D)))[0]]
+            if all(T4 - s2 <= a and b <= s2 for a, b in (r["h"] for r in q)):
+                break
+        else:
+            return None
+        return {"T4": T4, "s": (s1, s2), "h": h, "mid": (m0, m1), "D": D}
+
+    def _enc_ranges(self, T, O):
+        """Per encoder level (0 .. top): the block output range, the rate-change
+        output range (down levels) and the h range read, for a chunk that owns
+        bottleneck frames O."""
+        nr, n_lvl = len(self.rates), len(self.s_enc)
+        Ts = level_lengths(T, self.rates)
+        out = [None] * n_lvl
+        req = O   # required output range of the level above (E_{i+1}), or V_top
+        for i in range(n_lvl - 1, -1, -1):
+            bw = self.s_enc[i]
+            Ti = Ts[min(i, nr)]
+            if bw.kind == "down":
+                if bw.fused is not None and bw.down is not None:
+                    r3 = (req[0] * bw.rate, min(Ti, req[1] * bw.rate))
+                    e_rng = (r3[0] // bw.rate, -(-r3[1] // bw.rate))
+                    vin = span_union(r3, need(bw.rate_conv, e_rng, Ti))
+                else:
+                    r3 = need(bw.rate_conv, req, Ti)
+                    e_rng, vin = req, r3
+            else:
+                r3, e_rng, vin = req, None, req
+            hn = need(bw.conv1, need(bw.conv2, need(bw.conv3, vin, Ti), Ti), Ti)
+            out[i] = {"out": r3, "e": e_rng, "h": hn}
+            req = hn
+        return out
+
+    def _dec_ranges(self, T, P):
+        """Per decoder level l (0 = top .. last): the block output range, the
+        up-conv frame range (l >= 1) and the h range read, for a chunk that
+        owns output samples P of the last level (the head's x)."""
+        nr, n_lvl = len(self.rates), len(self.s_enc)
+        Ts = level_lengths(T, self.rates)
+        out = [None] * n_lvl
+        r3 = P
+        for l in range(n_lvl - 1, -1, -1):
+            i = n_lvl - 1 - l
+            bw = self.s_dec[l]
+            Ti = Ts[min(i, nr)]
+            vin = r3
+            if l == n_lvl - 1:   # the fused head's conv (k3) on the block output
+                vin = (max(0, r3[0] - 1), min(Ti, r3[1] + 1))
+            hn = need(bw.conv1, need(bw.conv2, need(bw.conv3, vin, Ti), Ti), Ti)
+            ent = {"out": r3, "h": hn}
+            if bw.kind == "up":
+                # h = skip + up(previous level): frames u of the level above
+                # make samples [u r, u r + r)
+                fr = (hn[0] // bw.rate, -(-hn[1] // bw.rate))
+                ent["up"] = fr
+                r3 = need(bw.rate_conv, fr, Ts[min(i + 1, nr)])
+            out[l] = ent
+        return out
+
+    def rec_score_chunked(self, prog, bufs, x: Act, film_base, film_bs, cp, in_scale=0, sc_list=None,
+                          before_level=None, head=None):
+        """The score network pass (rec_score) as chunks on lanes 2 / 3 around
+        the bottleneck GRU's step segments on lane 0 (chunk_plan).  Starts and
+        ends on lane 0.  before_level(l): as rec_score, called on each lane
+        before the lane's first decoder level l."""
+        n_lvl, nr = len(self.s_enc), len(self.rates)
+        top = n_lvl - 1
+        T = x.T
+        Ts = bufs["T"]
+        T4, (s1, s2), h, (m0, m1), D = cp["T4"], cp["s"], cp["h"], cp["mid"], cp["D"]
+        fb = lambda j: film_base + 4 * self.film_off[j]
+        p = prog
+        ev0 = p.signal()
+        to_lane = lambda l: set_lane(p, l)
+
+        def enc_chunk(O):
+            share = (O[1] - O[0]) / T4
+            rr = self._enc_ranges(T, O)
+            for i in range(n_lvl):
+                bw = self.s_enc[i]
+                x_in = None
+                if i == 0:
+                    d_in = conv_desc(self.s_input, x, bufs["E0"], in_scale=in_scale)
+                    x_in = (x, in_scale, self.s_in_w, self.s_in_b, d_in)
+                got = rec_block(p, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
+                                film=fb(i), film_bs=film_bs, x_in=x_in,
+                                e_out=bufs[f"E{i+1}"] if bw.kind == "down" else None,
+                                rng=rr[i]["out"], e_rng=rr[i]["e"], share=share)
+                assert i == 0 or got == rr[i]["h"], ("encoder chunk ranges", i, got, rr[i])
+            rec_gru(p, self.s_gru, 0, bufs[f"V{top}"], bufs["GI"], bufs[f"V{top}"], bufs["gran"], self.status,
+                    proj_rng=O, share=share)
+
+        def dec_chunk(P, waits):
+            share = (P[1] - P[0]) / Ts[0]
+            rr = self._dec_ranges(T, P)
+            h_act = None
+            for l in range(n_lvl):
+                i = top - l
+                bw = self.s_dec[l]
+                if waits and before_level is not None:
+                    before_level(l)
+                if bw.kind == "up":
+                    li = min(i, nr)
+                    add_conv(p, conv_desc(bw.rate_conv, h_act, bufs[f"E{i}"], n_frames=h_act.T, out_len=Ts[li],
+                                          valid_len=bw.rate * h_act.T, res1=bufs[f"V{i}"], s1=NF2,
+                                          rng=rr[l]["up"]), share)
+                    hin = bufs[f"E{i}"]
+                else:
+                    hin = bufs[f"V{i}"]
+                last = l == n_lvl - 1
+                tA = bufs[f"E{i}"] if i == top else bufs.get(f"X{i}", bufs[f"A{i}"])
+                got = rec_block(p, bw, hin, bufs[f"A{i}"], tA, bufs[f"B{i}"], film=fb(n_lvl + l), film_bs=film_bs,
+                                sc=sc_list[l], head=head if last else None, rng=rr[l]["out"], share=share)
+                assert got == rr[l]["h"], ("decoder chunk ranges", l, got, rr[l])
+                h_act = bufs[f"A{i}"]
+
+        gru = lambda st: rec_gru(p, self.s_gru, 0, bufs[f"V{top}"], bufs["GI"], bufs[f"V{top}"], bufs["gran"],
+                                 self.status, res=bufs[f"V{top}"], res_scale=NF2, steps=st, hstate=bufs["HS"])
+        ev = {}
+        for lane, outer, inner in ((2, (0, s1), (s1, h)), (3, (T4 - s1, T4), (h, T4 - s1))):
+            to_lane(lane)
+            p.wait(ev0)
+            enc_chunk(outer)
+            ev[lane, 1] = p.signal()
+            enc_chunk(inner)
+            ev[lane, 2] = p.signal()
+        # the recurrence runs on lane 0: side lanes that wait on each other
+        # (2 <-> GRU lane) crash the HIP runtime's stream capture, so every
+        # cross-lane edge of the pass goes through lane 0
+        to_lane(0)
+        p.wait(ev[2, 1])
+        p.wait(ev[3, 1])
+        gru((0, s1))
+        p.wait(ev[2, 2])
+        p.wait(ev[3, 2])
+        gru((s1, s2))
+        g2 = p.signal()
+        gru((s2, T4))
+        g3 = p.signal()
+        T0 = Ts[0]
+        for lane, mid, outer in ((2, (m0 * D, h * D), (0, m0 * D)), (3, (h * D, min(T0, m1 * D)), (min(T0, m1 * D), T0))):
+            to_lane(lane)
+            p.wait(g2)
+            dec_chunk(mid, True)
+            p.wait(g3)
+            dec_chunk(outer, False)
+            ev[lane, 3] = p.signal()
+        to_lane(0)
+        p.wait(ev[2, 3])
+        p.wait(ev[3, 3])
 
     def rec_sc(self, prog, conds, scs):
         for l, (c, s) in enumerate(zip(conds, scs)):

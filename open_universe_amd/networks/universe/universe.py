@@ -362,7 +362,7 @@ class Universe(nn.Module):
             plan = self._arena_plan(key, slot, lambda ar: EnhancePlan(eng, B, T, int(n_steps), float(epsilon),
                                                                       keep_rms=bool(keep_rms),
                                                                       diff=dict(self.diff_kwargs), slot=slot,
-                                                                      arena=ar, st_lane=False))
+                                                                      arena=ar, st_lane=False, chunk=False))
             self._inflight.add(key)
             if pre_noise is not None:
                 pre_noise(i)

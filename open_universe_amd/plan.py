@@ -111,7 +111,7 @@ class EnhancePlan(_PlanBase):
 
     def __init__(self, eng, batch, mix_len, n_steps, epsilon, keep_rms=False,
                  use_aux_signal=False, warm_start=None, diff=None, ensemble=None,
-                 ensemble_mode=None, slot=0, arena=None, st_lane=True):
+                 ensemble_mode=None, slot=0, arena=None, st_lane=True, chunk=None):
         # arena: record every buffer into this Arena (engine.Arena; the caller
         # owns it and retries with a bigger one on ArenaFull)
         if arena is not None:
@@ -130,6 +130,7 @@ class EnhancePlan(_PlanBase):
         Tp = mix_len + self.pad
         self.Tp = Tp
         self.use_aux = use_aux_signal
+        self.chunks = None
         self.warm = warm_start
         diff = diff or eng.cfg["diffusion"]
         # sampler constants (universe.py:301-305)
@@ -231,7 +232,10 @@ class EnhancePlan(_PlanBase):
                     c.update(c_score=f32(s_now * s_now))
                 coefs.append(c)
             self.WIN = torch.from_numpy(win).to(dev)
-            self.sb = eng.alloc_score(B, Tp)
+            # the chunked score pass (Engine.chunk_plan): GRU segments on lane
+            # 4, conv chunks on lanes 2 / 3
+            self.chunks = eng.chunk_plan(B, Tp, force=chunk is True) if chunk is not False else None
+            self.sb = eng.alloc_score(B, Tp, chunked=self.chunks is not None)
             E.rec_gru_ws_zero(p, self.sb["gran"])   # lane 0, ahead of the first score GRU
             # initial sample (universe.py:322-331)
             if warm_start is None:
@@ -250,9 +254,19 @@ class EnhancePlan(_PlanBase):
                 zi += 0 if last else 1
                 head = eng.head_desc(None, self.X.ptr, B, Tp, mode=2 if last else 1,
                                      x_ptr=self.X.ptr, z_ptr=z_ptr, coef=coefs[n])
-                eng.rec_score(p, self.sb, self.X, film_base + 4 * n * eng.film_rows, 0,
-                              in_scale=in_scale, sc_list=self.SC, before_level=join, head=head)
+                if self.chunks is not None:
+                    eng.rec_score_chunked(p, self.sb, self.X, film_base + 4 * n * eng.film_rows, 0, self.chunks,
+                                          in_scale=in_scale, sc_list=self.SC, before_level=join, head=head)
+                else:
+                    eng.rec_score(p, self.sb, self.X, film_base + 4 * n * eng.film_rows, 0,
+                                  in_scale=in_scale, sc_list=self.SC, before_level=join, head=head)
             x_final = self.X
+            if self.chunks is not None and ev_cond:
+                # the side lanes waited on the conditions; lane 0 joins lane 1
+                # through its last signal only (every event a stream waits on
+                # before its next node adds an edge to that node, and a capture
+                # whose node took 9 crashed in the HIP runtime)
+                p.wait(max(ev_cond.values()))
         p.add(L.OP_FINISH, L.FinishArgs(x=x_final.ptr, x_bstride=Tp, left=self.pad // 2,
                                         batch=B, len=mix_len, y=self.OUT.data_ptr(),
                                         mix_rms=self.MIXRMS.data_ptr() if keep_rms else 0))
