@@ -409,8 +409,16 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
     auto hs_at = [&](int b, int u) -> float {   // h of unit u before step tb (written by the previous launch)
         return tb > 0 ? d.hstate[((int64_t)b * 2 + dir) * H + u] : 0.f;
     };
+    // h before step tb, loaded ahead of the loop: a load inside the loop's
+    // first-step branch made the compiler drain every outstanding load at the
+    // branch join (the gi prefetch included): 0.73 -> 1.0 us per step
+    float h0[NB][KPL];
 #pragma unroll
-    for (int bb = 0; bb < NB; ++bb) hp[bb] = hs_at(b0 + min(bb, nbh - 1), j);
+    for (int bb = 0; bb < NB; ++bb) {
+        hp[bb] = hs_at(b0 + min(bb, nbh - 1), j);
+#pragma unroll
+        for (int k = 0; k < KPL; ++k) h0[bb][k] = hs_at(b0 + min(bb, nbh - 1), lane * KPL + k);
+    }
     prefetch(tb);
     OU_STAMP_INIT
 
@@ -421,7 +429,7 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
 #pragma unroll
             for (int bb = 0; bb < NB; ++bb)
 #pragma unroll
-                for (int k = 0; k < KPL; ++k) h[bb][k] = hs_at(b0 + min(bb, nbh - 1), lane * KPL + k);
+                for (int k = 0; k < KPL; ++k) h[bb][k] = h0[bb][k];
         } else {
             const uint32_t want = (uint32_t)t;   // tag of h_{t-1}
             const int par = (t - 1) & 1;

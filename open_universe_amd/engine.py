@@ -1388,38 +1388,48 @@ class Engine:
 
         gru = lambda st: rec_gru(p, self.s_gru, 0, bufs[f"V{top}"], bufs["GI"], bufs[f"V{top}"], bufs["gran"],
                                  self.status, res=bufs[f"V{top}"], res_scale=NF2, steps=st, hstate=bufs["HS"])
+        # recorded in the order the work should run (the hipGraph executor
+        # launches nodes in capture order): outer encoder chunks, segment 1,
+        # inner chunks, segment 2, middle decoder chunks, segment 3, outer
+        # decoder chunks.  Every cross-lane edge goes through lane 0, which
+        # runs the recurrence: side lanes that wait on each other crash the
+        # HIP runtime's stream capture.
+        T0 = Ts[0]
+        L_, R_ = 2, 3
         ev = {}
-        for lane, outer, inner in ((2, (0, s1), (s1, h)), (3, (T4 - s1, T4), (h, T4 - s1))):
+        for lane, O in ((L_, (0, s1)), (R_, (T4 - s1, T4))):
             to_lane(lane)
             p.wait(ev0)
-            enc_chunk(outer)
+            enc_chunk(O)
             ev[lane, 1] = p.signal()
-            enc_chunk(inner)
-            ev[lane, 2] = p.signal()
-        # the recurrence runs on lane 0: side lanes that wait on each other
-        # (2 <-> GRU lane) crash the HIP runtime's stream capture, so every
-        # cross-lane edge of the pass goes through lane 0
         to_lane(0)
-        p.wait(ev[2, 1])
-        p.wait(ev[3, 1])
+        p.wait(ev[L_, 1])
+        p.wait(ev[R_, 1])
         gru((0, s1))
-        p.wait(ev[2, 2])
-        p.wait(ev[3, 2])
+        for lane, O in ((L_, (s1, h)), (R_, (h, T4 - s1))):
+            to_lane(lane)
+            enc_chunk(O)
+            ev[lane, 2] = p.signal()
+        to_lane(0)
+        p.wait(ev[L_, 2])
+        p.wait(ev[R_, 2])
         gru((s1, s2))
         g2 = p.signal()
-        gru((s2, T4))
-        g3 = p.signal()
-        T0 = Ts[0]
-        for lane, mid, outer in ((2, (m0 * D, h * D), (0, m0 * D)), (3, (h * D, min(T0, m1 * D)), (min(T0, m1 * D), T0))):
+        for lane, P in ((L_, (m0 * D, h * D)), (R_, (h * D, min(T0, m1 * D)))):
             to_lane(lane)
             p.wait(g2)
-            dec_chunk(mid, True)
+            dec_chunk(P, True)
+        to_lane(0)
+        gru((s2, T4))
+        g3 = p.signal()
+        for lane, P in ((L_, (0, m0 * D)), (R_, (min(T0, m1 * D), T0))):
+            to_lane(lane)
             p.wait(g3)
-            dec_chunk(outer, False)
+            dec_chunk(P, False)
             ev[lane, 3] = p.signal()
         to_lane(0)
-        p.wait(ev[2, 3])
-        p.wait(ev[3, 3])
+        p.wait(ev[L_, 3])
+        p.wait(ev[R_, 3])
 
     def rec_sc(self, prog, conds, scs):
         for l, (c, s) in enumerate(zip(conds, scs)):

@@ -89,6 +89,7 @@ class _PlanBase:
         import os
 
         eager_first = os.environ.get("OUHIP_EAGER_FIRST", "1") != "0"
+        use_graph = use_graph and os.environ.get("OUHIP_GRAPH", "1") != "0"   # 0: always the native launch loop
         if use_graph and (self.uses > 1 or self.prog.captured or not eager_first):
             if not self.prog.captured:
                 self.prog.capture()

@@ -39,7 +39,10 @@ struct Case {
     int rate, down_kt;   // rate 0: no fused rate-change conv
 };
 
-int run(const Case& c)
+// chunk: outputs for frames [f0, f1) only (a third of the signal, aligned
+// to the rate), h read over [h0, h1); checks that no y / cond_out / head /
+// e element outside the range was written
+int run(const Case& c, bool chunk = false)
 {
     const int C = c.C, T = c.T, B = c.B;
     ou_block_desc d{};
@@ -84,7 +87,36 @@ int run(const Case& c)
         d.slope_down = 0.15f; d.rate = c.rate; d.down_kt = c.down_kt;
         d.e = f((size_t)B * 2 * C * TE); d.e_bstride = (int64_t)2 * C * TE; d.e_cstride = TE;
     }
-    const int rc = ou_block(&d, nullptr);
+    int f0 = 0, f1 = T;
+    if (chunk) {
+        const int r = c.rate ? c.rate : 1;
+        f0 = T / 3 / r * r;
+        f1 = std::min(T, (2 * T / 3 + 1 + r - 1) / r * r);
+        if (f1 <= f0) f1 = std::min(T, f0 + r);
+        d.f0 = f0; d.f1 = f1;
+        d.h0 = std::max(0, f0 - 4 - 2 * r); d.h1 = std::min(T, f1 + 4 + 2 * r);
+    }
+    int rc = ou_block(&d, nullptr);
+    if (rc == 0 && chunk) {
+        auto check = [&](const float* buf, int rows, int len, int a, int bnd, const char* what) {
+            if (!buf) return;
+            for (int b = 0; b < B; ++b)
+                for (int ch = 0; ch < rows; ++ch)
+                    for (int t = 0; t < len; ++t)
+                        if ((t < a || t >= bnd) && buf[((size_t)b * rows + ch) * len + t] != 0.25f) {
+                            std::fprintf(stderr, "EMU: chunk [%d, %d) wrote %s frame %d\n", a, bnd, what, t);
+                            rc = 3;
+                            return;
+                        }
+        };
+        if (!c.head) check(y, C, T, f0, f1, "y");
+        if (c.cond) check(d.cond_out, C, T, f0, f1, "cond_out");
+        if (c.head) check(d.head.out, 1, T, f0, f1, "head out");
+        if (c.rate) {
+            const int TE = (T + c.rate - 1) / c.rate;
+            check(d.e, 2 * C, TE, f0 / c.rate, (f1 + c.rate - 1) / c.rate, "e");
+        }
+    }
     for (void* p : own) std::free(p);
     return rc;
 }
@@ -129,12 +161,15 @@ int main(int argc, char** argv)
         if (std::getenv("OUHIP_EMU_VERBOSE"))
             std::fprintf(stderr, "case %d: C %d T %d B %d prec %d film %d sc %d cond %d res2 %d in %d head %d rate %d kt %d\n",
                          i, c.C, c.T, c.B, c.prec, c.film, c.sc, c.cond, c.res2, c.in, c.head, c.rate, c.down_kt);
-        const int rc = run(c);
-        if (rc != 0) {
-            std::fprintf(stderr, "case %d: ou_block returned %d: %s\n", i, rc, ouhip_detail::err_buf());
-            return 2;
+        for (int chunk = 0; chunk < 2; ++chunk) {
+            const int rc = run(c, chunk);
+            if (rc != 0) {
+                std::fprintf(stderr, "case %d%s: ou_block returned %d: %s\n", i, chunk ? " (frame range)" : "", rc,
+                             ouhip_detail::err_buf());
+                return 2;
+            }
+            ++n;
         }
-        ++n;
     }
     std::printf("ok: %d fused-block launches bounds-checked\n", n);
     return 0;

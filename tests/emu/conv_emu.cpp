@@ -22,7 +22,10 @@ static float* alloc(size_t n)
     return p;
 }
 
-static int run(const Geom& g, int tile)
+// chunk: launch output frames [U / 3, 2 U / 3 + 1) only, reading x up to the
+// last sample they need (as engine.conv_desc(rng=...) records it), and check
+// that nothing outside those frames' outputs was written
+static int run(const Geom& g, int tile, bool chunk = false)
 {
     const int cin_eff = g.cin * g.frame;
     const int m = g.cout * g.rout;
@@ -58,7 +61,28 @@ static int run(const Geom& g, int tile)
     d.tile = tile & ~(2048 | 4096);
     d.prec = split ? ((tile & 4096) ? 2 : 1) : 0;
     d.w_unscale = unscale;
-    const int rc = ou_conv(&d, nullptr);
+    int a = 0, bnd = U;
+    if (chunk) {
+        a = U / 3;
+        bnd = std::min(U, 2 * U / 3 + 1);
+        d.f0 = a;
+        d.n_frames = bnd - a;
+        d.in_len = std::max(1, std::min(d.in_len, (bnd - d.pad + g.kt - 1) * g.frame + d.shift));
+    }
+    int rc = ou_conv(&d, nullptr);
+    if (rc == 0 && chunk) {
+        for (int b = 0; b < g.B; ++b)
+            for (int c = 0; c < g.cout; ++c)
+                for (int t = 0; t < out_len; ++t) {
+                    const bool mine = t >= a * g.rout && t < bnd * g.rout;
+                    if (!mine && y[((size_t)b * g.cout + c) * out_len + t] != 0.25f) {
+                        std::fprintf(stderr, "EMU: chunk [%d, %d) wrote output sample %d (b %d c %d)\n", a, bnd, t, b, c);
+                        rc = 3;
+                        b = g.B; c = g.cout;
+                        break;
+                    }
+                }
+    }
     for (float* p : {w, x, y, bias, r1, r2, fm, sc}) std::free(p);
     return rc;
 }
@@ -94,7 +118,7 @@ int main(int argc, char** argv)
     const int only = argc > 1 ? std::atoi(argv[1]) : -1;
     int n = 0;
     constexpr int kFirstRsGeom = 10;   // geometries from here on: register-streamed tiles only
-    int nrs = 0;
+    int nrs = 0, nchunk = 0;
     const bool rs_only = std::getenv("OUHIP_EMU_RS_ONLY") != nullptr;   // register-streamed tiles only
     for (int gi = 0; gi < (int)(sizeof(geoms) / sizeof(geoms[0])); ++gi) {
         if (only >= 0 && gi != only) continue;
@@ -119,9 +143,19 @@ int main(int argc, char** argv)
                 }
                 ++n;
                 nrs += tpw >= 6;
+                // the same tile on a frame range of the op (one-tile workgroups)
+                if (tpw == 0 || tpw >= 4) {
+                    const int rc2 = run(g, t | v | ((tpw == 5 || tpw == 7) ? 4096 : 0), true);
+                    if (rc2 != 0) {
+                        std::fprintf(stderr, "geom %d tile %d tpw %d (frame range): ou_conv returned %d\n", gi, t, tpw, rc2);
+                        return 2;
+                    }
+                    ++n;
+                    ++nchunk;
+                }
             }
         }
     }
-    std::printf("ok: %d launches bounds-checked (%d register-streamed)\n", n, nrs);
+    std::printf("ok: %d launches bounds-checked (%d register-streamed, %d on frame ranges)\n", n, nrs, nchunk);
     return 0;
 }
