@@ -519,7 +519,14 @@ int ou_program_size(const ou_program* p);
 int ou_program_run(ou_program* p, void* stream);
 /* Capture the program into a hipGraph (on a private stream) and instantiate. */
 int ou_program_capture(ou_program* p);
-/* Launch the instantiated graph on ``stream``. */
+/* Host-only check of the lane structure (what run / capture validate
+ * first): 0, or < 0 with ou_last_error.  No HIP call.                      */
+int ou_program_validate(const ou_program* p);
+/* Capture every maximal run of kernels on one lane (between two sync ops)
+ * as its own hipGraph instead; ou_program_launch then replays the lanes on
+ * real streams with host-side events, one graph launch per run.            */
+int ou_program_capture_segments(ou_program* p);
+/* Launch the captured program (whole graph, or segments) on ``stream``. */
 int ou_program_launch(ou_program* p, void* stream);
 /* Kind (OU_OP_*) of op i. */
 int ou_program_op_kind(const ou_program* p, int i);

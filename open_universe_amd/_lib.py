@@ -204,6 +204,8 @@ EXPORTS = {
     "ou_program_size": (c_int, [c_void_p]),
     "ou_program_run": (c_int, [c_void_p, c_void_p]),
     "ou_program_capture": (c_int, [c_void_p]),
+    "ou_program_capture_segments": (c_int, [c_void_p]),
+    "ou_program_validate": (c_int, [c_void_p]),
     "ou_program_launch": (c_int, [c_void_p, c_void_p]),
     "ou_program_op_kind": (c_int, [c_void_p, c_int]),
     "ou_program_profile": (c_int, [c_void_p, c_void_p, POINTER(c_float)]),
@@ -411,8 +413,19 @@ class Program:
     def run(self, stream):
         check(self.lib.ou_program_run(self.h, c_void_p(stream)), "program_run")
 
-    def capture(self):
-        check(self.lib.ou_program_capture(self.h), "program_capture")
+    def validate(self):
+        """Host-only lane-structure check (no HIP call): raises on error."""
+        check(self.lib.ou_program_validate(self.h), "program_validate")
+
+    def capture(self, segments=None):
+        """Capture as one hipGraph, or (segments, env OUHIP_GRAPH_MODE=seg)
+        one hipGraph per run of kernels on a lane, replayed on real streams."""
+        import os
+
+        if segments is None:
+            segments = os.environ.get("OUHIP_GRAPH_MODE", "whole") == "seg"
+        fn = self.lib.ou_program_capture_segments if segments else self.lib.ou_program_capture
+        check(fn(self.h), "program_capture")
         self.captured = True
 
     def launch(self, stream):

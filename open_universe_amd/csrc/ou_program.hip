@@ -28,6 +28,15 @@ struct ou_program {
     // lanes: lane 0 runs on the caller's (or the capture) stream, lane i > 0
     // on a side stream; SIGNAL / WAIT ops order them through events[]
     std::vector<hipEvent_t> events;
+    // segmented capture: every maximal run of kernels on one lane between two
+    // sync ops is its own hipGraph, launched on the lane's stream; the sync
+    // ops stay host-side events between them (real streams, real concurrency)
+    struct Seg {
+        int lane;
+        size_t first, last;   // ops [first, last)
+        hipGraphExec_t exec;  // null: a single op, launched directly
+    };
+    std::vector<Seg> segs;
 };
 
 // Streams the programs use besides the caller's: one capture stream and the
@@ -255,6 +264,9 @@ static void drop_graph(ou_program* p)
     if (p->graph) (void)hipGraphDestroy(p->graph);
     p->exec = nullptr;
     p->graph = nullptr;
+    for (auto& sg : p->segs)
+        if (sg.exec) (void)hipGraphExecDestroy(sg.exec);
+    p->segs.clear();
 }
 
 extern "C" {
@@ -363,8 +375,97 @@ int ou_program_capture(ou_program* p)
     return 0;
 }
 
+int ou_program_validate(const ou_program* p)
+{
+    if (!p) return ou_fail(-1, "program_validate: null");
+    int nl = 1, ne = 0;
+    const int rc = validate_lanes(p, &nl, &ne);
+    return rc ? rc : check_side_cycles(p);
+}
+
+int ou_program_capture_segments(ou_program* p)
+{
+    if (!p) return ou_fail(-1, "program_capture_segments: null");
+    drop_graph(p);
+    int nl = 1, ne = 0;
+    int rc = validate_lanes(p, &nl, &ne);
+    if (rc == 0) rc = ensure_sync(p, nl, ne);
+    if (rc) return rc;
+    int dev = 0;
+    if ((rc = current_device(&dev))) return rc;
+    hipStream_t cap = nullptr;
+    if ((rc = shared_stream(&g_cap[dev], &cap))) return rc;
+    int lane = 0;
+    const size_t n = p->ops.size();
+    for (size_t i = 0; i < n;) {
+        const auto& o = p->ops[i];
+        if (is_sync(o.kind)) {
+            if (o.kind == OU_OP_LANE) lane = ((const ou_sync_args*)o.desc.data())->id;
+            ++i;
+            continue;
+        }
+        size_t j = i;
+        while (j < n && !is_sync(p->ops[j].kind)) ++j;
+        ou_program::Seg sg{lane, i, j, nullptr};
+        if (j - i >= 2) {
+            OU_HIP_CHECK(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal), "begin capture");
+            for (size_t k = i; k < j && rc == 0; ++k) rc = run_op(p->ops[k].kind, p->ops[k].desc.data(), cap);
+            hipGraph_t g = nullptr;
+            hipError_t e = hipStreamEndCapture(cap, &g);
+            if (rc == 0 && e != hipSuccess) rc = ou_fail(-100, "end capture: %s", hipGetErrorString(e));
+            if (rc == 0) {
+                e = hipGraphInstantiate(&sg.exec, g, nullptr, nullptr, 0);
+                if (e != hipSuccess) rc = ou_fail(-100, "graph instantiate: %s", hipGetErrorString(e));
+            }
+            if (g) (void)hipGraphDestroy(g);
+            if (rc) {
+                drop_graph(p);
+                return rc;
+            }
+        }
+        p->segs.push_back(sg);
+        i = j;
+    }
+    return 0;
+}
+
+// Replay a segmented capture: lanes on s0 and the side streams as run_lanes,
+// each segment one graph launch.
+static int launch_segments(ou_program* p, hipStream_t s0)
+{
+    int nl = 1, ne = 0, rc = validate_lanes(p, &nl, &ne);
+    if (rc) return rc;
+    hipStream_t side[kMaxSide] = {};
+    if (nl > 1) {
+        int dev = 0;
+        if ((rc = current_device(&dev))) return rc;
+        for (int l = 1; l < nl; ++l)
+            if ((rc = shared_stream(&g_side[dev][l - 1], &side[l - 1]))) return rc;
+    }
+    hipStream_t cur = s0;
+    size_t si = 0;
+    for (size_t i = 0; i < p->ops.size();) {
+        const auto& o = p->ops[i];
+        if (is_sync(o.kind)) {
+            const int v = ((const ou_sync_args*)o.desc.data())->id;
+            if (o.kind == OU_OP_LANE) cur = v == 0 ? s0 : side[v - 1];
+            else if (o.kind == OU_OP_SIGNAL) OU_HIP_CHECK(hipEventRecord(p->events[v], cur), "program signal");
+            else OU_HIP_CHECK(hipStreamWaitEvent(cur, p->events[v], 0), "program wait");
+            ++i;
+            continue;
+        }
+        if (si >= p->segs.size() || p->segs[si].first != i) return ou_fail(-1, "program: segment table out of step");
+        const auto& sg = p->segs[si++];
+        if (sg.exec) OU_HIP_CHECK(hipGraphLaunch(sg.exec, cur), "segment graph launch");
+        else if ((rc = run_op(o.kind, o.desc.data(), cur))) return rc;
+        i = sg.last;
+    }
+    return 0;
+}
+
 int ou_program_launch(ou_program* p, void* stream)
 {
+    if (p && !p->exec && !p->segs.empty()) return launch_segments(p, (hipStream_t)stream);
     if (!p || !p->exec) return ou_fail(-1, "program_launch: not captured");
     OU_HIP_CHECK(hipGraphLaunch(p->exec, (hipStream_t)stream), "graph launch");
     return 0;

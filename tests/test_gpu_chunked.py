@@ -95,3 +95,19 @@ def test_short_clips_are_not_chunked(model, monkeypatch):
     assert eng.chunk_plan(1, 128160) is not None
     assert eng.chunk_plan(1, 160 * 60) is None   # T4 = 60: too few GRU steps to split
     assert eng.chunk_plan(8, 128160) is None     # wide batches fill the chip without it
+
+
+@pytest.mark.parametrize("chunk", [False, True], ids=["lanes", "chunked"])
+def test_segment_capture_equals_whole_graph(chunk, monkeypatch):
+    """ou_program_capture_segments (one hipGraph per run of kernels on a
+    lane, lanes on real streams) replays the same program bit for bit."""
+    m = _model(1)
+    eng = m._get_engine()
+    T = 64000
+    mix = (0.1 * torch.randn(1, 1, T, generator=torch.Generator().manual_seed(5))).to(DEV)
+    p = EnhancePlan(eng, 1, T, 8, 1.3, chunk=chunk)
+    a = p(mix, torch.Generator(device=DEV).manual_seed(9), use_graph=False).clone()
+    p.prog.capture(segments=True)
+    b = p(mix, torch.Generator(device=DEV).manual_seed(9)).clone()
+    c = p(mix, torch.Generator(device=DEV).manual_seed(9)).clone()
+    assert torch.equal(a, b) and torch.equal(a, c)
