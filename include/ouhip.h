@@ -347,7 +347,8 @@ int ou_snake_aa(const ou_snake_desc* d, void* stream);
 /* ------------------------------------------------------------------------
  * Fused ConvBlock main path (ou_block.hip): the three PReLU_Conv calls of a
  * ConvBlock and the arithmetic between them in one launch, for channel
- * counts whose whole channel range fits one workgroup (32, 64, 128; 256 and
+ * counts whose whole channel range fits one workgroup (32, 64, 128, and
+ * PP24's 96 and 192; 256 and
  * 512 stay on ou_conv, see ou_block_supported) and
  * split-f16 / f16 operands.  Replaces blocks.py:393-416:
  *   c1 = conv1(h) (k5);  c1 = (c1 + sc) * s_sc;  c1 = film(c1);  cond_out = c1

@@ -18,7 +18,8 @@
 // the CU: per block the HBM traffic drops from 3 reads + 3 writes (+ the
 // residual re-read) of a C x T tensor to 1 read + 1 write, and 3 kernel
 // latencies become 1.  Halo frames are recomputed by the neighbouring
-// workgroup (F = 124 / 60 / 28 frames at C = 32 / 64 / 128).
+// workgroup (F = 124 / 60 / 28 frames at C = 32 / 64 / 128; 124 / 60 at
+// PP24's 96 / 192).
 //
 // Arithmetic is the split-f16 form of ou_conv (P = 1): every operand is
 // v = hi + lo * 2^-11 (f16 halves; weights packed by ou_block_pack with a
@@ -62,6 +63,12 @@ constexpr int kStageShift = 6;   // activations are staged as x * 2^-6 (ou_conv'
 #ifndef OU_BLOCK_NT128
 #define OU_BLOCK_NT128 1
 #endif
+#ifndef OU_BLOCK_NT96
+#define OU_BLOCK_NT96 4    // PP24 level 1 (a multiple of its 4 waves along N)
+#endif
+#ifndef OU_BLOCK_NT192
+#define OU_BLOCK_NT192 2   // PP24 level 2 (2 x 2 waves)
+#endif
 #ifndef OU_BLOCK_RING1
 #define OU_BLOCK_RING1 6   // weight-fragment ring depth (k-steps) of one-m-tile waves
 #endif
@@ -78,7 +85,9 @@ struct BCfg {
     static constexpr int WAVES = 4;                // waves per workgroup (block_threads() must agree;
                                                    // 8 waves at C = 256 measured slower: 64 vs 53 us)
     static constexpr int NTH = 64 * WAVES;
-    static constexpr int WM = MT >= WAVES ? WAVES : MT;   // waves along M
+    // waves along M: the largest of 4 / 2 / 1 that divides the M tiles
+    // (96 channels: 1 x 4 waves, 3 M tiles each; 192: 2 x 2, 3 each)
+    static constexpr int WM = MT % WAVES == 0 ? WAVES : MT % 2 == 0 ? 2 : 1;
     static constexpr int WN = WAVES / WM;          // waves along N (frames)
     static constexpr int MR = MT / WM;             // M tiles per wave
     static constexpr int NR = NT / WN;             // N tiles per wave
@@ -286,8 +295,18 @@ constexpr int block_threads()
     return C > 0 ? 256 : 0;
 }
 
+// resident workgroups per CU the register budget is sized for: two (256
+// VGPRs a lane) where a wave owns one or two M tiles; one (512) for PP24's
+// 96 / 192 channels, whose waves own three M tiles (their ~107 KB of LDS
+// allows one workgroup per CU anyway)
+template <int C>
+constexpr int block_min_wgs()
+{
+    return (C == 96 || C == 192) ? 1 : 2;
+}
+
 template <int C, int NT, int P, int EPI, int R = 1, int KF = 1>
-__global__ __launch_bounds__(block_threads<C>(), block_threads<C>() == 256 ? 2 : 1) void block_kernel(ou_block_desc d)
+__global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_kernel(ou_block_desc d)
 {
     using K = BCfg<C, NT, P>;
     constexpr int MR = K::MR, NR = K::NR, NF = K::NF, SX = K::SX;
@@ -710,7 +729,8 @@ int launch_epi(const ou_block_desc& d, hipStream_t s)
 template <int C>
 constexpr int nt_for()
 {
-    return C == 32 ? OU_BLOCK_NT32 : C == 64 ? OU_BLOCK_NT64 : C == 128 ? OU_BLOCK_NT128 : 1;
+    return C == 32 ? OU_BLOCK_NT32 : C == 64 ? OU_BLOCK_NT64 : C == 128 ? OU_BLOCK_NT128
+         : C == 96 ? OU_BLOCK_NT96 : C == 192 ? OU_BLOCK_NT192 : 1;
 }
 
 template <int P>
@@ -720,6 +740,8 @@ int launch_p(const ou_block_desc& d, hipStream_t s)
     case 32: return launch_epi<32, nt_for<32>(), P>(d, s);
     case 64: return launch_epi<64, nt_for<64>(), P>(d, s);
     case 128: return launch_epi<128, nt_for<128>(), P>(d, s);
+    case 96: return launch_epi<96, nt_for<96>(), P>(d, s);
+    case 192: return launch_epi<192, nt_for<192>(), P>(d, s);
     case 256: return launch_epi<256, 1, P>(d, s);
     }
     return ou_fail(-1, "block: unsupported channel count %d", d.channels);
@@ -735,7 +757,8 @@ int launch_p(const ou_block_desc& d, hipStream_t s)
 // it is 2.0x / 1.4x / 1.2x faster than the unfused launches.
 extern "C" int ou_block_supported(int channels, int prec)
 {
-    return (prec == 1 || prec == 2) && (channels == 32 || channels == 64 || channels == 128);
+    return (prec == 1 || prec == 2) &&
+           (channels == 32 || channels == 64 || channels == 128 || channels == 96 || channels == 192);
 }
 
 extern "C" int ou_block_down_supported(int channels, int rate, int kt, int prec)
@@ -749,6 +772,8 @@ extern "C" int ou_block_frames(int channels)
     case 32: return BCfg<32, nt_for<32>(), 1>::F;
     case 64: return BCfg<64, nt_for<64>(), 1>::F;
     case 128: return BCfg<128, nt_for<128>(), 1>::F;
+    case 96: return BCfg<96, nt_for<96>(), 1>::F;
+    case 192: return BCfg<192, nt_for<192>(), 1>::F;
     case 256: return BCfg<256, 1, 1>::F;
     }
     return 0;

@@ -127,7 +127,7 @@ int main(int argc, char** argv)
 {
     std::vector<Case> cases;
     for (int prec : {1, 2})
-        for (int C : {32, 64, 128}) {
+        for (int C : {32, 64, 128, 96, 192}) {
             const int F = ou_block_frames(C);
             // ragged lengths: shorter than a workgroup, just past one, not a multiple
             for (int T : {7, F + 1, 3 * F - 5}) {
