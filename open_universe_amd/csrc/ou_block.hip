@@ -43,6 +43,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <vector>
 
 #include "../../include/ouhip.h"
 #include "ou_common.h"
@@ -63,6 +64,9 @@ constexpr int kStageShift = 6;   // activations are staged as x * 2^-6 (ou_conv'
 #ifndef OU_BLOCK_NT128
 #define OU_BLOCK_NT128 1
 #endif
+#ifndef OU_BLOCK_NT48
+#define OU_BLOCK_NT48 4    // PP24 level 0 (2 x 2 waves, rows padded to 64)
+#endif
 #ifndef OU_BLOCK_NT96
 #define OU_BLOCK_NT96 4    // PP24 level 1 (a multiple of its 4 waves along N)
 #endif
@@ -81,7 +85,8 @@ constexpr int kStageShift = 6;   // activations are staged as x * 2^-6 (ou_conv'
 
 template <int C, int NT, int P>
 struct BCfg {
-    static constexpr int MT = C / 32;              // 32-row M tiles (output channels)
+    static constexpr int MT = (C + 31) / 32;       // 32-row M tiles (output channels; 48: rows 48-63
+                                                   // are zero-weight padding, computed, never stored)
     static constexpr int WAVES = 4;                // waves per workgroup (block_threads() must agree;
                                                    // 8 waves at C = 256 measured slower: 64 vs 53 us)
     static constexpr int NTH = 64 * WAVES;
@@ -104,7 +109,7 @@ struct BCfg {
     static constexpr int LDS_BYTES = 2 * (NPL * PA + NPL * PB);
     static constexpr int KS = C / 16;              // 16-channel k-steps per tap
     static constexpr int RING = MR == 1 ? OU_BLOCK_RING1 : 4;   // weight-fragment ring depth (k-steps)
-    static_assert(C % 32 == 0 && WM * WN == WAVES && MT % WM == 0 && NT % WN == 0, "block tiling");
+    static_assert(C % 16 == 0 && WM * WN == WAVES && MT % WM == 0 && NT % WN == 0, "block tiling");
     static_assert((SX / 8) % 2 == 1, "LDS row stride must be an odd number of 16-B slots");
 };
 
@@ -390,6 +395,12 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     floatx16 acc[MR][NR], accx[MR][NR];
     // per-row constants of this wave's output rows: m = row(mr, r)
     auto row = [&](int mr, int r) { return (wm * MR + mr) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };
+    // C not a multiple of 32 (48): rows >= C are padding -- loads clamp to a
+    // real row (the value is never stored), stores skip them
+    constexpr bool PADM = C % 32 != 0;
+    auto rowc = [&](int mr, int r) { return PADM ? min(row(mr, r), C - 1) : row(mr, r); };
+    auto rok = [&](int mr, int r) { return !PADM || row(mr, r) < C; };
+    auto gok = [&](int mr, int j) { return !PADM || (wm * MR + mr) * 32 + 8 * j + 4 * h < C; };
 
     // ---- stage 1: conv1 (k5) over frames t0 - 2 + u, u in [0, NF) -> region B
     stage_mma<5, C, NT, P>((const half8_t*)d.w[0], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
@@ -402,7 +413,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
         for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int m = row(mr, r);
+                const int m = rowc(mr, r);
                 bia[mr][r] = d.bias[0] ? d.bias[0][m] : 0.f;
                 if constexpr (EPI & kEpiFilm) {
                     gam[mr][r] = film[m];
@@ -437,11 +448,13 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                     if (inside && t >= t0 && t < t0 + F && t < TS) {
                         float* co = d.cond_out + (int64_t)b * d.co_bstride + t;
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) co[(int64_t)row(mr, r) * d.co_cstride] = o[r];
+                        for (int r = 0; r < 16; ++r)
+                            if (rok(mr, r)) co[(int64_t)row(mr, r) * d.co_cstride] = o[r];
                     }
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
+                    if (!gok(mr, j)) continue;
                     float x[4];
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
@@ -472,7 +485,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) bia[mr][r] = d.bias[1] ? d.bias[1][row(mr, r)] : 0.f;
+            for (int r = 0; r < 16; ++r) bia[mr][r] = d.bias[1] ? d.bias[1][rowc(mr, r)] : 0.f;
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
@@ -482,6 +495,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                 const float keep = (t >= 0 && t < T) ? kIn : 0.f;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
+                    if (!gok(mr, j)) continue;
                     float x[4];
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
@@ -523,17 +537,24 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
 #pragma unroll
                     for (int r = 0; r < 16; ++r) hv[mr][nr][r] = in_conv(row(mr, r), xl, xm, xr);
             } else {
+                // frames outside [h0, h1) (a chunk's caller has not produced
+                // them) feed no stored output; zero, so that kEpiDown's
+                // re-split of those frames cannot trip the range flag
+                const bool hk = t >= hlo && t < hhi;
 #pragma unroll
                 for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) hv[mr][nr][r] = hb[(int64_t)row(mr, r) * d.h_cstride + tc];
+                    for (int r = 0; r < 16; ++r) {
+                        const float v = hb[(int64_t)rowc(mr, r) * d.h_cstride + tc];
+                        hv[mr][nr][r] = hk ? v : 0.f;
+                    }
             }
             if constexpr (EPI & kEpiRes2) {
 #pragma unroll
                 for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
                     for (int r = 0; r < 16; ++r)
-                        rv[mr][nr][r] = d.res2[(int64_t)b * d.r2_bstride + (int64_t)row(mr, r) * d.r2_cstride + tc];
+                        rv[mr][nr][r] = d.res2[(int64_t)b * d.r2_bstride + (int64_t)rowc(mr, r) * d.r2_cstride + tc];
             }
         }
     };
@@ -546,7 +567,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) bia[mr][r] = d.bias[2] ? d.bias[2][row(mr, r)] : 0.f;
+            for (int r = 0; r < 16; ++r) bia[mr][r] = d.bias[2] ? d.bias[2][rowc(mr, r)] : 0.f;
         if constexpr (EPI & kEpiHead) {
             // the score head on the block output: Y[w][c] = prelu2(prelu1(y))
             // (f32, region A, zero outside [0, T)), then one thread per frame
@@ -618,7 +639,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                         v = (v + hv[mr][nr][r]) * d.s_res;
                         if constexpr (EPI & kEpiRes2) v = (v + rv[mr][nr][r]) * d.s2;
                         vv[r] = v;
-                        if (own) yb[(int64_t)row(mr, r) * d.y_cstride + t] = v;
+                        if (own && rok(mr, r)) yb[(int64_t)row(mr, r) * d.y_cstride + t] = v;
                     }
                     if constexpr (EPI & kEpiDown) {
                         constexpr int RH = R * (KF - 1 - (KF - 1) / 2);
@@ -633,6 +654,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                             }
                             half4_t hi, lo;
                             split4<P>(x[0], x[1], x[2], x[3], hi, lo, ovf);
+                            if (!gok(mr, j)) continue;
                             _Float16* dst = xa + w * SX + (wm * MR + mr) * 32 + 8 * j + 4 * h;
                             *(half4_t*)dst = hi;
                             if constexpr (P == 1) *(half4_t*)(dst + K::PA) = lo;
@@ -730,7 +752,7 @@ template <int C>
 constexpr int nt_for()
 {
     return C == 32 ? OU_BLOCK_NT32 : C == 64 ? OU_BLOCK_NT64 : C == 128 ? OU_BLOCK_NT128
-         : C == 96 ? OU_BLOCK_NT96 : C == 192 ? OU_BLOCK_NT192 : 1;
+         : C == 48 ? OU_BLOCK_NT48 : C == 96 ? OU_BLOCK_NT96 : C == 192 ? OU_BLOCK_NT192 : 1;
 }
 
 template <int P>
@@ -740,6 +762,7 @@ int launch_p(const ou_block_desc& d, hipStream_t s)
     case 32: return launch_epi<32, nt_for<32>(), P>(d, s);
     case 64: return launch_epi<64, nt_for<64>(), P>(d, s);
     case 128: return launch_epi<128, nt_for<128>(), P>(d, s);
+    case 48: return launch_epi<48, nt_for<48>(), P>(d, s);
     case 96: return launch_epi<96, nt_for<96>(), P>(d, s);
     case 192: return launch_epi<192, nt_for<192>(), P>(d, s);
     case 256: return launch_epi<256, 1, P>(d, s);
@@ -758,7 +781,8 @@ int launch_p(const ou_block_desc& d, hipStream_t s)
 extern "C" int ou_block_supported(int channels, int prec)
 {
     return (prec == 1 || prec == 2) &&
-           (channels == 32 || channels == 64 || channels == 128 || channels == 96 || channels == 192);
+           (channels == 32 || channels == 64 || channels == 128 || channels == 48 || channels == 96 ||
+            channels == 192);
 }
 
 extern "C" int ou_block_down_supported(int channels, int rate, int kt, int prec)
@@ -772,6 +796,7 @@ extern "C" int ou_block_frames(int channels)
     case 32: return BCfg<32, nt_for<32>(), 1>::F;
     case 64: return BCfg<64, nt_for<64>(), 1>::F;
     case 128: return BCfg<128, nt_for<128>(), 1>::F;
+    case 48: return BCfg<48, nt_for<48>(), 1>::F;
     case 96: return BCfg<96, nt_for<96>(), 1>::F;
     case 192: return BCfg<192, nt_for<192>(), 1>::F;
     case 256: return BCfg<256, 1, 1>::F;
@@ -781,12 +806,18 @@ extern "C" int ou_block_frames(int channels)
 
 extern "C" int64_t ou_block_packed_halves(int channels, int kt)
 {
-    return (int64_t)channels * channels * kt * 2;
+    return (int64_t)(channels + 31) / 32 * 32 * channels * kt * 2;   // rows padded to 32
 }
 
 extern "C" int ou_block_pack(const float* w, int channels, int kt, void* out, float* w_unscale)
 {
-    return ou_block_pack_rect(w, channels, channels, kt, out, w_unscale);
+    if (channels % 32 == 0 || !w || channels <= 0 || kt <= 0)
+        return ou_block_pack_rect(w, channels, channels, kt, out, w_unscale);
+    // 48 channels: zero rows up to the next 32 (ou_block computes, never stores, them)
+    const int m = (channels + 31) / 32 * 32;
+    std::vector<float> wp((size_t)m * channels * kt, 0.f);
+    std::copy(w, w + (size_t)channels * channels * kt, wp.begin());
+    return ou_block_pack_rect(wp.data(), m, channels, kt, out, w_unscale);
 }
 
 extern "C" int ou_block_pack_rect(const float* w, int m, int channels, int kt, void* out, float* w_unscale)

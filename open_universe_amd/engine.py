@@ -336,7 +336,10 @@ def prep_fused(specs, C, prec, device):
         return None
     parts, offs, uns, off = [], [], [], 0
     for sp in specs:
-        packed, un = L.block_pack_np(sp.w)
+        w = sp.w
+        if w.shape[0] % 32:   # 48 channels: zero rows up to the next 32 (computed, never stored)
+            w = np.concatenate([w, np.zeros((-w.shape[0] % 32,) + w.shape[1:], w.dtype)])
+        packed, un = L.block_pack_np(w)
         parts.append(packed)
         offs.append(off)
         uns.append(un)

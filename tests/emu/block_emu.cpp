@@ -28,6 +28,11 @@ void* pack(int m, int C, int kt, float* unscale)
 {
     std::vector<float> w((size_t)m * C * kt);
     for (size_t i = 0; i < w.size(); ++i) w[i] = 0.01f * (float)((i * 37) % 17) - 0.08f;
+    if (m == C) {   // the block's own convs: ou_block_pack (rows padded to 32 at 48 channels)
+        void* out = std::malloc((size_t)ou_block_packed_halves(C, kt) * sizeof(_Float16));
+        if (ou_block_pack(w.data(), C, kt, out, unscale) != 0) std::abort();
+        return out;
+    }
     void* out = std::malloc((size_t)m * C * kt * 2 * sizeof(_Float16));
     if (ou_block_pack_rect(w.data(), m, C, kt, out, unscale) != 0) std::abort();
     return out;
@@ -127,7 +132,7 @@ int main(int argc, char** argv)
 {
     std::vector<Case> cases;
     for (int prec : {1, 2})
-        for (int C : {32, 64, 128, 96, 192}) {
+        for (int C : {32, 64, 128, 48, 96, 192}) {
             const int F = ou_block_frames(C);
             // ragged lengths: shorter than a workgroup, just past one, not a multiple
             for (int T : {7, F + 1, 3 * F - 5}) {

@@ -128,3 +128,18 @@ def test_conv_values_match_reference(tmp_path):
     for p in procs:
         out, err = p.communicate(timeout=900)
         assert p.returncode == 0 and "ok:" in out, (out[-2000:], err[-2000:])
+
+
+def test_block_values_match_reference(tmp_path):
+    """Fiber emulation of ou_block against a double-precision evaluation of
+    the ConvBlock formula at 32 / 48 / 64 / 96 / 128 / 192 channels (48:
+    padded MFMA rows), split-f16 and f16, FiLM / input_cond / cond_out /
+    res2, whole-signal and on frame ranges (garbage h outside [h0, h1))."""
+    exe = str(tmp_path / "block_emu_values")
+    _build("block_emu_values.cpp", exe, "-O0", "-DOU_EMU_FIBERS")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    procs = [subprocess.Popen([exe, str(g)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+             for g in range(6)]
+    for p in procs:
+        out, err = p.communicate(timeout=1200)
+        assert p.returncode == 0 and "ok:" in out, (out[-2000:], err[-2000:])
