@@ -348,9 +348,9 @@ int ou_snake_aa(const ou_snake_desc* d, void* stream);
  * Fused ConvBlock main path (ou_block.hip): the three PReLU_Conv calls of a
  * ConvBlock and the arithmetic between them in one launch, for channel
  * counts whose whole channel range fits one workgroup (32, 64, 128, and
- * PP24's 96 and 192; 256 and
+ * PP24's 48, 96 and 192; 256 and
  * 512 stay on ou_conv, see ou_block_supported) and
- * split-f16 / f16 operands.  Replaces blocks.py:393-416:
+ * split-f16 / f16 / f32 operands.  Replaces blocks.py:393-416:
  *   c1 = conv1(h) (k5);  c1 = (c1 + sc) * s_sc;  c1 = film(c1);  cond_out = c1
  *   y  = ((h + conv3(conv2(c1))) * s_res + res2) * s2        (k3, k3)
  * Each conv applies its scalar PReLU slope to its input; frames outside
@@ -361,7 +361,7 @@ typedef struct ou_block_desc {
     const float* h;            /* block input [B][C][T]                          */
     int64_t h_bstride, h_cstride;
     int32_t channels, length;  /* C, T                                           */
-    int32_t batch, prec;       /* prec 1 split-f16, 2 f16                        */
+    int32_t batch, prec;       /* prec 0 f32, 1 split-f16, 2 f16                 */
     const void* w[3];          /* conv1 (k5), conv2, conv3 (k3): ou_block_pack   */
     const float* bias[3];      /* [C] or NULL                                    */
     float slope[3];            /* PReLU slope on each conv's input               */
@@ -430,6 +430,11 @@ int ou_block_pack(const float* w, int channels, int kt, void* out, float* w_unsc
 /* The same packing for w[m][channels][kt] (m % 32 == 0, channels % 16 == 0):
  * the fused rate-change conv's 2C x C x (down_kt * rate) weights.            */
 int ou_block_pack_rect(const float* w, int m, int channels, int kt, void* out, float* w_unscale);
+/* f32 operands (prec 0): floats of the packed conv, and the packing
+ * [m-tile][tap][4 channel pairs][lane][4] (lane l: row l & 31, channel
+ * 2 pair + (l >> 5); rows padded to 32); *w_unscale = 2^6. */
+int64_t ou_block_packed_f32(int channels, int kt);
+int ou_block_pack_f32(const float* w, int channels, int kt, float* out, float* w_unscale);
 /* 1 when ou_block fuses the rate-change conv for (channels, rate, kt, prec). */
 int ou_block_down_supported(int channels, int rate, int kt, int prec);
 int ou_block(const ou_block_desc* d, void* stream);

@@ -188,6 +188,8 @@ EXPORTS = {
     "ou_block_frames": (c_int, [c_int]),
     "ou_block_packed_halves": (c_int64, [c_int, c_int]),
     "ou_block_pack": (c_int, [POINTER(c_float), c_int, c_int, c_void_p, POINTER(c_float)]),
+    "ou_block_packed_f32": (c_int64, [c_int, c_int]),
+    "ou_block_pack_f32": (c_int, [POINTER(c_float), c_int, c_int, POINTER(c_float), POINTER(c_float)]),
     "ou_block_pack_rect": (c_int, [POINTER(c_float), c_int, c_int, c_int, c_void_p, POINTER(c_float)]),
     "ou_block_down_supported": (c_int, [c_int, c_int, c_int, c_int]),
     "ou_block": (c_int, [POINTER(BlockDesc), c_void_p]),
@@ -321,6 +323,32 @@ def block_pack_np(w_logical):
     hi, lo = _hi_lo(np.ascontiguousarray(a))
     out = np.stack([hi, lo], axis=3)                                                   # mt, k, ks, part, h, r, i
     return np.ascontiguousarray(out).reshape(-1).view(np.int16), unscale
+
+
+def block_pack_f32_np(w_logical):
+    """ou_block_pack_f32 restated with numpy (byte-identical): [mt][tap][s4]
+    [lane = h*32 + r][j] of w[mt*32 + r][2 (4 s4 + j) + h][tap] (rows already
+    padded to a multiple of 32); w_unscale = 2^6."""
+    import numpy as np
+
+    w = np.ascontiguousarray(w_logical, dtype=np.float32)
+    m, c, kt = w.shape
+    assert m % 32 == 0 and c % 16 == 0, w.shape
+    a = w.reshape(m // 32, 32, c // 8, 4, 2, kt).transpose(0, 5, 2, 4, 1, 3)   # mt, k, s4, h, r, j
+    return np.ascontiguousarray(a).reshape(-1), 64.0
+
+
+def block_pack_f32(w_logical):
+    """ou_block_pack_f32 through the C ABI (channels x channels x kt)."""
+    import numpy as np
+
+    w = np.ascontiguousarray(w_logical, dtype=np.float32)
+    c, _, kt = w.shape
+    out = np.empty(load().ou_block_packed_f32(c, kt), dtype=np.float32)
+    un = c_float(0.0)
+    check(load().ou_block_pack_f32(w.ctypes.data_as(POINTER(c_float)), c, kt, out.ctypes.data_as(POINTER(c_float)),
+                                   ctypes.byref(un)), "block_pack_f32")
+    return out, float(un.value)
 
 
 def conv_pack_split(w_logical):

@@ -43,6 +43,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/ouhip.h"
@@ -51,6 +52,7 @@
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
 typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -98,19 +100,24 @@ struct BCfg {
     static constexpr int NR = NT / WN;             // N tiles per wave
     static constexpr int NF = 32 * NT;             // frames of one conv stage
     static constexpr int F = NF - 4;               // output frames per workgroup
-    static constexpr int SX = C + 8;               // LDS row stride in halves
+    // LDS element: f16 halves (split-f16 hi | lo planes, f16), f32 (prec 0)
+    using E = std::conditional_t<P == 0, float, _Float16>;
+    // row stride in elements, an odd number of 16-B slots (conflict-free
+    // 16-B reads of 32 consecutive rows)
+    static constexpr int SX = P == 0 ? C + 4 : C + 8;
     static constexpr int R1 = NF + 4;              // conv1 input rows (frames t0-4 ..)
     static constexpr int R2 = NF + 2;              // conv2 / conv3 input rows
     static constexpr int NPL = P == 1 ? 2 : 1;     // planes: hi (+ lo)
-    static constexpr int PA = R1 * SX;             // plane stride of region A (halves)
+    static constexpr int PA = R1 * SX;             // plane stride of region A (elements)
     static constexpr int PB = R2 * SX;             // plane stride of region B
     static constexpr int A_OFF = 0;                // region A: conv1 input, then conv3 input
     static constexpr int B_OFF = NPL * PA;         // region B: conv2 input
-    static constexpr int LDS_BYTES = 2 * (NPL * PA + NPL * PB);
+    static constexpr int LDS_BYTES = (int)sizeof(E) * (NPL * PA + NPL * PB);
     static constexpr int KS = C / 16;              // 16-channel k-steps per tap
     static constexpr int RING = MR == 1 ? OU_BLOCK_RING1 : 4;   // weight-fragment ring depth (k-steps)
     static_assert(C % 16 == 0 && WM * WN == WAVES && MT % WM == 0 && NT % WN == 0, "block tiling");
-    static_assert((SX / 8) % 2 == 1, "LDS row stride must be an odd number of 16-B slots");
+    static_assert((SX * (int)sizeof(E) / 16) % 2 == 1 && (SX * (int)sizeof(E)) % 16 == 0,
+                  "LDS row stride must be an odd number of 16-B slots");
 };
 
 __device__ __forceinline__ float prelu(float v, float a) { return v >= 0.f ? v : a * v; }
@@ -176,6 +183,80 @@ __device__ __forceinline__ void stage_mma(const half8_t* __restrict__ wp, const 
                         __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][mr][1], b[nr], accx[mr][nr], 0, 0, 0);
                 }
             }
+    }
+}
+
+// The f32-operand form (prec 0) of one conv stage: v_mfma_f32_32x32x2_f32
+// over KT taps x C / 2 channel pairs.  LDS rows hold f32 channels in
+// pair-split order (even channels in the first half row, odd in the second:
+// ch_pos), so lane half h reads channel 2s + h of 4 consecutive pair steps
+// as one 16-B read; wp: ou_block_pack_f32, [mt][tap][s4][lane][4].
+template <int C>
+__device__ __forceinline__ int ch_pos(int c)
+{
+    return (c & 1) * (C / 2) + (c >> 1);
+}
+
+template <int KT, int C, int NT>
+__device__ __forceinline__ void stage_mma_f32(const f32x4_t* __restrict__ wp, const float* xin, int wm, int wn,
+                                              int lane, int dbg,
+                                              floatx16 (&acc)[BCfg<C, NT, 0>::MR][BCfg<C, NT, 0>::NR])
+{
+    using K = BCfg<C, NT, 0>;
+    constexpr int MR = K::MR, NR = K::NR, S4 = C / 8, NS = KT * S4;
+    const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[mr][nr][r] = 0.f;
+        }
+    if (dbg & 2) return;
+    constexpr int D = NS < 4 ? NS : 4;
+    f32x4_t ra[D][MR];
+    auto load_a = [&](int s, f32x4_t (&dst)[MR]) {
+        const int k = s / S4, s4 = s - (s / S4) * S4;
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr) dst[mr] = wp[(((int64_t)(wm * MR + mr) * KT + k) * S4 + s4) * 64 + lane];
+    };
+#pragma unroll
+    for (int s = 0; s < D - 1; ++s) load_a(s, ra[s]);
+    const float* xb = xin + (wn * NR * 32 + l32) * K::SX + h * (C / 2);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        if (s + D - 1 < NS) load_a(s + D - 1, ra[(s + D - 1) % D]);
+        if constexpr (OU_BLOCK_FENCE) asm volatile("" ::: "memory");
+        const int k = s / S4, s4 = s - (s / S4) * S4;
+        f32x4_t bq[NR];
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) bq[nr] = *(const f32x4_t*)(xb + (nr * 32 + k) * K::SX + 4 * s4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                for (int nr = 0; nr < NR; ++nr)
+                    acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[s % D][mr][j], bq[nr][j], acc[mr][nr], 0, 0, 0);
+    }
+}
+
+// One conv stage on a wave's tiles: split-f16 / f16 (acc + the cross terms in
+// accx) or f32 operands (accx stays zero).
+template <int KT, int C, int NT, int P>
+__device__ __forceinline__ void run_stage(const void* w, const typename BCfg<C, NT, P>::E* xin, int pstride, int wm,
+                                          int wn, int lane, int dbg,
+                                          floatx16 (&acc)[BCfg<C, NT, P>::MR][BCfg<C, NT, P>::NR],
+                                          floatx16 (&accx)[BCfg<C, NT, P>::MR][BCfg<C, NT, P>::NR])
+{
+    if constexpr (P == 0) {
+        stage_mma_f32<KT, C, NT>((const f32x4_t*)w, xin, wm, wn, lane, dbg, acc);
+#pragma unroll
+        for (int mr = 0; mr < BCfg<C, NT, P>::MR; ++mr)
+#pragma unroll
+            for (int nr = 0; nr < BCfg<C, NT, P>::NR; ++nr) accx[mr][nr] = floatx16{};
+    } else {
+        stage_mma<KT, C, NT, P>((const half8_t*)w, xin, pstride, wm, wn, lane, dbg, acc, accx);
     }
 }
 
@@ -319,9 +400,10 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     constexpr int F = block_f<C, NT, P, EPI, R, KF>();
     constexpr float kIn = 1.f / (1 << kStageShift);
     OU_DYNAMIC_LDS(half8_t, lds8);
-    _Float16* lds = (_Float16*)lds8;
-    _Float16* xa = lds + K::A_OFF;
-    _Float16* xbuf = lds + K::B_OFF;
+    using E = typename K::E;
+    E* lds = (E*)lds8;
+    E* xa = lds + K::A_OFF;
+    E* xbuf = lds + K::B_OFF;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave % K::WM, wn = wave / K::WM;
     const int l32 = lane & 31, h = lane >> 5;
@@ -381,13 +463,19 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
             float x[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) x[i] = (v[it][i] >= 0.f ? kIn : a1 * kIn) * v[it][i];
-            half4_t h0, h1, l0, l1;
-            split4<P>(x[0], x[1], x[2], x[3], h0, l0, ovf);
-            split4<P>(x[4], x[5], x[6], x[7], h1, l1, ovf);
-            _Float16* dst = xa + r * SX + 8 * g;
-            *(half8_t*)dst = half8_t{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-            if constexpr (P == 1)
-                *(half8_t*)(dst + K::PA) = half8_t{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+            if constexpr (P == 0) {   // f32, pair-split channel order (ch_pos)
+                E* row = xa + r * SX;
+                *(f32x4_t*)(row + 4 * g) = f32x4_t{x[0], x[2], x[4], x[6]};
+                *(f32x4_t*)(row + C / 2 + 4 * g) = f32x4_t{x[1], x[3], x[5], x[7]};
+            } else {
+                half4_t h0, h1, l0, l1;
+                split4<P>(x[0], x[1], x[2], x[3], h0, l0, ovf);
+                split4<P>(x[4], x[5], x[6], x[7], h1, l1, ovf);
+                E* dst = xa + r * SX + 8 * g;
+                *(half8_t*)dst = half8_t{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+                if constexpr (P == 1)
+                    *(half8_t*)(dst + K::PA) = half8_t{l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+            }
         }
     }
     __syncthreads();
@@ -401,9 +489,31 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     auto rowc = [&](int mr, int r) { return PADM ? min(row(mr, r), C - 1) : row(mr, r); };
     auto rok = [&](int mr, int r) { return !PADM || row(mr, r) < C; };
     auto gok = [&](int mr, int j) { return !PADM || (wm * MR + mr) * 32 + 8 * j + 4 * h < C; };
+    // a stage output: channels c0 .. c0 + 3 (c0 % 4 == 0) of one LDS row, as
+    // the next stage's operand (split halves, or f32 in ch_pos order)
+    auto put4 = [&](E* row, int c0, const float (&x)[4], int pstride) {
+        if constexpr (P == 0) {
+            *(float2_t*)(row + (c0 >> 1)) = float2_t{x[0], x[2]};
+            *(float2_t*)(row + C / 2 + (c0 >> 1)) = float2_t{x[1], x[3]};
+        } else {
+            half4_t hi, lo;
+            split4<P>(x[0], x[1], x[2], x[3], hi, lo, ovf);
+            *(half4_t*)(row + c0) = hi;
+            if constexpr (P == 1) *(half4_t*)(row + c0 + pstride) = lo;
+        }
+    };
+    auto zero8 = [&](E* row, int c0, int pstride) {   // channels c0 .. c0 + 7 (c0 % 8 == 0)
+        if constexpr (P == 0) {
+            *(f32x4_t*)(row + (c0 >> 1)) = f32x4_t{};
+            *(f32x4_t*)(row + C / 2 + (c0 >> 1)) = f32x4_t{};
+        } else {
+            *(half8_t*)(row + c0) = half8_t{};
+            if constexpr (P == 1) *(half8_t*)(row + c0 + pstride) = half8_t{};
+        }
+    };
 
     // ---- stage 1: conv1 (k5) over frames t0 - 2 + u, u in [0, NF) -> region B
-    stage_mma<5, C, NT, P>((const half8_t*)d.w[0], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
+    run_stage<5, C, NT, P>(d.w[0], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
     {
         const float a2 = d.slope[1];
         // operands of the epilogue, loaded before anything is stored
@@ -461,24 +571,16 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                         const float q = o[4 * j + i];
                         x[i] = (q >= 0.f ? kIn : a2 * kIn) * q;
                     }
-                    half4_t hi, lo;
-                    split4<P>(x[0], x[1], x[2], x[3], hi, lo, ovf);
-                    _Float16* dst = xbuf + u * SX + (wm * MR + mr) * 32 + 8 * j + 4 * h;
-                    *(half4_t*)dst = hi;
-                    if constexpr (P == 1) *(half4_t*)(dst + K::PB) = lo;
+                    put4(xbuf + u * SX, (wm * MR + mr) * 32 + 8 * j + 4 * h, x, K::PB);
                 }
             }
         // rows NF, NF + 1 feed only discarded conv2 columns: keep them zero
-        for (int e = tid; e < 2 * (C / 8); e += K::NTH) {
-            _Float16* dst = xbuf + (NF + e / (C / 8)) * SX + 8 * (e % (C / 8));
-            *(half8_t*)dst = half8_t{};
-            if constexpr (P == 1) *(half8_t*)(dst + K::PB) = half8_t{};
-        }
+        for (int e = tid; e < 2 * (C / 8); e += K::NTH) zero8(xbuf + (NF + e / (C / 8)) * SX, 8 * (e % (C / 8)), K::PB);
     }
     __syncthreads();
 
     // ---- stage 2: conv2 (k3) over frames t0 - 1 + v -> region A
-    stage_mma<3, C, NT, P>((const half8_t*)d.w[1], xbuf, K::PB, wm, wn, lane, d.dbg, acc, accx);
+    run_stage<3, C, NT, P>(d.w[1], xbuf, K::PB, wm, wn, lane, d.dbg, acc, accx);
     {
         const float a3 = d.slope[2], un = d.w_unscale[1];
         float bia[MR][16];
@@ -504,18 +606,10 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                                                        un, bia[mr][r]);
                         x[i] = (q >= 0.f ? keep : a3 * keep) * q;
                     }
-                    half4_t hi, lo;
-                    split4<P>(x[0], x[1], x[2], x[3], hi, lo, ovf);
-                    _Float16* dst = xa + v_ * SX + (wm * MR + mr) * 32 + 8 * j + 4 * h;
-                    *(half4_t*)dst = hi;
-                    if constexpr (P == 1) *(half4_t*)(dst + K::PA) = lo;
+                    put4(xa + v_ * SX, (wm * MR + mr) * 32 + 8 * j + 4 * h, x, K::PA);
                 }
             }
-        for (int e = tid; e < 2 * (C / 8); e += K::NTH) {
-            _Float16* dst = xa + (NF + e / (C / 8)) * SX + 8 * (e % (C / 8));
-            *(half8_t*)dst = half8_t{};
-            if constexpr (P == 1) *(half8_t*)(dst + K::PA) = half8_t{};
-        }
+        for (int e = tid; e < 2 * (C / 8); e += K::NTH) zero8(xa + (NF + e / (C / 8)) * SX, 8 * (e % (C / 8)), K::PA);
     }
     __syncthreads();
 
@@ -559,7 +653,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
         }
     };
     if constexpr (OU_BLOCK_HV_EARLY && !(EPI & kEpiIn)) load_res();
-    stage_mma<3, C, NT, P>((const half8_t*)d.w[2], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
+    run_stage<3, C, NT, P>(d.w[2], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
     if constexpr (!(OU_BLOCK_HV_EARLY && !(EPI & kEpiIn))) load_res();
     {
         const float un = d.w_unscale[2];
@@ -721,7 +815,7 @@ int launch_epi(const ou_block_desc& d, hipStream_t s)
     const int epi = (d.film ? kEpiFilm : 0) | (d.sc ? kEpiSc : 0) | (d.cond_out ? kEpiCond : 0) |
                     (d.res2 ? kEpiRes2 : 0) | (d.x ? kEpiIn : 0) | (d.head.w ? kEpiHead : 0) |
                     (d.w_down ? kEpiDown : 0);
-    if constexpr (C == 32 || C == 64) {   // encoder blocks with their rate-change conv
+    if constexpr ((C == 32 || C == 64) && P != 0) {   // encoder blocks with their rate-change conv
         switch (epi) {
         case kEpiDown: return launch_down<C, NT, P, kEpiDown>(d, s);
         case kEpiFilm | kEpiDown: return launch_down<C, NT, P, kEpiFilm | kEpiDown>(d, s);
@@ -780,14 +874,14 @@ int launch_p(const ou_block_desc& d, hipStream_t s)
 // it is 2.0x / 1.4x / 1.2x faster than the unfused launches.
 extern "C" int ou_block_supported(int channels, int prec)
 {
-    return (prec == 1 || prec == 2) &&
+    return (prec == 0 || prec == 1 || prec == 2) &&
            (channels == 32 || channels == 64 || channels == 128 || channels == 48 || channels == 96 ||
             channels == 192);
 }
 
 extern "C" int ou_block_down_supported(int channels, int rate, int kt, int prec)
 {
-    return ou_block_supported(channels, prec) && down_ok(channels, rate, kt);
+    return prec != 0 && ou_block_supported(channels, prec) && down_ok(channels, rate, kt);
 }
 
 extern "C" int ou_block_frames(int channels)
@@ -855,6 +949,32 @@ extern "C" int ou_block_pack_rect(const float* w, int m, int channels, int kt, v
     return 0;
 }
 
+extern "C" int64_t ou_block_packed_f32(int channels, int kt)
+{
+    return (int64_t)(channels + 31) / 32 * 32 * channels * kt;
+}
+
+// f32 operands (prec 0): [mt][tap][s4][lane][4] of w[row][2 (4 s4 + j) + (lane >> 5)][tap],
+// row = 32 mt + (lane & 31) (zero past `channels`); *w_unscale = 2^kStageShift
+// (the kernel stages activations as x * 2^-kStageShift, as the split form)
+extern "C" int ou_block_pack_f32(const float* w, int channels, int kt, float* out, float* w_unscale)
+{
+    if (!w || !out || !w_unscale || channels <= 0 || channels % 16 || kt <= 0)
+        return ou_fail(-1, "block_pack_f32: bad arguments");
+    const int C = channels, MT = (C + 31) / 32, S4 = C / 8;
+    for (int mt = 0; mt < MT; ++mt)
+        for (int k = 0; k < kt; ++k)
+            for (int s4 = 0; s4 < S4; ++s4)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 4; ++j) {
+                        const int row = mt * 32 + (lane & 31);
+                        const int c = 2 * (4 * s4 + j) + (lane >> 5);
+                        *out++ = row < C ? w[((int64_t)row * C + c) * kt + k] : 0.f;
+                    }
+    *w_unscale = (float)(1 << kStageShift);
+    return 0;
+}
+
 extern "C" int ou_block(const ou_block_desc* dp, void* stream)
 {
     if (!dp) return ou_fail(-1, "block: null descriptor");
@@ -864,5 +984,5 @@ extern "C" int ou_block(const ou_block_desc* dp, void* stream)
     if (!ou_block_supported(d.channels, d.prec))
         return ou_fail(-1, "block: channels %d / prec %d not supported", d.channels, d.prec);
     hipStream_t s = (hipStream_t)stream;
-    return d.prec == 1 ? launch_p<1>(d, s) : launch_p<2>(d, s);
+    return d.prec == 1 ? launch_p<1>(d, s) : d.prec == 2 ? launch_p<2>(d, s) : launch_p<0>(d, s);
 }

@@ -284,8 +284,8 @@ def prep_up(sd, p, r, antialias, device):
 @dataclass
 class FusedW:
     """The three convs of a ConvBlock packed for ou_block (one launch)."""
-    w: torch.Tensor          # packed halves of conv1 | conv2 | conv3 (int16 storage)
-    offs: tuple              # element offsets of the three packed convs in w
+    w: torch.Tensor          # packed conv1 | conv2 | conv3 (f16 halves as int16, or f32 for prec 0)
+    offs: tuple              # byte offsets of the three packed convs in w
     unscale: tuple
     prec: int
 
@@ -339,11 +339,12 @@ def prep_fused(specs, C, prec, device):
         w = sp.w
         if w.shape[0] % 32:   # 48 channels: zero rows up to the next 32 (computed, never stored)
             w = np.concatenate([w, np.zeros((-w.shape[0] % 32,) + w.shape[1:], w.dtype)])
-        packed, un = L.block_pack_np(w)
+        # f32 operands (prec 0): ou_block_pack_f32's layout; else split / f16 halves
+        packed, un = L.block_pack_f32_np(w) if prec == 0 else L.block_pack_np(w)
         parts.append(packed)
         offs.append(off)
         uns.append(un)
-        off += packed.size
+        off += packed.nbytes
     w = torch.from_numpy(np.concatenate(parts)).to(device)
     return FusedW(w, tuple(offs), tuple(uns), prec)
 
@@ -683,7 +684,7 @@ def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film
     d.channels, d.length, d.batch, d.prec = bw.C, h.T, h.B, fw.prec
     assert out.C == bw.C and out.T == h.T and out.B >= h.B, ("block output", out.t.shape, h.t.shape)
     for i, cw in enumerate((bw.conv1, bw.conv2, bw.conv3)):
-        d.w[i] = fw.w.data_ptr() + 2 * fw.offs[i]
+        d.w[i] = fw.w.data_ptr() + fw.offs[i]
         d.bias[i] = cw.bias.data_ptr() if cw.bias is not None else 0
         d.slope[i] = cw.slope
         d.w_unscale[i] = fw.unscale[i]

@@ -3,8 +3,8 @@
 // compared with a double-precision evaluation of the ou_block_desc formula
 // (include/ouhip.h, blocks.py:393-416), whole-signal and on a frame range
 // (f0, f1, h0, h1: only the range is stored and compared).  Channel counts
-// 32 / 48 / 64 / 96 / 128 / 192 (48: MFMA rows padded to 64), split-f16 and
-// f16 operands, the epilogues FiLM, input_cond + FiLM, cond_out and res2.
+// 32 / 48 / 64 / 96 / 128 / 192 (48: MFMA rows padded to 64), f32,
+// split-f16 and f16 operands, the epilogues FiLM, input_cond + FiLM, cond_out and res2.
 // Prints one line per failing case and exits 1.
 #include "../../open_universe_amd/csrc/ou_block.hip"
 
@@ -50,15 +50,22 @@ static int run(const Case& cs)
     const float slopes[3] = {0.25f, 0.1f, 0.3f};
     std::vector<float> w[3], bias[3];
     std::vector<std::vector<_Float16>> packed(3);
+    std::vector<std::vector<float>> packed32(3);
     ou_block_desc d{};
     for (int i = 0; i < 3; ++i) {
         w[i].resize((size_t)C * C * kts[i]);
         for (auto& e : w[i]) e = rnd() / std::sqrt((float)(C * kts[i]));
         bias[i].resize(C);
         for (auto& e : bias[i]) e = 0.1f * rnd();
-        packed[i].resize(ou_block_packed_halves(C, kts[i]));
-        if (ou_block_pack(w[i].data(), C, kts[i], packed[i].data(), &d.w_unscale[i]) != 0) return 10;
-        d.w[i] = packed[i].data();
+        if (cs.prec == 0) {
+            packed32[i].resize(ou_block_packed_f32(C, kts[i]));
+            if (ou_block_pack_f32(w[i].data(), C, kts[i], packed32[i].data(), &d.w_unscale[i]) != 0) return 10;
+            d.w[i] = packed32[i].data();
+        } else {
+            packed[i].resize(ou_block_packed_halves(C, kts[i]));
+            if (ou_block_pack(w[i].data(), C, kts[i], packed[i].data(), &d.w_unscale[i]) != 0) return 10;
+            d.w[i] = packed[i].data();
+        }
         d.bias[i] = bias[i].data();
         d.slope[i] = slopes[i];
     }
@@ -135,7 +142,7 @@ int main(int argc, char** argv)
 {
     std::vector<Case> cases;
     for (int C : {48, 96, 192, 32, 64, 128})
-        for (int prec : {1, 2}) {
+        for (int prec : {0, 1, 2}) {
             const int T = C >= 128 ? 45 : 70;
             cases.push_back({C, T, prec, false, false, false, false, false});
             cases.push_back({C, T, prec, true, true, false, false, false});
@@ -145,7 +152,7 @@ int main(int argc, char** argv)
     const int only = argc > 1 ? std::atoi(argv[1]) : -1;
     int bad = 0, n = 0;
     for (int i = 0; i < (int)cases.size(); ++i) {
-        if (only >= 0 && i / 8 != only) continue;   // argv: channel-count group (8 cases each)
+        if (only >= 0 && i / 12 != only) continue;   // argv: channel-count group (12 cases each)
         bad += run(cases[i]);
         ++n;
     }

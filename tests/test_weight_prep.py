@@ -212,3 +212,18 @@ def test_gru_cu16_packing_matches_restatement():
     want = w[d, g * H + wv * 16 + 2 * p + u, 32 * q + k].astype(np.float16).reshape(-1)
     assert got.dtype == np.float16 and got.shape == want.shape
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("C,kt", [(32, 5), (48, 3), (64, 3), (96, 5), (192, 3)])
+def test_numpy_block_f32_packing_matches_c(C, kt):
+    """ou_block's f32-operand layout (prec 0): the numpy restatement the
+    engine uses is byte-identical to ou_block_pack_f32 (48 channels: rows
+    padded to 64 with zeros)."""
+    from open_universe_amd import _lib as L
+
+    w = np.random.default_rng(C * 10 + kt).standard_normal((C, C, kt)).astype(np.float32)
+    c, uc = L.block_pack_f32(w)
+    wp = np.concatenate([w, np.zeros((-C % 32, C, kt), np.float32)]) if C % 32 else w
+    n, un = L.block_pack_f32_np(wp)
+    assert uc == un == 64.0
+    assert c.shape == n.shape and np.array_equal(c, n)
