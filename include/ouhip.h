@@ -170,7 +170,10 @@ typedef struct ou_gru_desc {
     int32_t flags;             /* -1 default; bit0 XCD-local chains, bit1 spin    */
                                /* without s_sleep, bit2 64-unit workgroups, bit3  */
                                /* 128-unit workgroups, bit4 timing diagnostic     */
-                               /* (skips the hand-off wait: wrong results)        */
+                               /* (skips the hand-off wait: wrong results), bit8  */
+                               /* per-step gi prefetch instead of LDS-staged gi   */
+                               /* chunks (one item per chain), bit9 timing        */
+                               /* diagnostic (gi read as 0: wrong results)        */
     uint64_t* granules;        /* workspace: ou_gru_workspace_bytes()             */
     int32_t* status;           /* device int, set nonzero on spin timeout         */
     int32_t t_begin, t_end;    /* steps [t_begin, t_end) of the T-step sequences  */

@@ -82,6 +82,29 @@ typedef unsigned ou_ldsa_t;
 #define OU_WAIT_VMCNT(n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory")
 #endif
 
+// XCD-aware workgroup order (speed only, never correctness).  Workgroups
+// are dealt round-robin over the 8 XCDs, so the neighbouring workgroups that
+// share a weight panel (the N tiles of one m-group) land on 8 different L2s
+// and every XCD fetches every panel.  ou_xcd_block maps the dispatch index to
+// a logical one -- each set of workgroups that share an XCD gets a contiguous
+// logical range, bijective for any grid size -- and returns the logical
+// (x, y, z) block, x fastest.  OU_NO_XCD_ORDER builds the identity (A/B runs).
+__device__ __forceinline__ void ou_xcd_block(int& bx, int& by, int& bz)
+{
+    const int gx = (int)gridDim.x, gy = (int)gridDim.y;
+#ifdef OU_NO_XCD_ORDER
+    bx = (int)blockIdx.x, by = (int)blockIdx.y, bz = (int)blockIdx.z;
+#else
+    const int n = gx * gy * (int)gridDim.z;
+    const int p = (int)blockIdx.x + gx * ((int)blockIdx.y + gy * (int)blockIdx.z);
+    const int x = p & 7, k = p >> 3, q = n >> 3, r = n & 7;
+    const int l = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+    bx = l % gx;
+    by = (l / gx) % gy;
+    bz = l / (gx * gy);
+#endif
+}
+
 // dynamic LDS of a kernel (tests/emu replaces it with a bounds-checked block)
 #ifndef OU_DYNAMIC_LDS
 #define OU_DYNAMIC_LDS(T, name) extern __shared__ T name[]

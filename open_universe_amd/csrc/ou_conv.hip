@@ -295,12 +295,14 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const int wm = (wave / WN) % WM;
     const int wk = wave / (WN * WM);
     const int nks = ksmode ? 1 << ((d.tile >> 12) & 3) : 1;   // K slices per output tile
-    const int b = ksmode == 1 ? (int)blockIdx.z / nks : (int)blockIdx.z;
-    const int ks = ksmode == 1 ? (int)blockIdx.z - b * nks : 0;
+    int bx, by, bz;
+    ou_xcd_block(bx, by, bz);
+    const int b = ksmode == 1 ? bz / nks : bz;
+    const int ks = ksmode == 1 ? bz - b * nks : 0;
     const int q0 = ksmode == 1 ? ks * nchunks / nks : 0;
     const int q1 = ksmode == 1 ? (ks + 1) * nchunks / nks : nchunks;
-    const int n0 = blockIdx.x * C::BN + d.f0;     // first output frame (global)
-    const int mt0 = blockIdx.y * (WM * MR);       // first m-tile of the workgroup
+    const int n0 = bx * C::BN + d.f0;     // first output frame (global)
+    const int mt0 = by * (WM * MR);       // first m-tile of the workgroup
     const int h = lane >> 5;
     const int l32 = lane & 31;
     const int R = d.frame;
@@ -605,7 +607,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     }
 
     if (ksmode == 1) {   // this slice's sums -> d.ks_ws, [tile][slice][sub-tile][acc][lane]
-        const int64_t tl = ((int64_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        const int64_t tl = ((int64_t)b * gridDim.y + by) * gridDim.x + bx;
         float* pw = d.ks_ws + ((tl * nks + ks) * (WM * WN) + wm * WN + wn) * (MR * NR * 16 * 64) + lane;
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
@@ -618,7 +620,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     } else {   // ksmode 2: add the slices' sums in slice order
         if (wk > 0) return;
         const int S = 1 << ((d.tile >> 12) & 3);
-        const int64_t tl = ((int64_t)b * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        const int64_t tl = ((int64_t)b * gridDim.y + by) * gridDim.x + bx;
         const float* pr = d.ks_ws + (tl * S * (WM * WN) + wm * WN + wn) * (MR * NR * 16 * 64) + lane;
         for (int k = 0; k < S; ++k) {
             const float* pk = pr + (int64_t)k * (WM * WN) * (MR * NR * 16 * 64);
@@ -635,8 +637,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     }
 
     // ---- epilogue ----
-    conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane,
-                          (int)(blockIdx.x + blockIdx.y + blockIdx.z));
+    conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane, bx + by + bz);
     OU_CSTAMP(5);
     OU_CSTAMP_SAVE;
 }
@@ -704,9 +705,11 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave % WM, wk = wave / WM;
     const int h = lane >> 5, l32 = lane & 31;
-    const int b = blockIdx.z;
-    const int n0 = blockIdx.x * R::BN + d.f0;   // first output frame (global)
-    const int mtu = blockIdx.y * WM + wm;       // this wave's m-tile (rows past M: computed, not stored)
+    int bx, by, bz;
+    ou_xcd_block(bx, by, bz);
+    const int b = bz;
+    const int n0 = bx * R::BN + d.f0;   // first output frame (global)
+    const int mtu = by * WM + wm;       // this wave's m-tile (rows past M: computed, not stored)
     const int mt = min(mtu, mtiles - 1);
     const int diag = (d.tile >> 8) & 3;   // diagnostics (tools/conv_bench.py --rdiag): 1 no input loads, 2 no K loop
 
@@ -856,7 +859,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[0][nr][r] += red[((((j - 1) * WM + wm) * NR + nr) * 16 + r) * 64 + lane];
     }
-    conv_epilogue<1, NR>(d, b, mtu, n0, acc, lane, (int)(blockIdx.x + blockIdx.y + blockIdx.z));
+    conv_epilogue<1, NR>(d, b, mtu, n0, acc, lane, bx + by + bz);
 }
 
 // ---------------------------------------------------------------------------

@@ -301,6 +301,7 @@ __device__ __forceinline__ void swap16(float& x, float& y)
 }
 
 constexpr int kKsWaves = 4;   // waves per workgroup
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 
 template <int H, int NB, int UW>
@@ -337,14 +338,20 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
     const int j = ubase + (lane >> USH);     // unit whose gates this lane computes
     const bool writer = (lane & ((1 << USH) - 1)) == 0;
 
-    float w[UW][3][KPL];
+    // W_hh of units (2p, 2p + 1) side by side: the dot products run as
+    // v_pk_fma_f32 (two units per instruction, each unit's chain in the same
+    // k order as a scalar fmaf chain, so the sums are bit-identical)
+    f32x2 w[UW / 2][3][KPL];
     const float* wbase = d.w_hh + (int64_t)dir * 3 * H * H + lane * KPL;
 #pragma unroll
-    for (int u = 0; u < UW; ++u)
+    for (int p = 0; p < UW / 2; ++p)
 #pragma unroll
         for (int g = 0; g < 3; ++g)
 #pragma unroll
-            for (int k = 0; k < KPL; ++k) w[u][g][k] = wbase[(int64_t)(g * H + ubase + u) * H + k];
+            for (int k = 0; k < KPL; ++k) {
+                w[p][g][k].x = wbase[(int64_t)(g * H + ubase + 2 * p) * H + k];
+                w[p][g][k].y = wbase[(int64_t)(g * H + ubase + 2 * p + 1) * H + k];
+            }
     const float bhr = d.b_hh[dir * 3 * H + 0 * H + j];
     const float bhz = d.b_hh[dir * 3 * H + 1 * H + j];
     const float bhn = d.b_hh[dir * 3 * H + 2 * H + j];
@@ -391,8 +398,14 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
     const int tb = d.t_begin, te = d.t_end > 0 ? min(d.t_end, T) : T;
     float hp[NB];                            // h_{t-1} of unit j
     float gir[NB], giz[NB], gin[NB], rsd[NB];
+    const bool no_gi = flags & 512;   // timing diagnostic only (gi, residual read as 0): wrong results
     auto prefetch = [&](int step) {
         const int tm = dir == 0 ? step : T - 1 - step;
+        if (no_gi) {
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) gir[bb] = giz[bb] = gin[bb] = rsd[bb] = 0.f;
+            return;
+        }
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb) {
             if (bb < nbh) {
@@ -404,6 +417,48 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
                                         (int64_t)(dir * H + j) * d.res_cstride + tm]
                                 : 0.f;
             }
+        }
+    };
+    // One item per chain (NB == 1, the batch-1 case): gi and the residual of
+    // the wave's UW units are staged through LDS in chunks of CS steps
+    // instead of prefetched one step ahead.  Vector loads retire in order, so
+    // the poll loop's vmcnt wait also waited for the previous step's gi
+    // prefetch (~0.07 us of a 0.8 us step: tools/gru_bench.py, flags 513);
+    // a chunk load pays that latency once per CS steps.  Per wave and chunk
+    // the 4 UW rows (3 gates x UW units of gi, UW residual rows) x CS steps
+    // are loaded coalesced along time and written as [step][unit][r z n res],
+    // so a step reads its four values with one ds_read_b128 issued before
+    // the hand-off wait.  flags bit8 keeps the per-step prefetch (A/B runs).
+    constexpr int CS = UW == 4 ? 128 : 64;   // steps per chunk (4 UW x CS x 4 B = 8 KB per wave)
+    const bool stage = NB == 1 && !(flags & 256) && !no_gi;
+    float4* gst = nullptr;
+    if constexpr (NB == 1) {
+        __shared__ float4 gst_all[kKsWaves][CS * UW];
+        gst = gst_all[wave];
+    }
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    auto stage_chunk = [&](int c0) {   // steps [c0, c0 + CS) (clamped to te - 1) -> LDS
+        constexpr int NV4 = 4 * UW * CS / 64;   // values per lane
+        const int ub = (member * kKsWaves + wv) * UW;
+        float v[NV4];
+#pragma unroll
+        for (int i = 0; i < NV4; ++i) {
+            const int e = lane + 64 * i, row = e / CS, st = min(c0 + e % CS, te - 1);
+            const int tm = dir == 0 ? st : T - 1 - st;
+            if (row < 3 * UW) {
+                const int g = row / UW, u = row % UW;
+                v[i] = d.gi[(int64_t)b0 * d.gi_bstride + (int64_t)(dir * 3 * H + g * H + ub + u) * T + tm];
+            } else {
+                const int u = row - 3 * UW;
+                v[i] = d.res ? d.res[(int64_t)b0 * d.res_bstride + (int64_t)(dir * H + ub + u) * d.res_cstride + tm]
+                             : 0.f;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NV4; ++i) {
+            const int e = lane + 64 * i, row = e / CS, sc = e % CS;
+            const int comp = row < 3 * UW ? row / UW : 3, u = row < 3 * UW ? row % UW : row - 3 * UW;
+            ((float*)gst)[(sc * UW + u) * 4 + comp] = v[i];
         }
     };
     auto hs_at = [&](int b, int u) -> float {   // h of unit u before step tb (written by the previous launch)
@@ -419,12 +474,19 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
 #pragma unroll
         for (int k = 0; k < KPL; ++k) h0[bb][k] = hs_at(b0 + min(bb, nbh - 1), lane * KPL + k);
     }
-    prefetch(tb);
+    if (stage) stage_chunk(tb);
+    else prefetch(tb);
     OU_STAMP_INIT
 
     for (int t = tb; t < te; ++t) {
         const int time = dir == 0 ? t : T - 1 - t;
         float h[NB][KPL];
+        // this step's staged gi / residual (LDS read in flight during the wait)
+        float4 gv{};
+        if (stage) {
+            if (t > tb && (t - tb) % CS == 0) stage_chunk(t);
+            gv = gst[((t - tb) % CS) * UW + (lane >> USH)];
+        }
         if (t == tb) {
 #pragma unroll
             for (int bb = 0; bb < NB; ++bb)
@@ -470,24 +532,29 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
         OU_STAMP(0);
 
         float cr[NB], cz[NB], cn[NB], cres[NB];
+        if (stage) {
+            cr[0] = gv.x, cz[0] = gv.y, cn[0] = gv.z, cres[0] = gv.w;
+        } else {
 #pragma unroll
-        for (int bb = 0; bb < NB; ++bb) {
-            cr[bb] = gir[bb]; cz[bb] = giz[bb]; cn[bb] = gin[bb]; cres[bb] = rsd[bb];
+            for (int bb = 0; bb < NB; ++bb) {
+                cr[bb] = gir[bb]; cz[bb] = giz[bb]; cn[bb] = gin[bb]; cres[bb] = rsd[bb];
+            }
+            if (t + 1 < te) prefetch(t + 1);
         }
-        if (t + 1 < te) prefetch(t + 1);
 
         // partial dot products, value index (u * NB + b) * 3 + g
         float acc[NV];
 #pragma unroll
-        for (int u = 0; u < UW; ++u)
+        for (int p = 0; p < UW / 2; ++p)
 #pragma unroll
             for (int bb = 0; bb < NB; ++bb)
 #pragma unroll
                 for (int g = 0; g < 3; ++g) {
-                    float a = 0.f;
+                    f32x2 a = {0.f, 0.f};
 #pragma unroll
-                    for (int k = 0; k < KPL; ++k) a = fmaf(w[u][g][k], h[bb][k], a);
-                    acc[(u * NB + bb) * 3 + g] = a;
+                    for (int k = 0; k < KPL; ++k) a = __builtin_elementwise_fma(w[p][g][k], (f32x2){h[bb][k], h[bb][k]}, a);
+                    acc[(2 * p * NB + bb) * 3 + g] = a.x;
+                    acc[((2 * p + 1) * NB + bb) * 3 + g] = a.y;
                 }
         OU_STAMP(1);
 

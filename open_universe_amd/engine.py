@@ -13,6 +13,7 @@ The layer walk mirrors the reference modules it replaces:
   Universe.enhance         networks/universe/universe.py:231-375
 """
 import ctypes
+import os
 import math
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -722,7 +723,7 @@ def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film
     return d
 
 
-GRU_FLAGS = -1   # kernel default (XCD-local chains); see ou_gru_desc.flags
+GRU_FLAGS = int(os.environ.get("OUHIP_GRU_FLAGS", "-1"))   # -1: kernel default; see ou_gru_desc.flags
 _GRU_WS_ZEROED = False   # set by EnhancePlan: it zeroes the GRU workspaces once per replay
 
 
