@@ -338,9 +338,10 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
     const int j = ubase + (lane >> USH);     // unit whose gates this lane computes
     const bool writer = (lane & ((1 << USH) - 1)) == 0;
 
-    // W_hh of units (2p, 2p + 1) side by side: the dot products run as
-    // v_pk_fma_f32 (two units per instruction, each unit's chain in the same
-    // k order as a scalar fmaf chain, so the sums are bit-identical)
+    // W_hh of units (2p, 2p + 1) side by side, scalar fmaf chains in k order.
+    // (v_pk_fma_f32 on these pairs measured no faster, and a recurrence split
+    // into step segments then no longer reproduced the whole launch bit for
+    // bit: tests/test_gpu_chunked.py)
     f32x2 w[UW / 2][3][KPL];
     const float* wbase = d.w_hh + (int64_t)dir * 3 * H * H + lane * KPL;
 #pragma unroll
@@ -552,7 +553,10 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
                 for (int g = 0; g < 3; ++g) {
                     f32x2 a = {0.f, 0.f};
 #pragma unroll
-                    for (int k = 0; k < KPL; ++k) a = __builtin_elementwise_fma(w[p][g][k], (f32x2){h[bb][k], h[bb][k]}, a);
+                    for (int k = 0; k < KPL; ++k) {
+                        a.x = fmaf(w[p][g][k].x, h[bb][k], a.x);
+                        a.y = fmaf(w[p][g][k].y, h[bb][k], a.y);
+                    }
                     acc[(2 * p * NB + bb) * 3 + g] = a.x;
                     acc[((2 * p + 1) * NB + bb) * 3 + g] = a.y;
                 }
