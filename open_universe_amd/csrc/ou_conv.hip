@@ -152,7 +152,25 @@ __device__ uint64_t g_conv_stamps[kStampWGs * kStampPhases];
 // reruns the enhance with f32 operands.
 constexpr int kSplitShift = 6;
 typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t ou_u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t ou_u32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+
+// Output row m -> (channel co, phase ph) of a transposed conv's pixel
+// shuffle.  rout > 0: phase-major rows (m = ph cout + co); rout < 0:
+// channel-major rows (m = co |rout| + ph), so a lane's 4 consecutive
+// accumulator rows hold consecutive output samples of one or two channels
+// (the epilogue then moves them with one 16-B / two 8-B accesses).
+__device__ __forceinline__ void ou_row_map(int m, int rout, int cout, int& co, int& ph)
+{
+    if (rout < 0) {
+        co = m / -rout;
+        ph = m - co * -rout;
+    } else {
+        ph = rout > 1 ? m / cout : 0;
+        co = m - ph * cout;
+    }
+}
 
 // Epilogue of one wave's MR x NR accumulator tiles (scaled, K complete):
 // bias, zero-fill past valid_len, residual 1, FiLM, residual 2, the rout
@@ -168,7 +186,7 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
     // loads of the tile are issued before any arithmetic, so their latency is
     // paid once, not once per row.
     const int M = d.m;
-    const int rout = d.rout;
+    const int rout = d.rout < 0 ? -d.rout : d.rout;   // output samples per frame
     const int cout = M / rout;
     const int yrows = cout;
     const int ylen = d.out_len;
@@ -184,6 +202,13 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
     const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
     const __amdgpu_buffer_rsrc_t fs = ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y,
                                               has_fm ? (int64_t)cout * 8 : 0);
+    // vector path: channel-major rows at rout 2 / 4 with every row start
+    // (4 rout)-byte aligned (uniform over the launch)
+    auto al = [&](const float* p, int64_t bst, int64_t cst) {
+        return !p || (((uintptr_t)p % (4 * rout)) == 0 && bst % rout == 0 && cst % rout == 0);
+    };
+    const bool vec = d.rout < 0 && (rout == 2 || rout == 4) && M % 4 == 0 && al(d.y, d.y_bstride, d.y_cstride) &&
+                     al(d.res1, d.r1_bstride, d.r1_cstride) && al(d.res2, d.r2_bstride, d.r2_cstride);
     float ymax = 0.f;   // max |stored y| of this wave (d.amax_out)
 #pragma unroll
     for (int mr = 0; mr < MR; ++mr) {
@@ -193,8 +218,7 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int m = min(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
-            ph[r] = rout > 1 ? m / cout : 0;
-            co[r] = m - ph[r] * cout;
+            ou_row_map(m, d.rout, cout, co[r], ph[r]);
         }
         // absent operands: one uniform branch around the whole group of loads
         // (never a per-element select between a load and a default)
@@ -221,6 +245,64 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
 #pragma unroll
         for (int nr = 0; nr < NR; ++nr) {
             const int u = ub + nr * 32 + l32;
+            if (vec) {
+                // channel-major rows at rout 4 / 2: register group g (rows
+                // 8 g + 4 h + j, j < 4) holds samples u rout .. u rout + rout - 1
+                // of 4 / rout channels -- one 16-B or two 8-B accesses per
+                // group and tensor, consecutive lanes on consecutive frames
+                const int t0 = u * rout;
+                const bool uok = u < d.f0 + d.n_frames && t0 < ylen;
+                if (__all(!uok || t0 + rout <= ylen)) {
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const bool ok = uok && mt * 32 + 8 * g + 4 * h < M;
+                        float v1[4], v2[4], val[4];
+#pragma unroll
+                        for (int sv = 0; sv < 4 / 4 + (rout == 2); ++sv) {
+                            const int c = co[4 * g + 2 * sv];
+                            const int o1 = ok ? (c * (int)d.r1_cstride + t0) * 4 : kSentinel;
+                            const int o2 = ok ? (c * (int)d.r2_cstride + t0) * 4 : kSentinel;
+                            if (rout == 4) {
+                                const auto a1 = __builtin_amdgcn_raw_buffer_load_b128(r1s, o1, 0, 0);
+                                const auto a2 = __builtin_amdgcn_raw_buffer_load_b128(r2s, o2, 0, 0);
+#pragma unroll
+                                for (int j = 0; j < 4; ++j) v1[j] = __uint_as_float(a1[j]), v2[j] = __uint_as_float(a2[j]);
+                            } else {
+                                const auto a1 = __builtin_amdgcn_raw_buffer_load_b64(r1s, o1, 0, 0);
+                                const auto a2 = __builtin_amdgcn_raw_buffer_load_b64(r2s, o2, 0, 0);
+#pragma unroll
+                                for (int j = 0; j < 2; ++j)
+                                    v1[2 * sv + j] = __uint_as_float(a1[j]), v2[2 * sv + j] = __uint_as_float(a2[j]);
+                            }
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int r = 4 * g + j;
+                            float v = acc[mr][nr][r] + bias[r];
+                            if (t0 + ph[r] >= d.valid_len) v = 0.f;
+                            v = (v + v1[j]) * s1e;
+                            v = (fa[r] + fadd) * v + fb[r];
+                            v = (v + v2[j]) * s2e;
+                            ymax = fmaxf(ymax, ok ? fabsf(v) : 0.f);
+                            val[j] = v;
+                        }
+#pragma unroll
+                        for (int sv = 0; sv < 4 / 4 + (rout == 2); ++sv) {
+                            const int c = co[4 * g + 2 * sv];
+                            const int oy = ok ? (c * (int)d.y_cstride + t0) * 4 : kSentinel;
+                            if (rout == 4)
+                                __builtin_amdgcn_raw_buffer_store_b128(
+                                    ou_u32x4{__float_as_uint(val[0]), __float_as_uint(val[1]), __float_as_uint(val[2]),
+                                             __float_as_uint(val[3])},
+                                    ys, oy, 0, 0);
+                            else
+                                __builtin_amdgcn_raw_buffer_store_b64(
+                                    ou_u32x2{__float_as_uint(val[2 * sv]), __float_as_uint(val[2 * sv + 1])}, ys, oy, 0, 0);
+                        }
+                    }
+                    continue;
+                }
+            }
             int off[16];
             float v1[16], v2[16];
 #pragma unroll
@@ -690,7 +772,8 @@ int rlds_bytes(int cec)
 
 
 template <int KT, int WM, int WK, int NR, int P>
-__global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride, int PC, int CCH)
+__global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride, int PC, int CCH,
+                                                    int S)
 {
     using R = RCfg<KT, WM, WK, NR>;
     constexpr int W = R::W, D = R::RING;
@@ -707,7 +790,10 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     const int h = lane >> 5, l32 = lane & 31;
     int bx, by, bz;
     ou_xcd_block(bx, by, bz);
-    const int b = bz;
+    // K slices (S > 1, tile bits 12-13): grid z = batch x S, slice ks walks
+    // chunks [ks nchunks / S, (ks + 1) nchunks / S) and stores its partial
+    // sums to d.ks_ws; conv_rreduce adds them in slice order (deterministic)
+    const int b = bz / S, ks = bz - (bz / S) * S;
     const int n0 = bx * R::BN + d.f0;   // first output frame (global)
     const int mtu = by * WM + wm;       // this wave's m-tile (rows past M: computed, not stored)
     const int mt = min(mtu, mtiles - 1);
@@ -737,7 +823,8 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     const int NI = (CCH / 8) * WS;
     bool ovf = false;
     const _Float16* xp = xs + l32 * SX + h * HALF;
-    for (int q = 0; q < nchunks; ++q) {
+    const int qa = ks * nchunks / S, qb = (ks + 1) * nchunks / S;
+    for (int q = qa; q < qb; ++q) {
         const int p0 = (q / nchc) * PC, c0 = (q - (q / nchc) * nchc) * CCH;
         const half8_t* ap = ap0 + (int64_t)((p0 * cin + c0) / 16) * 2 * KT * 64;
         // a wave with no steps (NS < WK) still issues its prologue loads: clamp
@@ -751,7 +838,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
         };
 #pragma unroll
         for (int j = 0; j < D - 1; ++j) load_a(s0 + j, ra[j]);
-        if (q > 0) __syncthreads();   // every wave is done reading the previous chunk
+        if (q > qa) __syncthreads();   // every wave is done reading the previous chunk
         // ---- stage the chunk: item = (8 channels c0 + 8 g .., sample j of the
         // chunk's window): consecutive lanes load consecutive samples of PC
         // phases (the whole frame when PC = R); sample j is frame j / PC, phase
@@ -858,6 +945,45 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
             for (int nr = 0; nr < NR; ++nr)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[0][nr][r] += red[((((j - 1) * WM + wm) * NR + nr) * 16 + r) * 64 + lane];
+    }
+    if (S > 1) {   // this slice's sums -> d.ks_ws [tile][slice][wm][nr][16][lane]
+        const int64_t tl = ((int64_t)b * gridDim.y + by) * gridDim.x + bx;
+        float* pw = d.ks_ws + (((tl * S + ks) * WM + wm) * NR) * 16 * 64 + lane;
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) pw[(nr * 16 + r) * 64] = acc[0][nr][r];
+        return;
+    }
+    conv_epilogue<1, NR>(d, b, mtu, n0, acc, lane, bx + by + bz);
+}
+
+// Second launch of a K-sliced register-streamed conv: one wave per m-tile of
+// a (frame tile, m-group) adds the S partial sums in slice order and runs the
+// epilogue.  grid (frame tiles, m-groups, batch) as conv_rkernel's without
+// the slices; 64 WM threads.
+template <int NR>
+__global__ __launch_bounds__(256) void conv_rreduce(ou_conv_desc d, int S, int WM)
+{
+    int bx, by, bz;
+    ou_xcd_block(bx, by, bz);
+    const int lane = threadIdx.x & 63, wm = threadIdx.x >> 6;
+    const int b = bz, n0 = bx * 32 * NR + d.f0, mtu = by * WM + wm;
+    const int64_t tl = ((int64_t)b * gridDim.y + by) * gridDim.x + bx;
+    floatx16 acc[1][NR];
+#pragma unroll
+    for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[0][nr][r] = 0.f;
+    for (int k = 0; k < S; ++k) {
+        const float* pr = d.ks_ws + (((tl * S + k) * WM + wm) * NR) * 16 * 64 + lane;
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float v = pr[(nr * 16 + r) * 64];
+                acc[0][nr][r] = k == 0 ? v : acc[0][nr][r] + v;
+            }
     }
     conv_epilogue<1, NR>(d, b, mtu, n0, acc, lane, bx + by + bz);
 }
@@ -1007,15 +1133,14 @@ __global__ __launch_bounds__(256) void conv_pkernel(ou_conv_desc d, int nchunks,
     };
 
     const int M = d.m;
-    const int rout = d.rout;
+    const int rout = d.rout < 0 ? -d.rout : d.rout;
     const int cout = M / rout;
     const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr;
     float ev1[MR][NR][16];
     float ebias[MR][16];
     auto row_of = [&](int mt, int r, int& co, int& ph) {
         const int m = min(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
-        ph = rout > 1 ? m / cout : 0;
-        co = m - ph * cout;
+        ou_row_map(m, d.rout, cout, co, ph);
     };
     // residual 1 and bias of a tile's epilogue, issued one chunk ahead
     const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
@@ -1876,6 +2001,10 @@ int launch_r(const ou_conv_desc& d, hipStream_t s)
     int pc = 0, cch = 0;
     if (!rchunks<KT, WM, WK, NR, P>(d.cin, d.frame, &pc, &cch))
         return ou_fail(-2, "conv: no register-streamed K chunking for cin %d x frame %d", d.cin, d.frame);
+    const int S = 1 << ((d.tile >> 12) & 3);   // K slices
+    const int nchunks = (d.frame / pc) * (d.cin / cch);
+    if (S > nchunks)
+        return ou_fail(-2, "conv: %d K slices for %d register-streamed K chunks", S, nchunks);
     const int lds = rlds_bytes<KT, WM, WK, NR, P>(pc * cch);
     auto kern = conv_rkernel<KT, WM, WK, NR, P>;
     static bool attr = false;   // opt in to the full 160 KiB once
@@ -1889,7 +2018,16 @@ int launch_r(const ou_conv_desc& d, hipStream_t s)
     const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
     const int64_t a_mt_stride = (int64_t)cin_pad * KT * 32;
     dim3 grid((d.n_frames + R::BN - 1) / R::BN, (mtiles + WM - 1) / WM, d.batch);
-    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, d, mtiles, a_mt_stride, pc, cch);
+    if (S > 1) {
+        const int64_t need = (int64_t)grid.x * grid.y * grid.z * S * WM * NR * 16 * 64 * 4;
+        if (!d.ks_ws || d.ks_ws_bytes < need)
+            return ou_fail(-2, "conv: K-slice workspace %lld B < %lld B", (long long)d.ks_ws_bytes, (long long)need);
+    }
+    hipLaunchKernelGGL(kern, dim3(grid.x, grid.y, grid.z * S), dim3(256), lds, s, d, mtiles, a_mt_stride, pc, cch, S);
+    if (S > 1) {
+        OU_HIP_CHECK(hipGetLastError(), "conv: register-streamed slices");
+        hipLaunchKernelGGL((conv_rreduce<NR>), grid, dim3(64 * WM), 0, s, d, S, WM);
+    }
     return ou_check_launch("conv");
 }
 
@@ -2109,16 +2247,16 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     if (!dp) return ou_fail(-1, "conv: null descriptor");
     const ou_conv_desc& d = *dp;
     if (!d.x || !d.w || !d.y || d.m <= 0 || d.batch <= 0 || d.n_frames <= 0 || d.cin <= 0 ||
-        d.frame <= 0 || d.rout <= 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0 || d.f0 < 0)
+        d.frame <= 0 || d.rout == 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0 || d.f0 < 0)
         return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d frame=%d f0=%d)", d.m, d.rout, d.frame, d.f0);
     if (d.tile >= 0 && (d.tile & kRsBit)) {   // register-streamed kernel (bits 0-7: RTILES shape)
-        if ((d.tile & ~(kRsBit | 0x3ff)) || (d.tile & 0xff) >= kNumRTiles)
+        if ((d.tile & ~(kRsBit | 0x3ff | (3 << 12))) || (d.tile & 0xff) >= kNumRTiles)
             return ou_fail(-2, "conv: bad register-streamed tile 0x%x", d.tile);
         if ((d.prec != 1 && d.prec != 2) || d.cin % 16 || d.amax_in)
             return ou_fail(-2, "conv: the register-streamed kernel needs prec 1/2, cin %% 16 == 0, no amax_in");
         if (!(d.w_unscale > 0.f)) return ou_fail(-1, "conv: split-f16 needs the w_unscale of ou_conv_pack_split");
         hipStream_t rs = (hipStream_t)stream;
-        const int t = d.tile & (0xff | kRsBit);   // bits 8-9 (diagnostics) travel in d.tile
+        const int t = d.tile & (0xff | kRsBit);   // bits 8-9 (diagnostics) and 12-13 (K slices) travel in d.tile
         switch (d.kt) {
         case 1: return OU_LAUNCH_KT(1, d, t, 1, false, rs);
         case 3: return OU_LAUNCH_KT(3, d, t, 1, false, rs);
@@ -2181,8 +2319,8 @@ extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile_f
 extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int ou_conv_tile_ok(int kt, int tile)
 {
-    if (tile & kRsBit)   // register-streamed: shape id only; LDS (cin-dependent) checked at launch
-        return !(tile & ~(kRsBit | 0xff)) && (tile & 0xff) < kNumRTiles && (kt == 1 || kt == 3 || kt == 5);
+    if (tile & kRsBit)   // register-streamed: shape id (+ K slices); LDS and chunks checked at launch
+        return !(tile & ~(kRsBit | 0xff | (3 << 12))) && (tile & 0xff) < kNumRTiles && (kt == 1 || kt == 3 || kt == 5);
     if (tile & kSplitBit) {   // split-f16 (d.prec = 1): one-tile workgroups, no other bits
         if (tile & ~(kSplitBit | 0xff)) return 0;
         if ((tile & 0xff) >= kNumTiles) return 0;

@@ -151,6 +151,7 @@ class ConvW:
     w_unscale: float = 1.0   # split-f16 weight scale (ou_conv_pack_split)
     status: int = 0          # device int32* for the split-f16 range flag (0 = none)
     ks_ws: tuple = (0, 0)    # K-slice workspace (ptr, bytes) shared by the engine's convs
+    cm: bool = False         # rout > 1: channel-major rows (m = co * rout + ph; ConvDesc.rout < 0)
 
     @property
     def cout(self):
@@ -170,6 +171,7 @@ class ConvSpec:
     bias: Optional[np.ndarray]
     shift: int = 0
     ref_macs: float = 0.0   # MACs of the replaced reference ops per output frame
+    cm: bool = False        # rout > 1: rows ordered m = co * rout + ph (else ph * cout + co)
 
 
 def make_conv(spec, device, prec=None):
@@ -193,7 +195,7 @@ def make_conv(spec, device, prec=None):
     b = None if spec.bias is None else torch.from_numpy(np.ascontiguousarray(spec.bias, np.float32)).to(device)
     return ConvW(m, spec.cin, kt, spec.frame, spec.pad, spec.rout, float(spec.slope), cc, packed, b,
                  spec.shift, spec.ref_macs, int(prec), float(unscale), _PREP_STATUS if prec else 0,
-                 _PREP_KSWS)
+                 _PREP_KSWS, cm=bool(spec.cm))
 
 
 def _slope(sd, p):
@@ -242,7 +244,10 @@ def spec_up(sd, p, r, antialias):
     """Transposed PReLU_Conv(2C, C, r, stride=r) (+ FIR after, blocks.py:221-225)
     as a polyphase convolution over input frames producing r*C rows that the
     kernel's epilogue pixel-shuffles.  weight_norm dim 0 of a ConvTranspose1d
-    weight (Cin, Cout, r) is per input channel; fold_weight handles it."""
+    weight (Cin, Cout, r) is per input channel; fold_weight handles it.  Rows
+    are channel-major (m = co * r + ph): a lane's consecutive accumulator rows
+    are consecutive output samples, stored as one 16-B / two 8-B accesses at
+    r = 4 / 2 (ConvDesc.rout = -r).  OUHIP_UP_CM=0 keeps phase-major rows."""
     w = fold_weight(sd, p + ".conv").astype(np.float64)  # (Cin, Cout, r)
     cin, cout, _ = w.shape
     if antialias:
@@ -254,11 +259,18 @@ def spec_up(sd, p, r, antialias):
                 d = s_ // r
                 e = s_ - d * r
                 wl[ph, :, :, d + 1] += fir[j] * w[:, :, e].T
-        return ConvSpec(wl.reshape(r * cout, cin, 3), cin, 1, 1, r, _slope(sd, p), _bias(sd, p + ".bias"),
-                        ref_macs=float(cin * cout * r + cout * (2 * r + 1) * r))
-    wl = w.transpose(2, 1, 0).reshape(r * cout, cin, 1)
-    return ConvSpec(wl, cin, 1, 0, r, _slope(sd, p), _bias(sd, p + ".conv.bias"),
-                    ref_macs=float(cin * cout * r))
+        if UP_CM:
+            wl = wl.transpose(1, 0, 2, 3)
+        return ConvSpec(np.ascontiguousarray(wl).reshape(r * cout, cin, 3), cin, 1, 1, r, _slope(sd, p),
+                        _bias(sd, p + ".bias"), ref_macs=float(cin * cout * r + cout * (2 * r + 1) * r), cm=UP_CM)
+    wl = w.transpose(2, 1, 0)   # (r, cout, cin)
+    if UP_CM:
+        wl = wl.transpose(1, 0, 2)
+    return ConvSpec(np.ascontiguousarray(wl).reshape(r * cout, cin, 1), cin, 1, 0, r, _slope(sd, p),
+                    _bias(sd, p + ".conv.bias"), ref_macs=float(cin * cout * r), cm=UP_CM)
+
+
+UP_CM = os.environ.get("OUHIP_UP_CM", "1") != "0"
 
 
 def prep_same(sd, p, k, device):
@@ -538,7 +550,7 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
     d.f0 = 0
     d.batch = x.B if batch is None else batch
     d.y, d.y_bstride, d.y_cstride = y.ptr, y.bs, y.cs
-    d.rout = cw.rout
+    d.rout = -cw.rout if (cw.cm and cw.rout > 1) else cw.rout
     d.out_len = y.T if out_len is None else out_len
     d.valid_len = (1 << 30) if valid_len is None else valid_len
     d.bias = cw.bias.data_ptr() if cw.bias is not None else 0
@@ -877,7 +889,7 @@ class ConvTuner:
             # register-streamed kernel (tile bit 14): whole input windows
             # staged once; ou_conv refuses the shapes whose window exceeds LDS
             if d.cin % 16 == 0 and not d.amax_in:
-                cands += [t | RS_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | RS_BIT)]
+                cands += [t | RS_BIT | k for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | RS_BIT) for k in ksl]
         elif d.amax_out:
             cands = [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t) for k in ksl]
         else:

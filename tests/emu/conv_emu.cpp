@@ -13,6 +13,7 @@
 struct Geom {
     int cout, cin, frame, kt, T, B, rout;
     bool res1, res2, film, scale;
+    bool cm = false;   // channel-major output rows (ou_conv_desc.rout < 0)
 };
 
 static float* alloc(size_t n)
@@ -25,7 +26,7 @@ static float* alloc(size_t n)
 // chunk: launch output frames [U / 3, 2 U / 3 + 1) only, reading x up to the
 // last sample they need (as engine.conv_desc(rng=...) records it), and check
 // that nothing outside those frames' outputs was written
-static int run(const Geom& g, int tile, bool chunk = false)
+static int run(const Geom& g, int tile, bool chunk = false, int kslices = 1)
 {
     const int cin_eff = g.cin * g.frame;
     const int m = g.cout * g.rout;
@@ -53,7 +54,7 @@ static int run(const Geom& g, int tile, bool chunk = false)
     d.w = w; d.m = m; d.kt = g.kt; d.pad = (g.kt - 1) / 2; d.cc = 0;
     d.n_frames = U; d.batch = g.B;
     d.y = y; d.y_bstride = (int64_t)g.cout * out_len; d.y_cstride = out_len;
-    d.rout = g.rout; d.out_len = out_len; d.valid_len = out_len - 3;
+    d.rout = g.cm ? -g.rout : g.rout; d.out_len = out_len; d.valid_len = out_len - 3;
     d.bias = bias;
     d.res1 = r1; d.r1_bstride = d.y_bstride; d.r1_cstride = d.y_cstride; d.s1 = 0.7f;
     d.film = fm; d.film_bstride = 2 * g.cout;
@@ -61,6 +62,14 @@ static int run(const Geom& g, int tile, bool chunk = false)
     d.tile = tile & ~(2048 | 4096);
     d.prec = split ? ((tile & 4096) ? 2 : 1) : 0;
     d.w_unscale = unscale;
+    float* ksws = nullptr;   // K-slice partial sums (register-streamed slices: tile bits 12-13)
+    if (kslices > 1) {
+        d.tile |= (kslices == 2 ? 1 : kslices == 4 ? 2 : 3) << 12;
+        const int64_t n = (int64_t)((U + 31) / 32 + 2) * ((m + 31) / 32 + 4) * g.B * kslices * 4 * 1024;
+        ksws = alloc((size_t)n);
+        d.ks_ws = ksws;
+        d.ks_ws_bytes = n * 4;
+    }
     int a = 0, bnd = U;
     if (chunk) {
         a = U / 3;
@@ -83,7 +92,7 @@ static int run(const Geom& g, int tile, bool chunk = false)
                     }
                 }
     }
-    for (float* p : {w, x, y, bias, r1, r2, fm, sc}) std::free(p);
+    for (float* p : {w, x, y, bias, r1, r2, fm, sc, ksws}) std::free(p);
     return rc;
 }
 
@@ -100,6 +109,8 @@ int main(int argc, char** argv)
         {642, 1, 160, 4, 1600, 1, 1, false, false, false, false},   // STFT as a framed GEMM
         {128, 256, 1, 3, 41, 2, 4, true, false, false, false},      // transposed conv, 4 phases
         {160, 96, 1, 3, 67, 1, 5, false, false, false, false},      // M = 800, partial m-groups
+        {128, 256, 1, 3, 41, 2, 4, true, false, false, false, true},  // channel-major rows: 16-B epilogue
+        {32, 64, 1, 3, 301, 1, 2, true, true, true, false, true},     // channel-major, 2 phases: 8-B epilogue
         // register-streamed kernel (tile bit 14) shapes, run with its tiles
         // only (kFirstRsGeom on): ragged 16-channel up
         // conv (3 steps < 4 K waves: the b31c724 fault), 1 step, deep k3 / k5,
@@ -117,8 +128,8 @@ int main(int argc, char** argv)
     };
     const int only = argc > 1 ? std::atoi(argv[1]) : -1;
     int n = 0;
-    constexpr int kFirstRsGeom = 10;   // geometries from here on: register-streamed tiles only
-    int nrs = 0, nchunk = 0;
+    constexpr int kFirstRsGeom = 12;   // geometries from here on: register-streamed tiles only
+    int nrs = 0, nchunk = 0, nks = 0;
     const bool rs_only = std::getenv("OUHIP_EMU_RS_ONLY") != nullptr;   // register-streamed tiles only
     for (int gi = 0; gi < (int)(sizeof(geoms) / sizeof(geoms[0])); ++gi) {
         if (only >= 0 && gi != only) continue;
@@ -153,9 +164,26 @@ int main(int argc, char** argv)
                     ++n;
                     ++nchunk;
                 }
+                // register-streamed K slices (K-chunked windows: the st_convs);
+                // refused where the chunks are fewer than the slices
+                if (tpw == 6)
+                    for (int ksl : {2, 4, 8})
+                        for (bool ch : {false, true}) {
+                            const int rc3 = run(g, t | v, ch, ksl);
+                            if (rc3 == -2) continue;
+                            if (rc3 != 0) {
+                                std::fprintf(stderr, "geom %d tile %d: %d K slices%s: ou_conv returned %d\n", gi, t, ksl,
+                                             ch ? " (frame range)" : "", rc3);
+                                return 2;
+                            }
+                            ++n;
+                            ++nrs;
+                            ++nks;
+                        }
             }
         }
     }
-    std::printf("ok: %d launches bounds-checked (%d register-streamed, %d on frame ranges)\n", n, nrs, nchunk);
+    std::printf("ok: %d launches bounds-checked (%d register-streamed, %d of them K-sliced, %d on frame ranges)\n", n,
+                nrs, nks, nchunk);
     return 0;
 }

@@ -9,6 +9,7 @@
 struct Geom {
     int cout, cin, frame, kt, T, B, rout;
     bool res1, res2, film, scale;
+    bool cm = false;   // channel-major output rows (ou_conv_desc.rout < 0)
 };
 
 static uint32_t g_seed = 12345;
@@ -29,6 +30,9 @@ int main(int argc, char** argv)
         {64, 32, 2, 3, 100, 2, 1, false, false, false, false},
         {48, 24, 5, 3, 103, 1, 1, false, false, false, false},
         {64, 48, 1, 3, 29, 2, 4, true, false, false, false},   // transposed conv, 4 phases
+        {64, 48, 1, 3, 29, 2, 4, true, false, false, false, true},   // channel-major rows: 16-B epilogue
+        {32, 64, 1, 3, 45, 1, 2, true, true, true, false, true},     // channel-major, 2 phases: 8-B epilogue
+        {24, 32, 1, 1, 37, 2, 5, true, false, false, false, true},   // channel-major, 5 phases: scalar epilogue
     };
     const int only = argc > 1 ? std::atoi(argv[1]) : -1;
     int bad = 0, n = 0;
@@ -51,7 +55,7 @@ int main(int argc, char** argv)
         std::vector<double> ref((size_t)g.B * g.cout * out_len, 0.0);
         for (int b = 0; b < g.B; ++b)
             for (int mm = 0; mm < m; ++mm) {
-                const int ph = mm / g.cout, co = mm % g.cout;
+                const int ph = g.cm ? mm % g.rout : mm / g.cout, co = g.cm ? mm / g.rout : mm % g.cout;
                 for (int u = 0; u < U; ++u) {
                     double acc = 0.0;
                     for (int c = 0; c < cin_eff; ++c)
@@ -91,7 +95,7 @@ int main(int argc, char** argv)
                 d.cin = g.cin; d.in_len = g.T; d.frame = g.frame; d.in_scale = g.scale ? sc.data() : nullptr;
                 d.slope = 0.25f; d.w = packed.data(); d.m = m; d.kt = g.kt; d.pad = pad;
                 d.n_frames = U; d.batch = g.B; d.y = y.data(); d.y_bstride = (int64_t)g.cout * out_len;
-                d.y_cstride = out_len; d.rout = g.rout; d.out_len = out_len; d.valid_len = valid;
+                d.y_cstride = out_len; d.rout = g.cm ? -g.rout : g.rout; d.out_len = out_len; d.valid_len = valid;
                 d.bias = bias.data();
                 d.res1 = g.res1 ? r1.data() : nullptr; d.r1_bstride = d.y_bstride; d.r1_cstride = out_len; d.s1 = 0.7f;
                 d.film = g.film ? fm.data() : nullptr; d.film_bstride = 2 * g.cout;

@@ -86,6 +86,7 @@ inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::m
 // wave vote / atomics: lanes run one after another here, so a vote sees only
 // the calling lane (used by the split-f16 range flag, never taken in tests)
 inline bool __any(bool p) { return p; }
+inline bool __all(bool p) { return p; }
 inline int atomicOr(int* p, int v) { const int o = *p; *p |= v; return o; }
 inline unsigned atomicMax(unsigned* p, unsigned v) { const unsigned o = *p; *p = o > v ? o : v; return o; }
 inline float __shfl_xor(float v, int) { return v; }
@@ -136,6 +137,21 @@ inline void emu_store_b128(emu_u4 v, emu_rsrc r, int voff, int soff, int)
     if (!emu_in_range(r, (uint32_t)voff, (uint32_t)soff, 16, "store_b128")) return;
     std::memcpy((char*)r.base + (uint32_t)voff + (uint32_t)soff, &v, 16);
 }
+typedef uint32_t emu_u2 __attribute__((ext_vector_type(2)));
+inline emu_u2 emu_load_b64(emu_rsrc r, int voff, int soff, int)
+{
+    emu_u2 v = {0, 0};
+    if (!emu_in_range(r, (uint32_t)voff, (uint32_t)soff, 8, "load_b64")) return v;
+    std::memcpy(&v, r.base + (uint32_t)voff + (uint32_t)soff, 8);
+    return v;
+}
+inline void emu_store_b64(emu_u2 v, emu_rsrc r, int voff, int soff, int)
+{
+    if (!emu_in_range(r, (uint32_t)voff, (uint32_t)soff, 8, "store_b64")) return;
+    std::memcpy((char*)r.base + (uint32_t)voff + (uint32_t)soff, &v, 8);
+}
+#define __builtin_amdgcn_raw_buffer_load_b64 emu_load_b64
+#define __builtin_amdgcn_raw_buffer_store_b64 emu_store_b64
 #define __builtin_amdgcn_raw_buffer_store_b128 emu_store_b128
 #define __builtin_amdgcn_readfirstlane(x) (x)
 #define __builtin_amdgcn_s_waitcnt(x) ((void)0)

@@ -82,7 +82,7 @@ def test_emulator_catches_the_reverted_rkernel_clamp(tmp_path):
                   "const int sc = min(s, s1 - 1);")
     exe = str(tmp_path / "conv_emu_rev")
     _build("conv_emu.cpp", exe, *ASAN, f'-DOU_EMU_CONV_SRC="{src}"')
-    _must_fail([exe, "10"], env={"OUHIP_EMU_RS_ONLY": "1"})
+    _must_fail([exe, "12"], env={"OUHIP_EMU_RS_ONLY": "1"})
 
 
 def test_emulator_catches_an_unclamped_block_read(tmp_path):

@@ -266,7 +266,8 @@ def test_conv_register_streamed_every_shape(geom):
     xa, r1a, r2a = E.Act(x.to(DEV)), E.Act(r1.to(DEV)), E.Act(r2.to(DEV))
     lib = L.load()
     stream = torch.cuda.current_stream().cuda_stream
-    bad, n = [], 0
+    ws = torch.empty(E.KSWS_BYTES // 4, dtype=torch.float32, device=DEV)   # K-slice partial sums
+    bad, n, nks = [], 0, 0
     for prec in (1, 2):
         cw = E.make_conv(spec, DEV, prec=prec)
 
@@ -275,6 +276,7 @@ def test_conv_register_streamed_every_shape(geom):
             d = E.conv_desc(cw, xa, y, res1=r1a, s1=0.7, film=film.data_ptr(), film_bs=2 * cout, res2=r2a,
                             s2=0.5, n_frames=U, out_len=L_out, valid_len=L_out - 2)
             d.tile = tile
+            d.ks_ws, d.ks_ws_bytes = ws.data_ptr(), E.KSWS_BYTES
             rc = lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
             torch.cuda.synchronize()
             return rc, y.t.cpu()
@@ -298,4 +300,16 @@ def test_conv_register_streamed_every_shape(geom):
             err = ((y - ref).norm() / ref.norm()).item()
             if not err < 2e-6:
                 bad.append((prec, t, err))
+            # K slices (K-chunked windows only; refused where chunks < slices)
+            for k in (1, 2, 3):
+                rc, y = run(t | RS_BIT | (k << 12))
+                if rc == -2:
+                    continue
+                assert rc == 0, lib.ou_last_error()
+                nks += 1
+                err = ((y - ref).norm() / ref.norm()).item()
+                if not err < 2e-6:
+                    bad.append((prec, t, 1 << k, err))
     assert n >= 6 and not bad, bad
+    if cin * frame >= 2048 and frame > 1:   # the st_conv shapes: K-chunked, so sliceable
+        assert nks > 0

@@ -37,7 +37,10 @@ def emulate(spec, x, n_frames, out_len, valid_len=None, in_scale=None):
     acc = F.conv1d(xv, torch.from_numpy(np.asarray(spec.w, np.float64)))
     m = acc.shape[1]
     cout = m // spec.rout
-    y = acc.reshape(B, spec.rout, cout, n_frames).permute(0, 2, 3, 1).reshape(B, cout, -1)
+    if spec.cm:   # channel-major rows m = co * rout + ph
+        y = acc.reshape(B, cout, spec.rout, n_frames).permute(0, 1, 3, 2).reshape(B, cout, -1)
+    else:         # phase-major rows m = ph * cout + co
+        y = acc.reshape(B, spec.rout, cout, n_frames).permute(0, 2, 3, 1).reshape(B, cout, -1)
     if spec.bias is not None:
         y = y + torch.from_numpy(np.asarray(spec.bias, np.float64))[None, :, None]
     if valid_len is not None and valid_len < y.shape[-1]:
