@@ -72,7 +72,9 @@ typedef struct ou_conv_desc {
     int32_t batch;
     float* y;
     int64_t y_bstride, y_cstride;
-    int32_t rout;              /* output phases (transposed conv), 1 otherwise   */
+    int32_t rout;              /* output phases (transposed conv), 1 otherwise;  */
+                               /* < 0: |rout| phases with channel-major rows     */
+                               /* m = co * |rout| + ph (else m = ph * cout + co) */
     int32_t out_len;           /* store t < out_len                              */
     int32_t valid_len;         /* t >= valid_len stored as 0 before res1         */
     const float* bias;         /* [cout] or NULL                                 */

@@ -81,6 +81,12 @@ constexpr int kStageShift = 6;   // activations are staged as x * 2^-6 (ou_conv'
 #ifndef OU_BLOCK_FENCE
 #define OU_BLOCK_FENCE 1   // pin each ring load ahead of the step's LDS reads (128 ch: 36.6 -> 32.7 us)
 #endif
+#ifndef OU_BLOCK_BPIPE
+#define OU_BLOCK_BPIPE 1   // LDS B fragments read one k-step ahead of their MFMAs
+#endif
+#ifndef OU_BLOCK_RING_EARLY
+#define OU_BLOCK_RING_EARLY 0   // 1: issue a stage's first weight fragments before the previous stage's epilogue (measured slower in the C2 bench: profiles/bench_ab_ring_mel_r03n.txt)
+#endif
 #ifndef OU_BLOCK_HV_EARLY
 #define OU_BLOCK_HV_EARLY 0   // load the block residual before the conv3 MFMA stage
 #endif
@@ -125,10 +131,40 @@ __device__ __forceinline__ float prelu(float v, float a) { return v >= 0.f ? v :
 // One conv stage: acc[mr][nr] (+ accx for the split cross terms) over KT taps
 // x C channels.  xin: LDS base of the stage's input (hi plane; lo plane at
 // + pstride); wp: packed weights [mt][tap][ks][plane][lane][8].
+// Weight-fragment ring of a split-f16 / f16 stage: step s's A fragments (hi |
+// lo) of the wave's m-tiles.  ring_pro issues the first D - 1 steps of a
+// stage; the kernel calls it for the NEXT stage before the current stage's
+// epilogue and barrier (and for conv1 before the input staging), so the L2
+// round trip of a stage's first fragments overlaps work instead of stalling
+// the stage's first MFMAs (OU_BLOCK_RING_EARLY=0: at the stage start).
+template <int KT, int C, int NT, int P>
+__device__ __forceinline__ void ring_load(const half8_t* __restrict__ wp, int wm, int lane, int s,
+                                          half8_t (&dst)[BCfg<C, NT, P>::MR][2])
+{
+    using K = BCfg<C, NT, P>;
+    const int k = s / K::KS, ks = s - (s / K::KS) * K::KS;
+#pragma unroll
+    for (int mr = 0; mr < K::MR; ++mr) {
+        const half8_t* p = wp + ((((int64_t)(wm * K::MR + mr) * KT + k) * K::KS + ks) * 2) * 64 + lane;
+        dst[mr][0] = p[0];
+        if constexpr (P == 1) dst[mr][1] = p[64];
+    }
+}
+template <int KT, int C, int NT, int P>
+__device__ __forceinline__ void ring_pro(const void* wp, int wm, int lane,
+                                         half8_t (&ra)[BCfg<C, NT, P>::RING][BCfg<C, NT, P>::MR][2])
+{
+    using K = BCfg<C, NT, P>;
+    constexpr int NS = KT * K::KS, D = NS < K::RING ? NS : K::RING;
+#pragma unroll
+    for (int s = 0; s < D - 1; ++s) ring_load<KT, C, NT, P>((const half8_t*)wp, wm, lane, s, ra[s]);
+}
+
 template <int KT, int C, int NT, int P>
 __device__ __forceinline__ void stage_mma(const half8_t* __restrict__ wp, const _Float16* xin, int pstride, int wm,
                                           int wn, int lane, int dbg, floatx16 (&acc)[BCfg<C, NT, P>::MR][BCfg<C, NT, P>::NR],
-                                          floatx16 (&accx)[BCfg<C, NT, P>::MR][BCfg<C, NT, P>::NR])
+                                          floatx16 (&accx)[BCfg<C, NT, P>::MR][BCfg<C, NT, P>::NR],
+                                          half8_t (&ra)[BCfg<C, NT, P>::RING][BCfg<C, NT, P>::MR][2], bool pre)
 {
     using K = BCfg<C, NT, P>;
     constexpr int MR = K::MR, NR = K::NR, KS = K::KS, NS = KT * KS;
@@ -144,43 +180,48 @@ __device__ __forceinline__ void stage_mma(const half8_t* __restrict__ wp, const 
     // loads of step s + D - 1 are issued before the MFMAs of step s
     if (dbg & 2) return;   // diagnostics (tools/block_bench.py --dbg): no MFMA stage
     constexpr int D = NS < K::RING ? NS : K::RING;
-    half8_t ra[D][MR][2];
-    auto load_a = [&](int s, half8_t (&dst)[MR][2]) {
-        const int k = s / KS, ks = s - (s / KS) * KS;
+    auto load_a = [&](int s, half8_t (&dst)[MR][2]) { ring_load<KT, C, NT, P>(wp, wm, lane, s, dst); };
+    if (!pre) {
 #pragma unroll
-        for (int mr = 0; mr < MR; ++mr) {
-            const half8_t* p = wp + ((((int64_t)(wm * MR + mr) * KT + k) * KS + ks) * 2) * 64 + lane;
-            dst[mr][0] = p[0];
-            if constexpr (P == 1) dst[mr][1] = p[64];
-        }
-    };
-#pragma unroll
-    for (int s = 0; s < D - 1; ++s) load_a(s, ra[s]);
+        for (int s = 0; s < D - 1; ++s) load_a(s, ra[s]);
+    }
     const _Float16* xb = xin + (wn * NR * 32 + l32) * K::SX + 8 * h;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-        if (s + D - 1 < NS) load_a(s + D - 1, ra[(s + D - 1) % D]);
-        // the fully unrolled loop otherwise lets the scheduler sink the ring
-        // loads next to their use (2-3 steps of latency cover instead of D - 1)
-        if constexpr (OU_BLOCK_FENCE) asm volatile("" ::: "memory");
+    // B fragments (LDS) one step ahead: step s + 1's reads are issued before
+    // step s's MFMAs, so an MFMA never waits on the read that feeds it
+    // (OU_BLOCK_BPIPE=0: read right before use)
+    half8_t b[2][NR], bl[2][NR];
+    auto load_b = [&](int s, half8_t (&bq)[NR], half8_t (&bo)[NR]) {
         const int k = s / KS, ks = s - (s / KS) * KS;
-        half8_t b[NR], bl[NR];
 #pragma unroll
         for (int nr = 0; nr < NR; ++nr) {
             const _Float16* q = xb + (nr * 32 + k) * K::SX + 16 * ks;
-            b[nr] = *(const half8_t*)q;
-            if constexpr (P == 1) bl[nr] = *(const half8_t*)(q + pstride);
+            bq[nr] = *(const half8_t*)q;
+            if constexpr (P == 1) bo[nr] = *(const half8_t*)(q + pstride);
         }
+    };
+    if constexpr (OU_BLOCK_BPIPE) load_b(0, b[0], bl[0]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        if (s + D - 1 < NS) load_a(s + D - 1, ra[(s + D - 1) % D]);
+        const int c = OU_BLOCK_BPIPE ? (s & 1) : 0;
+        if constexpr (OU_BLOCK_BPIPE) {
+            if (s + 1 < NS) load_b(s + 1, b[c ^ 1], bl[c ^ 1]);
+        } else {
+            load_b(s, b[0], bl[0]);
+        }
+        // the fully unrolled loop otherwise lets the scheduler sink the ring
+        // loads next to their use (2-3 steps of latency cover instead of D - 1)
+        if constexpr (OU_BLOCK_FENCE) asm volatile("" ::: "memory");
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
             for (int nr = 0; nr < NR; ++nr) {
-                acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][mr][0], b[nr], acc[mr][nr], 0, 0, 0);
+                acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][mr][0], b[c][nr], acc[mr][nr], 0, 0, 0);
                 if constexpr (P == 1) {
                     accx[mr][nr] =
-                        __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][mr][0], bl[nr], accx[mr][nr], 0, 0, 0);
+                        __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][mr][0], bl[c][nr], accx[mr][nr], 0, 0, 0);
                     accx[mr][nr] =
-                        __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][mr][1], b[nr], accx[mr][nr], 0, 0, 0);
+                        __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s % D][mr][1], b[c][nr], accx[mr][nr], 0, 0, 0);
                 }
             }
     }
@@ -247,7 +288,8 @@ template <int KT, int C, int NT, int P>
 __device__ __forceinline__ void run_stage(const void* w, const typename BCfg<C, NT, P>::E* xin, int pstride, int wm,
                                           int wn, int lane, int dbg,
                                           floatx16 (&acc)[BCfg<C, NT, P>::MR][BCfg<C, NT, P>::NR],
-                                          floatx16 (&accx)[BCfg<C, NT, P>::MR][BCfg<C, NT, P>::NR])
+                                          floatx16 (&accx)[BCfg<C, NT, P>::MR][BCfg<C, NT, P>::NR],
+                                          half8_t (&ra)[BCfg<C, NT, P>::RING][BCfg<C, NT, P>::MR][2], bool pre)
 {
     if constexpr (P == 0) {
         stage_mma_f32<KT, C, NT>((const f32x4_t*)w, xin, wm, wn, lane, dbg, acc);
@@ -256,7 +298,7 @@ __device__ __forceinline__ void run_stage(const void* w, const typename BCfg<C, 
 #pragma unroll
             for (int nr = 0; nr < BCfg<C, NT, P>::NR; ++nr) accx[mr][nr] = floatx16{};
     } else {
-        stage_mma<KT, C, NT, P>((const half8_t*)w, xin, pstride, wm, wn, lane, dbg, acc, accx);
+        stage_mma<KT, C, NT, P>((const half8_t*)w, xin, pstride, wm, wn, lane, dbg, acc, accx, ra, pre);
     }
 }
 
@@ -414,6 +456,11 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     const int hlo = d.h0, hhi = d.h1 > 0 ? min(d.h1, T) : T;   // h frames the caller produced
     const float* __restrict__ hb = d.h + (int64_t)b * d.h_bstride;
     bool ovf = false;
+    // weight-fragment ring shared by the three split-f16 / f16 stages; conv1's
+    // first fragments are requested before the input staging
+    constexpr bool early = OU_BLOCK_RING_EARLY && P != 0;
+    half8_t ring[K::RING][MR][2];
+    if constexpr (early) ring_pro<5, C, NT, P>(d.w[0], wm, lane, ring);
 
     // scaled input sample of the fused input conv (zero outside [0, T))
     const float* __restrict__ xin = (EPI & kEpiIn) ? d.x + (int64_t)b * d.x_bstride : nullptr;
@@ -513,7 +560,8 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     };
 
     // ---- stage 1: conv1 (k5) over frames t0 - 2 + u, u in [0, NF) -> region B
-    run_stage<5, C, NT, P>(d.w[0], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
+    run_stage<5, C, NT, P>(d.w[0], xa, K::PA, wm, wn, lane, d.dbg, acc, accx, ring, early);
+    if (early) ring_pro<3, C, NT, P>(d.w[1], wm, lane, ring);   // conv2's first fragments
     {
         const float a2 = d.slope[1];
         // operands of the epilogue, loaded before anything is stored
@@ -580,7 +628,8 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     __syncthreads();
 
     // ---- stage 2: conv2 (k3) over frames t0 - 1 + v -> region A
-    run_stage<3, C, NT, P>(d.w[1], xbuf, K::PB, wm, wn, lane, d.dbg, acc, accx);
+    run_stage<3, C, NT, P>(d.w[1], xbuf, K::PB, wm, wn, lane, d.dbg, acc, accx, ring, early);
+    if (early) ring_pro<3, C, NT, P>(d.w[2], wm, lane, ring);   // conv3's first fragments
     {
         const float a3 = d.slope[2], un = d.w_unscale[1];
         float bia[MR][16];
@@ -653,7 +702,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
         }
     };
     if constexpr (OU_BLOCK_HV_EARLY && !(EPI & kEpiIn)) load_res();
-    run_stage<3, C, NT, P>(d.w[2], xa, K::PA, wm, wn, lane, d.dbg, acc, accx);
+    run_stage<3, C, NT, P>(d.w[2], xa, K::PA, wm, wn, lane, d.dbg, acc, accx, ring, early);
     if constexpr (!(OU_BLOCK_HV_EARLY && !(EPI & kEpiIn))) load_res();
     {
         const float un = d.w_unscale[2];

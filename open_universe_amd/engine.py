@@ -1544,7 +1544,15 @@ class Engine:
         nr = len(rates)
         n_lvl = len(self.c_enc)
         B, U = x.B, bufs["U"]
-        # MelAdapter (condition.py:85-114): |STFT|^2 -> mel -> global norm -> conv -> ConvBlock
+        # MelAdapter (condition.py:85-114): |STFT|^2 -> mel -> global norm -> conv -> ConvBlock.
+        # Its output is first read by the level-0 st_conv (as that conv's
+        # residual), so with ``st_lane`` it is recorded there too: the
+        # conditioner's encoder -- the first step's critical path -- starts
+        # without waiting for it
+        mel_lane = st_lane if os.environ.get("OUHIP_MEL_LANE", "1") != "0" else None
+        if mel_lane is not None:
+            side = _LANE
+            set_lane(prog, mel_lane)
         prog.add(L.OP_CONV, conv_desc(self.c_stft, x, bufs["SPEC"], n_frames=U))
         pa = L.PowerArgs(x=bufs["SPEC"].ptr, y=bufs["POW"].ptr, batch=B, nf=self.mel_nfreq, frames=U)
         prog.add(L.OP_POWER, pa)
@@ -1554,6 +1562,8 @@ class Engine:
         prog.add(L.OP_INV_RMS, ra)
         prog.add(L.OP_CONV, conv_desc(self.c_melconv, bufs["MEL"], bufs["M0"], in_scale=bufs["INV"].data_ptr()))
         rec_block(prog, self.c_melblock, bufs["M0"], bufs["XMEL"], bufs["MA"], bufs["MB"])
+        if mel_lane is not None:
+            set_lane(prog, side)
         # encoder (condition.py:189-220)
         prog.add(L.OP_CONV, conv_desc(self.c_input, x, bufs["E0"]))
         nsum = 0
