@@ -244,10 +244,12 @@ def spec_up(sd, p, r, antialias):
     """Transposed PReLU_Conv(2C, C, r, stride=r) (+ FIR after, blocks.py:221-225)
     as a polyphase convolution over input frames producing r*C rows that the
     kernel's epilogue pixel-shuffles.  weight_norm dim 0 of a ConvTranspose1d
-    weight (Cin, Cout, r) is per input channel; fold_weight handles it.  Rows
-    are channel-major (m = co * r + ph): a lane's consecutive accumulator rows
-    are consecutive output samples, stored as one 16-B / two 8-B accesses at
-    r = 4 / 2 (ConvDesc.rout = -r).  OUHIP_UP_CM=0 keeps phase-major rows."""
+    weight (Cin, Cout, r) is per input channel; fold_weight handles it.  At
+    r >= 3 (OUHIP_UP_CM_MIN_RATE) the rows are channel-major (m = co * r + ph,
+    ConvDesc.rout = -r): a lane's consecutive accumulator rows are consecutive
+    output samples, stored as one 16-B access at r = 4 and completing whole
+    output lines within one wave at r = 5.  OUHIP_UP_CM=0 keeps phase-major
+    rows everywhere."""
     w = fold_weight(sd, p + ".conv").astype(np.float64)  # (Cin, Cout, r)
     cin, cout, _ = w.shape
     if antialias:
@@ -259,18 +261,22 @@ def spec_up(sd, p, r, antialias):
                 d = s_ // r
                 e = s_ - d * r
                 wl[ph, :, :, d + 1] += fir[j] * w[:, :, e].T
-        if UP_CM:
+        cm = UP_CM and r >= UP_CM_MIN_RATE
+        if cm:
             wl = wl.transpose(1, 0, 2, 3)
         return ConvSpec(np.ascontiguousarray(wl).reshape(r * cout, cin, 3), cin, 1, 1, r, _slope(sd, p),
-                        _bias(sd, p + ".bias"), ref_macs=float(cin * cout * r + cout * (2 * r + 1) * r), cm=UP_CM)
+                        _bias(sd, p + ".bias"), ref_macs=float(cin * cout * r + cout * (2 * r + 1) * r), cm=cm)
     wl = w.transpose(2, 1, 0)   # (r, cout, cin)
-    if UP_CM:
+    cm = UP_CM and r >= UP_CM_MIN_RATE
+    if cm:
         wl = wl.transpose(1, 0, 2)
     return ConvSpec(np.ascontiguousarray(wl).reshape(r * cout, cin, 1), cin, 1, 0, r, _slope(sd, p),
-                    _bias(sd, p + ".conv.bias"), ref_macs=float(cin * cout * r), cm=UP_CM)
+                    _bias(sd, p + ".conv.bias"), ref_macs=float(cin * cout * r), cm=cm)
 
 
 UP_CM = os.environ.get("OUHIP_UP_CM", "1") != "0"
+# rate 2 (the 64 -> 32-channel up conv) measured faster with phase-major rows
+UP_CM_MIN_RATE = int(os.environ.get("OUHIP_UP_CM_MIN_RATE", "3"))
 
 
 def prep_same(sd, p, k, device):
