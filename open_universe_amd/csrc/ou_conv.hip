@@ -753,10 +753,13 @@ __device__ __forceinline__ void split4r(float x0, float x1, float x2, float x3, 
 
 constexpr int kStageItems = 9;   // conv_rkernel: staging items (8 channels x 1 frame) per thread per round trip
 
+#ifndef OU_RS_RING
+#define OU_RS_RING 8
+#endif
 template <int KT, int WM, int WK, int NR>
 struct RCfg {
     static constexpr int BM = 32 * WM, BN = 32 * NR, W = BN + KT - 1;
-    static constexpr int RING = 8;   // weight-fragment ring depth (steps): 7 steps of MFMA hide the L2 latency
+    static constexpr int RING = OU_RS_RING;   // weight-fragment ring depth (steps): RING - 1 steps of MFMA hide the L2 latency
     static constexpr int RED = (WK - 1) * WM * NR * 16 * 64;   // floats of the K-split reduction
     static_assert(WM * WK == 4, "4 waves per workgroup");
 };
