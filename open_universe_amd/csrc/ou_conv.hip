@@ -754,7 +754,7 @@ __device__ __forceinline__ void split4r(float x0, float x1, float x2, float x3, 
 constexpr int kStageItems = 9;   // conv_rkernel: staging items (8 channels x 1 frame) per thread per round trip
 
 #ifndef OU_RS_RING
-#define OU_RS_RING 8
+#define OU_RS_RING 12
 #endif
 template <int KT, int WM, int WK, int NR>
 struct RCfg {

@@ -301,7 +301,6 @@ __device__ __forceinline__ void swap16(float& x, float& y)
 }
 
 constexpr int kKsWaves = 4;   // waves per workgroup
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 
 template <int H, int NB, int UW>
@@ -338,21 +337,14 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
     const int j = ubase + (lane >> USH);     // unit whose gates this lane computes
     const bool writer = (lane & ((1 << USH) - 1)) == 0;
 
-    // W_hh of units (2p, 2p + 1) side by side, scalar fmaf chains in k order.
-    // (v_pk_fma_f32 on these pairs measured no faster, and a recurrence split
-    // into step segments then no longer reproduced the whole launch bit for
-    // bit: tests/test_gpu_chunked.py)
-    f32x2 w[UW / 2][3][KPL];
+    float w[UW][3][KPL];
     const float* wbase = d.w_hh + (int64_t)dir * 3 * H * H + lane * KPL;
 #pragma unroll
-    for (int p = 0; p < UW / 2; ++p)
+    for (int u = 0; u < UW; ++u)
 #pragma unroll
         for (int g = 0; g < 3; ++g)
 #pragma unroll
-            for (int k = 0; k < KPL; ++k) {
-                w[p][g][k].x = wbase[(int64_t)(g * H + ubase + 2 * p) * H + k];
-                w[p][g][k].y = wbase[(int64_t)(g * H + ubase + 2 * p + 1) * H + k];
-            }
+            for (int k = 0; k < KPL; ++k) w[u][g][k] = wbase[(int64_t)(g * H + ubase + u) * H + k];
     const float bhr = d.b_hh[dir * 3 * H + 0 * H + j];
     const float bhz = d.b_hh[dir * 3 * H + 1 * H + j];
     const float bhn = d.b_hh[dir * 3 * H + 2 * H + j];
@@ -399,14 +391,8 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
     const int tb = d.t_begin, te = d.t_end > 0 ? min(d.t_end, T) : T;
     float hp[NB];                            // h_{t-1} of unit j
     float gir[NB], giz[NB], gin[NB], rsd[NB];
-    const bool no_gi = flags & 512;   // timing diagnostic only (gi, residual read as 0): wrong results
     auto prefetch = [&](int step) {
         const int tm = dir == 0 ? step : T - 1 - step;
-        if (no_gi) {
-#pragma unroll
-            for (int bb = 0; bb < NB; ++bb) gir[bb] = giz[bb] = gin[bb] = rsd[bb] = 0.f;
-            return;
-        }
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb) {
             if (bb < nbh) {
@@ -431,7 +417,7 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
     // so a step reads its four values with one ds_read_b128 issued before
     // the hand-off wait.  flags bit8 keeps the per-step prefetch (A/B runs).
     constexpr int CS = UW == 4 ? 128 : 64;   // steps per chunk (4 UW x CS x 4 B = 8 KB per wave)
-    const bool stage = NB == 1 && !(flags & 256) && !no_gi;
+    const bool stage = NB == 1 && !(flags & 256);
     float4* gst = nullptr;
     if constexpr (NB == 1) {
         __shared__ float4 gst_all[kKsWaves][CS * UW];
@@ -546,19 +532,15 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
         // partial dot products, value index (u * NB + b) * 3 + g
         float acc[NV];
 #pragma unroll
-        for (int p = 0; p < UW / 2; ++p)
+        for (int u = 0; u < UW; ++u)
 #pragma unroll
             for (int bb = 0; bb < NB; ++bb)
 #pragma unroll
                 for (int g = 0; g < 3; ++g) {
-                    f32x2 a = {0.f, 0.f};
+                    float a = 0.f;
 #pragma unroll
-                    for (int k = 0; k < KPL; ++k) {
-                        a.x = fmaf(w[p][g][k].x, h[bb][k], a.x);
-                        a.y = fmaf(w[p][g][k].y, h[bb][k], a.y);
-                    }
-                    acc[(2 * p * NB + bb) * 3 + g] = a.x;
-                    acc[((2 * p + 1) * NB + bb) * 3 + g] = a.y;
+                    for (int k = 0; k < KPL; ++k) a = fmaf(w[u][g][k], h[bb][k], a);
+                    acc[(u * NB + bb) * 3 + g] = a;
                 }
         OU_STAMP(1);
 

@@ -275,8 +275,8 @@ def spec_up(sd, p, r, antialias):
 
 
 UP_CM = os.environ.get("OUHIP_UP_CM", "1") != "0"
-# rate 2 (the 64 -> 32-channel up conv) measured faster with phase-major rows
-UP_CM_MIN_RATE = int(os.environ.get("OUHIP_UP_CM_MIN_RATE", "3"))
+# channel-major rows from this rate on (C2: rate 2 too measured faster, profiles/bench_ab_upcm_rate_r03p.txt)
+UP_CM_MIN_RATE = int(os.environ.get("OUHIP_UP_CM_MIN_RATE", "2"))
 
 
 def prep_same(sd, p, k, device):
