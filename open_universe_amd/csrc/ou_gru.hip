@@ -410,7 +410,8 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
     // the wave's UW units are staged through LDS in chunks of CS steps
     // instead of prefetched one step ahead.  Vector loads retire in order, so
     // the poll loop's vmcnt wait also waited for the previous step's gi
-    // prefetch (~0.07 us of a 0.8 us step: tools/gru_bench.py, flags 513);
+    // prefetch (~0.07 us of a 0.8 us step, measured with a build that skipped
+    // the gi loads);
     // a chunk load pays that latency once per CS steps.  Per wave and chunk
     // the 4 UW rows (3 gates x UW units of gi, UW residual rows) x CS steps
     // are loaded coalesced along time and written as [step][unit][r z n res],
