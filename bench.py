@@ -286,6 +286,9 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
                     help="BASELINE.json config (c2 = configs[1], the headline)")
     ap.add_argument("--seconds", type=float, default=None, help="override the config's clip length")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="clips per rank, overriding the config's (c4 at 16/8/4 on one GPU = the per-rank "
+                         "shard at 2/4/8 GPUs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-queued", action="store_true",
@@ -317,7 +320,7 @@ def main():
     C = CONFIGS[args.config]
     if args.seconds is None:
         args.seconds = C["seconds"]
-    B = rank_batch(C, world)
+    B = rank_batch(C, world) if args.batch is None else args.batch
 
     if args.stub_ms is not None:
         # launcher/control-plane test without a GPU: a step is a sleep
@@ -367,6 +370,7 @@ def main():
             prof = profile_roofline(plan, torch.cuda.current_stream(dev).cuda_stream, args.dump_ops)
 
     prec = model._get_engine().conv_prec
+    fallbacks = model.range_fallbacks   # timed-loop enhances rerun with f32 operands (OuRangeError)
     # the strictly-f32 figure: a second timed pass with f32 conv operands
     f32 = None
     if prec != 0 and not args.no_f32_pass and args.config in ("c2", "c4"):
@@ -436,7 +440,12 @@ def main():
                        "clip_s": args.seconds, "n_steps": C["n_steps"] or 8,
                        "parallelism": f"utterance-shard x{world}"},
             "xrt_per_gpu": round(value / world, 3),
+            "fallbacks": fallbacks,
+            "fallbacks_note": "enhance() calls of the timed loop (and warm-up) whose split-f16 conv operands left "
+                              "their range and were rerun with f32 operands; after one, the model stays on f32",
         }
+        if args.batch is not None:
+            out["config"]["batch_override"] = True
         if queued is not None:
             out["queued_value"] = queued["value"]
             out["queued"] = {**queued, "note": "extra leg: the same batch-1 clips, enhance() calls in flight "

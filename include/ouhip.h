@@ -187,8 +187,9 @@ typedef struct ou_gru_desc {
     int32_t ws_zeroed;         /* nonzero: the caller zeroed the workspace before */
                                /* the first launch on it (per replay); launches   */
                                /* leave it reusable, so no per-launch memset --   */
-                               /* needs steps >= 4 (the step tags of the previous */
-                               /* launch must not match a new launch's first two) */
+                               /* launches of steps < 5 still clear it (the tags  */
+                               /* T-1, T-2 a launch leaves must not match a new   */
+                               /* launch's first two polls, tags 1 and 2)         */
     int32_t _pad;
     const void* w_hh16;        /* non-NULL: W_hh in f16 packed by                 */
                                /* ou_gru_pack_cu16 (hidden 256, the f16 operand   */

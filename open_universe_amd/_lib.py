@@ -414,6 +414,9 @@ class Program:
                               "tile": desc.tile})
         elif op == OP_GRU:
             self.info.append({"H": desc.hidden, "T": desc.steps, "b": desc.batch})
+        elif op == OP_BLOCK:
+            self.info.append({"C": desc.channels, "n": desc.length, "b": desc.batch, "prec": desc.prec,
+                              "rate": desc.rate if desc.e else 0, "head": bool(desc.head.w), "in": bool(desc.x)})
         else:
             self.info.append({})
 

@@ -83,10 +83,42 @@ def audio_info(path):
         L.check(lib.ou_flac_info(buf, len(data), ctypes.byref(fs), ctypes.byref(ch), ctypes.byref(bps),
                                  ctypes.byref(n)), f"flac {path}")
         return int(ch.value), int(n.value), int(fs.value)
-    from scipy.io import wavfile
+    return _wav_info(path)
 
-    fs, data = wavfile.read(str(path), mmap=True)
-    return (data.shape[1] if data.ndim > 1 else 1), int(data.shape[0]), int(fs)
+
+def _wav_info(path):
+    """(channels, frames, sample rate) from a WAV file's RIFF 'fmt ' and
+    'data' chunk headers: frames = data bytes // block align.  Reads headers
+    only, so every container width works (scipy's mmap reader refuses 24-bit
+    PCM, which ``load_audio`` reads)."""
+    import os
+    import struct
+
+    size = os.path.getsize(path)
+    with open(path, "rb") as fh:
+        head = fh.read(12)
+        if len(head) < 12 or head[:4] != b"RIFF" or head[8:12] != b"WAVE":
+            raise ValueError(f"{path}: not a RIFF/WAVE file")
+        ch = fs = align = None
+        while True:
+            hdr = fh.read(8)
+            if len(hdr) < 8:
+                raise ValueError(f"{path}: no 'data' chunk")
+            cid, n = hdr[:4], struct.unpack("<I", hdr[4:])[0]
+            if cid == b"fmt ":
+                fmt = fh.read(n)
+                if len(fmt) < 16:
+                    raise ValueError(f"{path}: short 'fmt ' chunk")
+                _, ch, fs, _, align = struct.unpack("<HHIIH", fmt[:14])
+                if n & 1:
+                    fh.seek(1, 1)
+            elif cid == b"data":
+                if ch is None or not align:
+                    raise ValueError(f"{path}: 'data' before 'fmt '")
+                n = min(n, size - fh.tell())   # streamed files may carry 0xFFFFFFFF
+                return int(ch), int(n // align), int(fs)
+            else:
+                fh.seek(n + (n & 1), 1)
 
 
 def resampled_len(n, orig_freq, new_freq):

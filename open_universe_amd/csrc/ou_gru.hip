@@ -894,13 +894,16 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
         return ou_check_launch("gru");
     }
     if (!d.w_hh || !d.granules || !d.status) return ou_fail(-1, "gru: invalid descriptor");
-    // the k-split kernel clears its placement slots when it exits, and the
-    // step tags of a previous launch (>= steps - 1 >= 3) never match a new
-    // launch's first polls (tags 1, 2): a workspace zeroed once per replay
-    // serves every launch of it (ws_zeroed)
+    // the k-split kernel clears its placement slots when it exits.  A launch
+    // of T steps leaves the tags T - 1 and T - 2 in the two parity slots (it
+    // writes tag t + 1 for t + 1 < T); a new launch's first polls look for
+    // tags 1 and 2, and every later poll of a slot follows one that already
+    // saw this launch's tag there.  So with T - 2 >= 3 (T >= 5) a workspace
+    // zeroed once per replay serves every launch of it (ws_zeroed); shorter
+    // launches clear it themselves.
     // a launch continuing a split recurrence (t_begin > 0) starts from hstate:
     // the tags the previous launches left are all older than the ones it polls
-    if ((!d.ws_zeroed && d.t_begin == 0) || d.steps < 4)
+    if ((!d.ws_zeroed && d.t_begin == 0) || d.steps < 5)
         OU_HIP_CHECK(hipMemsetAsync(d.granules, 0, ou_gru_workspace_bytes(d.hidden, d.batch), s), "gru: memset");
     // k-split kernel (default for H % 64 == 0; flags bit5 selects the
     // workgroup-gather kernel below)

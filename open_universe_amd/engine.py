@@ -245,7 +245,7 @@ def spec_up(sd, p, r, antialias):
     as a polyphase convolution over input frames producing r*C rows that the
     kernel's epilogue pixel-shuffles.  weight_norm dim 0 of a ConvTranspose1d
     weight (Cin, Cout, r) is per input channel; fold_weight handles it.  At
-    r >= 3 (OUHIP_UP_CM_MIN_RATE) the rows are channel-major (m = co * r + ph,
+    r >= 2 (OUHIP_UP_CM_MIN_RATE) the rows are channel-major (m = co * r + ph,
     ConvDesc.rout = -r): a lane's consecutive accumulator rows are consecutive
     output samples, stored as one 16-B access at r = 4 and completing whole
     output lines within one wave at r = 5.  OUHIP_UP_CM=0 keeps phase-major
@@ -1280,8 +1280,11 @@ class Engine:
         if not (fuse_ends_enabled() and self.s_in_fusable and b0.fused is not None and b0.C == 32
                 and bl.fused is not None and bl.C == 32):
             return None
-        if any(bw.fused is None and bw.conv1.prec == 0 for bw in self.s_enc + self.s_dec):
-            return None   # f32 tiles may be persistent (no frame offset)
+        if self.conv_prec == 0 or any(bw.conv1.prec == 0 for bw in self.s_enc + self.s_dec):
+            # f32 operands: the rate-change, up and GRU-projection convs (and
+            # unfused blocks) may tune to persistent f32 tiles, which take no
+            # frame offset
+            return None
         f1, f2 = (float(v) for v in os.environ.get("OUHIP_CHUNK_SPLIT", "0.25,0.7").split(","))
         h = T4 // 2
         s1 = max(8, min(h - 8, int(round(f1 * T4))))

@@ -86,6 +86,7 @@ class Universe(nn.Module):
         self._plans = collections.OrderedDict()   # LRU of recorded plans, see _plan()
         self._inflight = set()   # plan keys submitted by enhance_many and not yet checked
         self._conv_prec = None   # None: OUHIP_CONV_PREC; 0 after a split-f16 range error
+        self.range_fallbacks = 0   # enhance()/enhance_many() calls rerun with f32 operands
 
     def init_losses(self, score_model, condition_model, losses, training):
         """Training losses are out of scope; nothing to build for Universe."""
@@ -308,6 +309,7 @@ class Universe(nn.Module):
                 # this model to f32 operands and rerun on the same noise
                 nz = plan.NZ.clone()
                 self._conv_prec = 0
+                self.range_fallbacks += 1
                 self.invalidate()
                 plan = self._arena_plan(key, 0, make_plan)
                 x = plan.run_with_noise(mix, nz).clone()[:, None, :]
@@ -387,6 +389,7 @@ class Universe(nn.Module):
             # as enhance(): a split-f16 input left its range -> f32 operands,
             # same noise, every clip of the call
             self._conv_prec = 0
+            self.range_fallbacks += 1
             self.invalidate()
             eng = self._get_engine()
             outs = []

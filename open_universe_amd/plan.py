@@ -234,7 +234,7 @@ class EnhancePlan(_PlanBase):
                 coefs.append(c)
             self.WIN = torch.from_numpy(win).to(dev)
             # the chunked score pass (Engine.chunk_plan): GRU segments on lane
-            # 4, conv chunks on lanes 2 / 3
+            # 0, conv chunks on side lanes 2 / 3 (rec_score_chunked)
             self.chunks = eng.chunk_plan(B, Tp, force=chunk is True) if chunk is not False else None
             self.sb = eng.alloc_score(B, Tp, chunked=self.chunks is not None)
             E.rec_gru_ws_zero(p, self.sb["gran"])   # lane 0, ahead of the first score GRU

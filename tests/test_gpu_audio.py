@@ -111,6 +111,7 @@ def test_enhance_cli_outputs_independent_of_world_size(tmp_path, monkeypatch, st
 
     from open_universe_amd.bin import enhance as cli
     from test_api_surface import _write_ckpt
+    from wav_writer import write_wav24
 
     ckpt, _, _, _ = _write_ckpt(str(tmp_path), with_ema=False)
     src = tmp_path / "noisy"
@@ -119,7 +120,10 @@ def test_enhance_cli_outputs_independent_of_world_size(tmp_path, monkeypatch, st
     lens = {"w0.wav": (16000, 9000), "w1.wav": (48000, 30000), "w2.wav": (16000, 4000), "w3.wav": (8000, 7000),
             "w4.wav": (16000, 12000)}
     for name, (fs, n) in lens.items():
-        wavfile.write(src / name, fs, (rng.standard_normal(n) * 0.1).astype(np.float32))
+        if name == "w3.wav":   # a 24-bit PCM file: audio_info parses its header on every rank
+            write_wav24(src / name, fs, rng.standard_normal(n) * 0.1)
+        else:
+            wavfile.write(src / name, fs, (rng.standard_normal(n) * 0.1).astype(np.float32))
     common = ["--model", ckpt, "--n_steps", "3", "--seed", "11", "--device", "cuda:0", "--streams", str(streams),
               "--chunk", "2"]
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):

@@ -123,6 +123,43 @@ def test_gru_layer(pp16):
     assert rel_rms(y.t.cpu(), ref) < 1e-5
 
 
+@pytest.mark.parametrize("T", [2, 3, 4, 5, 6])
+def test_gru_ws_zeroed_short_launches_back_to_back(pp16, T):
+    """Launches that skip the per-launch memset (ou_gru_desc.ws_zeroed) on one
+    workspace zeroed once: a short launch's leftover step tags (T-1, T-2) must
+    not satisfy the next launch's first polls (tags 1, 2) -- launches of fewer
+    than 5 steps clear the workspace themselves.  Each of three back-to-back
+    launches must equal the same layer run alone with a per-launch memset."""
+    d, cfg, m = pp16
+    eng = m._get_engine()
+    B = 2
+    xs = [torch.randn(B, 512, T, generator=torch.Generator().manual_seed(20 + i)) * 0.5 for i in range(3)]
+    gran = torch.zeros(L.load().ou_gru_workspace_bytes(256, B) // 8, dtype=torch.int64, device=DEV)
+
+    def run(ws_zeroed, inputs):
+        saved, E._GRU_WS_ZEROED = E._GRU_WS_ZEROED, ws_zeroed
+        try:
+            prog = L.Program()
+            if ws_zeroed:
+                E.rec_gru_ws_zero(prog, gran)
+            outs = []
+            for x in inputs:
+                xa, gi, y = E.Act(x.to(DEV)), E.new_act(B, 1536, T, DEV), E.new_act(B, 512, T, DEV)
+                E.rec_gru(prog, eng.s_gru, 0, xa, gi, y, gran, eng.status)
+                outs.append((xa, gi, y))
+            prog.run(torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+        finally:
+            E._GRU_WS_ZEROED = saved
+        assert int(eng.status.max()) == 0
+        return [y.t.cpu() for _, _, y in outs]
+
+    chained = run(True, xs)
+    for x, yc in zip(xs, chained):
+        alone = run(False, [x])[0]
+        assert torch.equal(yc, alone)
+
+
 @pytest.mark.parametrize("B,T", [(1, 301), (2, 57)])
 def test_gru_layer_f16_single_cu(pp16, B, T):
     """The f16 operand mode's recurrence (ou_gru with w_hh16: one 1024-thread

@@ -172,7 +172,11 @@ def test_full_width_pp24_enhance():
     with torch.no_grad():
         out = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
     assert m._get_engine().conv_prec == 0   # the f32 rerun happened
+    assert m.range_fallbacks == 1            # once, and reported (bench.py "fallbacks")
     assert rel_rms(out, d["enh_out"]) < 1e-3 and si_sdr(out, d["enh_out"]) > 60
+    with torch.no_grad():   # the model stays on f32 operands: no second rerun
+        out2 = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
+    assert m.range_fallbacks == 1 and torch.equal(out2, out)
 
 
 def test_full_width_pp24_damped_split_f16_vs_reference():
@@ -238,6 +242,25 @@ def test_c4_real_shape_damped_split_f16_item0_vs_oracle():
         ref = _oracle(m, cfg).enhance(mix[:1], noise_fn=lambda shp: nz[next(it), :1].reshape(shp))
     assert rel_rms(out[:1], ref) < 1e-3 and si_sdr(out[:1], ref) > 60
     # the other items are not copies of item 0
+    assert rel_rms(out[1:2], out[:1]) > 0.1
+
+
+def test_c3_real_shape_item0_vs_oracle():
+    """BASELINE configs[2] at its benched geometry: ORIG16 full width, batch 8,
+    8 s clips, 60 diffusion steps (universe.py:301-343 with n_steps=60), split-
+    f16 operands, the whole batch on the GPU; item 0 against the fp32 oracle on
+    the same noise slice (about 10 s of host time)."""
+    cfg, m = _synth_model("orig16", 0)
+    mix = _clips(8, 8.0, cfg["fs"], base=41)
+    with torch.no_grad():
+        out = m.enhance(mix.to(DEV), n_steps=60, rng=torch.Generator().manual_seed(2026)).cpu()
+        eng = m._get_engine()
+        assert eng.conv_prec == 1 and int(eng.status.abs().sum()) == 0 and m.range_fallbacks == 0
+        assert out.shape == (8, 128000) and torch.isfinite(out).all()
+        nz = next(iter(m._plans.values())).NZ.cpu()   # (draws, 8, 1, Tp): the noise the GPU used
+        it = iter(range(nz.shape[0]))
+        ref = _oracle(m, cfg).enhance(mix[:1], n_steps=60, noise_fn=lambda shp: nz[next(it), :1].reshape(shp))
+    assert rel_rms(out[:1], ref) < 1e-3 and si_sdr(out[:1], ref) > 60
     assert rel_rms(out[1:2], out[:1]) > 0.1
 
 
