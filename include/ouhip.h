@@ -545,6 +545,12 @@ int ou_program_op_kind(const ou_program* p, int i);
  * per-op device time in milliseconds to ms[0..size) (synchronises).  Used by
  * bench.py to attribute time to kernels inside the same workload. */
 int ou_program_profile(ou_program* p, void* stream, float* ms);
+/* Eager replay with the lanes on their streams (as ou_program_run) and a
+ * hipEvent before and after every op on its lane: t0[i] / t1[i] = ms from the
+ * replay's start to when op i's lane reached / finished it, -1 for sync ops
+ * (synchronises).  The concurrent timeline of the lane schedule
+ * (tools/critical_path.py). */
+int ou_program_trace(ou_program* p, void* stream, float* t0, float* t1);
 
 #ifdef __cplusplus
 }

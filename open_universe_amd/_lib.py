@@ -211,6 +211,7 @@ EXPORTS = {
     "ou_program_launch": (c_int, [c_void_p, c_void_p]),
     "ou_program_op_kind": (c_int, [c_void_p, c_int]),
     "ou_program_profile": (c_int, [c_void_p, c_void_p, POINTER(c_float)]),
+    "ou_program_trace": (c_int, [c_void_p, c_void_p, POINTER(c_float), POINTER(c_float)]),
 }
 
 _lib = None
@@ -399,15 +400,22 @@ class Program:
         self.flops = []         # algorithmic FLOPs of the reference ops each op replaces
         self.bytes = []         # algorithmic HBM bytes of each op (0 where not counted)
         self.info = []          # per-op geometry (profiling / reports)
+        self.lanes = []         # lane of each op
+        self.label = ""         # phase label recorded with each op (engine sets it; reports only)
+        self.labels = []
 
     def add(self, op, desc):
         assert isinstance(desc, OP_STRUCT[op])
+        if op == OP_LANE:
+            self.cur_lane = desc.id
         if op == OP_CONV and desc.tile < 0 and TUNER is not None:
             desc.tile = TUNER(desc)
         check(self.lib.ou_program_add(self.h, op, ctypes.byref(desc), ctypes.sizeof(desc)),
               f"program_add(op={op})")
         self.flops.append(float(getattr(desc, "_flops", 0.0)))
         self.bytes.append(float(getattr(desc, "_bytes", 0.0)))
+        self.lanes.append(self.cur_lane)
+        self.labels.append(self.label)
         if op == OP_CONV:
             self.info.append({"m": desc.m, "cin": desc.cin, "frame": desc.frame, "kt": desc.kt,
                               "n": desc.n_frames, "b": desc.batch, "rout": desc.rout,
@@ -424,7 +432,6 @@ class Program:
     # in eager replay, parallel branches of the captured hipGraph)
     def lane(self, i):
         self.add(OP_LANE, SyncArgs(id=i))
-        self.cur_lane = i
 
     def new_event(self):
         self.n_events = getattr(self, "n_events", 0) + 1
@@ -471,6 +478,15 @@ class Program:
         buf = (c_float * n)()
         check(self.lib.ou_program_profile(self.h, c_void_p(stream), buf), "program_profile")
         return list(buf)
+
+    def trace(self, stream):
+        """Eager replay with the lanes on their streams and events around
+        each op -> per-op (start ms, end ms) from the replay's start (None
+        for sync ops)."""
+        n = len(self)
+        a, b = (c_float * n)(), (c_float * n)()
+        check(self.lib.ou_program_trace(self.h, c_void_p(stream), a, b), "program_trace")
+        return [(x, y) if x >= 0 else None for x, y in zip(a, b)]
 
     def __del__(self):
         try:

@@ -477,6 +477,60 @@ int ou_program_op_kind(const ou_program* p, int i)
     return p->ops[i].kind;
 }
 
+// Eager replay with the lanes on their streams (as ou_program_run) and a
+// timing event before and after every op on its lane: t0[i] / t1[i] = ms from
+// the replay's start (an event on lane 0 before the first op) to the moment
+// op i's stream reached the op / finished it (-1 for sync ops).  Concurrency
+// is kept, so the timeline shows the critical path of the lane schedule.
+int ou_program_trace(ou_program* p, void* stream, float* t0, float* t1)
+{
+    if (!p || !t0 || !t1) return ou_fail(-1, "program_trace: null");
+    hipStream_t s0 = (hipStream_t)stream;
+    int nl = 1, ne = 0;
+    int rc = validate_lanes(p, &nl, &ne);
+    if (rc) return rc;
+    if ((rc = ensure_sync(p, nl, ne))) return rc;
+    hipStream_t side[kMaxSide] = {};
+    if (nl > 1) {
+        int dev = 0;
+        if ((rc = current_device(&dev))) return rc;
+        for (int l = 1; l < nl; ++l)
+            if ((rc = shared_stream(&g_side[dev][l - 1], &side[l - 1]))) return rc;
+    }
+    const size_t n = p->ops.size();
+    std::vector<hipEvent_t> ev(2 * n + 1, nullptr);
+    for (auto& e : ev) OU_HIP_CHECK(hipEventCreate(&e), "event create");
+    (void)hipEventRecord(ev[2 * n], s0);
+    hipStream_t cur = s0;
+    for (size_t i = 0; i < n && rc == 0; ++i) {
+        const auto& o = p->ops[i];
+        if (is_sync(o.kind)) {
+            const int v = ((const ou_sync_args*)o.desc.data())->id;
+            if (o.kind == OU_OP_LANE) cur = v == 0 ? s0 : side[v - 1];
+            else if (o.kind == OU_OP_SIGNAL) OU_HIP_CHECK(hipEventRecord(p->events[v], cur), "program signal");
+            else OU_HIP_CHECK(hipStreamWaitEvent(cur, p->events[v], 0), "program wait");
+            continue;
+        }
+        (void)hipEventRecord(ev[2 * i], cur);
+        rc = run_op(o.kind, o.desc.data(), cur);
+        (void)hipEventRecord(ev[2 * i + 1], cur);
+    }
+    if (rc == 0) {
+        hipError_t e = hipDeviceSynchronize();
+        if (e != hipSuccess) rc = ou_fail(-100, "trace sync: %s", hipGetErrorString(e));
+    }
+    for (size_t i = 0; i < n && rc == 0; ++i) {
+        float a = -1.f, b = -1.f;
+        if (!is_sync(p->ops[i].kind)) {
+            (void)hipEventElapsedTime(&a, ev[2 * n], ev[2 * i]);
+            (void)hipEventElapsedTime(&b, ev[2 * n], ev[2 * i + 1]);
+        }
+        t0[i] = a, t1[i] = b;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    return rc;
+}
+
 int ou_program_profile(ou_program* p, void* stream, float* ms)
 {
     if (!p || !ms) return ou_fail(-1, "program_profile: null");

@@ -1207,6 +1207,7 @@ class Engine:
         nr = len(self.rates)
         fb = lambda j: film_base + 4 * self.film_off[j]
         # input conv (score.py:244-246, 285)
+        prog.label = "score enc"
         d_in = conv_desc(self.s_input, x, bufs["E0"], in_scale=in_scale)
         fuse_in = (self.s_enc[0].fused is not None and self.s_enc[0].C == 32 and self.s_in_fusable
                    and fuse_ends_enabled())
@@ -1215,12 +1216,14 @@ class Engine:
         # encoder (score.py:105-115)
         for i in range(n_lvl):
             bw = self.s_enc[i]
+            prog.label = f"score enc L{i}"
             x_in = (x, in_scale, self.s_in_w, self.s_in_b, d_in) if (i == 0 and fuse_in) else None
             rec_block(prog, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
                       film=fb(i), film_bs=film_bs, x_in=x_in,
                       e_out=bufs[f"E{i+1}"] if bw.kind == "down" else None)
         # bottleneck GRU, fused with the decoder's first residual add
         top = n_lvl - 1
+        prog.label = "score gru"
         rec_gru(prog, self.s_gru, 0, bufs[f"V{top}"], bufs["GI"], bufs[f"V{top}"],
                 bufs["gran"], self.status, res=bufs[f"V{top}"], res_scale=NF2)
         # decoder (score.py:197-211)
@@ -1230,6 +1233,7 @@ class Engine:
             bw = self.s_dec[l]
             if before_level is not None:
                 before_level(l)
+            prog.label = f"score dec L{i}"
             if bw.kind == "up":
                 li = min(i, nr)
                 prog.add(L.OP_CONV, conv_desc(bw.rate_conv, h, bufs[f"V{i}"], n_frames=h.T,
@@ -1562,6 +1566,7 @@ class Engine:
         if mel_lane is not None:
             side = _LANE
             set_lane(prog, mel_lane)
+        prog.label = "cond mel"
         prog.add(L.OP_CONV, conv_desc(self.c_stft, x, bufs["SPEC"], n_frames=U))
         pa = L.PowerArgs(x=bufs["SPEC"].ptr, y=bufs["POW"].ptr, batch=B, nf=self.mel_nfreq, frames=U)
         prog.add(L.OP_POWER, pa)
@@ -1574,10 +1579,12 @@ class Engine:
         if mel_lane is not None:
             set_lane(prog, side)
         # encoder (condition.py:189-220)
+        prog.label = "cond enc L0"
         prog.add(L.OP_CONV, conv_desc(self.c_input, x, bufs["E0"]))
         nsum = 0
         for i in range(n_lvl):
             bw = self.c_enc[i]
+            prog.label = f"cond enc L{i}"
             if i < nr:
                 rec_block(prog, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
                           e_out=bufs[f"E{i+1}"])
@@ -1588,8 +1595,10 @@ class Engine:
                         ev = prog.signal()
                         set_lane(prog, st_lane)
                         prog.wait(ev)
+                    prog.label = f"cond st{i}"
                     prog.add(L.OP_CONV, conv_desc(self.c_st[i], bufs[f"V{i}"], bufs["SUM"],
                                                   n_frames=U, res1=prev, s1=1.0))
+                    prog.label = f"cond enc L{i}"
                     if st_lane is not None:
                         set_lane(prog, side)
                     nsum += 1
@@ -1606,19 +1615,25 @@ class Engine:
                           res2=bufs["SUM"], s2=nf)
         if not self.c_extra:
             raise NotImplementedError("conditioner without extra_conv_block")
+        prog.label = "cond cb1"
         rec_block(prog, self.c_cb1, bufs["OUT"], bufs["CB1"], bufs["LA"], bufs["LB"])
+        prog.label = "cond gru1"
         rec_gru(prog, self.c_gru, 0, bufs["CB1"], bufs["GI"], bufs["G1"], bufs["gran"], self.status)
         res = bufs["CB1"] if self.c_gru_res else None
+        prog.label = "cond gru2"
         rec_gru(prog, self.c_gru, 1, bufs["G1"], bufs["GI"], bufs["G2"], bufs["gran"], self.status,
                 res=res, res_scale=NF2)
+        prog.label = "cond cb2"
         rec_block(prog, self.c_cb2, bufs["G2"], bufs["H"], bufs["LA"], bufs["LB"])
         # decoder (condition.py:264-270)
+        prog.label = "cond dec in"
         rec_block(prog, self.c_dec_in, bufs["H"], bufs["D0"], bufs["LA"], bufs["LB"])
         h = bufs["D0"]
         for l in range(n_lvl):
             bw = self.c_dec[l]
             i = n_lvl - 1 - l
             li = min(i, nr)
+            prog.label = f"cond dec L{i}"
             if bw.kind == "up":
                 hup = bufs["HUP"][l]
                 prog.add(L.OP_CONV, conv_desc(bw.rate_conv, h, hup, n_frames=h.T,

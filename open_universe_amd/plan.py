@@ -163,6 +163,7 @@ class EnhancePlan(_PlanBase):
         E._GRU_WS_ZEROED = True
         # ---- record ----
         mixact = Act(self.MIX)
+        p.label = "prep"
         if keep_rms:
             p.add(L.OP_RMS, L.RmsArgs(x=mixact.ptr, out=self.MIXRMS.data_ptr(), batch=B,
                                       n=mix_len, denom=float(mix_len), eps=0.0))
@@ -189,6 +190,7 @@ class EnhancePlan(_PlanBase):
             self.SC = eng.alloc_sc(B, Tp)
 
             def after_level(l, cond):
+                p.label = f"cond sc{l}"
                 p.add(L.OP_CONV, E.conv_desc(eng.s_sc[l], cond, self.SC[l]))
                 ev_cond[l] = p.signal()
         conds, yaux = eng.rec_cond(p, cb, self.XN, need_aux=use_aux_signal or warm_start is not None,
@@ -216,6 +218,7 @@ class EnhancePlan(_PlanBase):
             self.SNET = torch.from_numpy(snet).to(dev)
             self.FILM = E.empty((n_steps, eng.film_rows), dtype=torch.float32, device=dev)
             self.GBUF = E.empty((n_steps, eng.emb_dim), dtype=torch.float32, device=dev)
+            p.label = "score embed"
             eng.rec_embed(p, self.SNET, n_steps, self.FILM, self.GBUF)
             win = np.ones((n_steps, B), dtype=np.float32)
             coefs = []
@@ -268,6 +271,7 @@ class EnhancePlan(_PlanBase):
                 # before its next node adds an edge to that node, and a capture
                 # whose node took 9 crashed in the HIP runtime)
                 p.wait(max(ev_cond.values()))
+        p.label = "finish"
         p.add(L.OP_FINISH, L.FinishArgs(x=x_final.ptr, x_bstride=Tp, left=self.pad // 2,
                                         batch=B, len=mix_len, y=self.OUT.data_ptr(),
                                         mix_rms=self.MIXRMS.data_ptr() if keep_rms else 0))

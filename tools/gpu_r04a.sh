@@ -16,3 +16,5 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method threa
 tail -3 $O/tests_$TAG.log
 bash tools/gpu_profile.sh $TAG c2 || exit 1
 bash tools/gpu_level_pmc.sh ${TAG}_lv c2 || exit 1
+timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 --ops --out $O/cp_$TAG.json > $O/cp_$TAG.txt 2>&1 || { tail -20 $O/cp_$TAG.txt; exit 1; }
+head -60 $O/cp_$TAG.txt
