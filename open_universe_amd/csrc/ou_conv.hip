@@ -760,6 +760,7 @@ template <int KT, int WM, int WK, int NR>
 struct RCfg {
     static constexpr int BM = 32 * WM, BN = 32 * NR, W = BN + KT - 1;
     static constexpr int RING = OU_RS_RING;   // weight-fragment ring depth (steps): RING - 1 steps of MFMA hide the L2 latency
+    static constexpr int DR = KT == 5 ? (RING / 5 > 1 ? RING / 5 : 2) * 5 : (KT == 3 ? RING / 3 * 3 : RING);   // a multiple of KT
     static constexpr int RED = (WK - 1) * WM * NR * 16 * 64;   // floats of the K-split reduction
     static_assert(WM * WK == 4, "4 waves per workgroup");
 };
@@ -779,7 +780,8 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
                                                     int S)
 {
     using R = RCfg<KT, WM, WK, NR>;
-    constexpr int W = R::W, D = R::RING;
+    constexpr int W = R::W;
+    OU_CSTAMP_INIT
     OU_DYNAMIC_LDS(float4, lds4);
     _Float16* xs = (_Float16*)lds4;
     // K channels: the frame view's cin * R (phase-major: ph * cin + ci), in
@@ -788,7 +790,8 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     // window fits LDS
     const int cin = d.cin, RF = d.frame, CEC = PC * CCH, SX = CEC + 8, HALF = CEC / 2, plane = W * SX;
     const int nchc = cin / CCH, nchunks = (RF / PC) * nchc;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar step math
     const int wm = wave % WM, wk = wave / WM;
     const int h = lane >> 5, l32 = lane & 31;
     int bx, by, bz;
@@ -813,10 +816,24 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     // (G = the chunk's first 16-group + g) through a D-deep ring whose first
     // D - 1 steps are issued before the chunk's staging, so their L2 latency
     // overlaps it.
-    const int NS = (CEC / 16) * KT;
-    const int s0 = wk * NS / WK, s1 = (wk + 1) * NS / WK;
-    const half8_t* ap0 = (const half8_t*)d.w + mt * (a_mt_stride / 4) + lane;
-    half8_t ra[D][2];
+    // K steps of a chunk: i = (16-channel group g of the chunk, tap k) with
+    // i = (g - g0) KT + k; wave wk owns groups [g0, g1).  A fragments (hi |
+    // lo) stream from the packed order [m-tile][G][hi | lo][tap][lane][8]
+    // (G = the chunk's first 16-group + g) through a DR-deep register ring
+    // (DR a multiple of KT), DR - 1 steps ahead; the ring's first steps are
+    // issued before the chunk's staging, so their L2 latency overlaps it.
+    // Every step index, offset and bound is wave-uniform (the wave index
+    // goes through readfirstlane), so the step loop's address arithmetic runs
+    // on the scalar unit: buffer loads with a lane-constant voffset and a
+    // scalar soffset, LDS reads at per-(frame tile, tap) row bases advanced
+    // once per DR steps, and uniform branches for the ragged last block --
+    // the MFMA gaps carry no per-step VALU index math.
+    constexpr int DR = R::DR;
+    const int G = CEC / 16;
+    const int g0 = wk * G / WK, g1 = (wk + 1) * G / WK, n = (g1 - g0) * KT;
+    const __amdgpu_buffer_rsrc_t ars = ou_rsrc((const char*)d.w + (int64_t)mt * a_mt_stride * 4, a_mt_stride * 4);
+    const unsigned avoff = (unsigned)lane * 16u;
+    half8_t ra[DR][2];
     const float* xb = d.x + (int64_t)b * d.x_bstride;
     const int64_t xc = d.x_cstride;
     const float scale = d.in_scale ? d.in_scale[b] : 1.f, slope = d.slope;
@@ -825,22 +842,29 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     const int WS = W * PC;                                 // window samples of one chunk, per channel
     const int NI = (CCH / 8) * WS;
     bool ovf = false;
-    const _Float16* xp = xs + l32 * SX + h * HALF;
+    // LDS row bases of this lane's B fragments, per (frame tile, tap), at group g0
+    const _Float16* xrow[NR][KT];
+#pragma unroll
+    for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+        for (int k = 0; k < KT; ++k) xrow[nr][k] = xs + (l32 + nr * 32 + k) * SX + h * HALF + 8 * g0;
     const int qa = ks * nchunks / S, qb = (ks + 1) * nchunks / S;
     for (int q = qa; q < qb; ++q) {
         const int p0 = (q / nchc) * PC, c0 = (q - (q / nchc) * nchc) * CCH;
-        const half8_t* ap = ap0 + (int64_t)((p0 * cin + c0) / 16) * 2 * KT * 64;
-        // a wave with no steps (NS < WK) still issues its prologue loads: clamp
-        // every step index into [s0, NS), never below its range (s0 < NS always)
-        auto load_a = [&](int s, half8_t (&dst)[2]) {
-            const int sc = max(s0, min(s, s1 - 1));
-            const int g = sc / KT, k = sc - (sc / KT) * KT;
-            const half8_t* pp = ap + ((int64_t)(2 * g) * KT + k) * 64;
-            dst[0] = pp[0];
-            if constexpr (P == 1) dst[1] = pp[KT * 64];
+        // byte offset of the chunk's group g0 in the m-tile's panel
+        const unsigned abase = (unsigned)(((p0 * cin + c0) / 16 + g0) * 2 * KT) * 1024u;
+        auto load_a = [&](int i, half8_t (&dst)[2]) {   // i: uniform step index
+            const unsigned so = abase + (unsigned)(2 * (i / KT) * KT + i % KT) * 1024u;
+            dst[0] = __builtin_bit_cast(half8_t, __builtin_amdgcn_raw_buffer_load_b128(ars, avoff, so, 0));
+            if constexpr (P == 1)
+                dst[1] = __builtin_bit_cast(half8_t,
+                                            __builtin_amdgcn_raw_buffer_load_b128(ars, avoff, so + KT * 1024u, 0));
         };
+        if (n > 0) {   // uniform; clamped (unconditional) loads keep the vmcnt counting exact
 #pragma unroll
-        for (int j = 0; j < D - 1; ++j) load_a(s0 + j, ra[j]);
+            for (int j = 0; j < DR - 1; ++j) load_a(min(j, n - 1), ra[j]);
+        }
+        OU_CSTAMP(0);
         if (q > qa) __syncthreads();   // every wave is done reading the previous chunk
         // ---- stage the chunk: item = (8 channels c0 + 8 g .., sample j of the
         // chunk's window): consecutive lanes load consecutive samples of PC
@@ -890,38 +914,51 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
                 }
             }
         }
+        OU_CSTAMP(1);
         __syncthreads();
+        OU_CSTAMP(2);
 
-        // branch-free blocks of D steps: steps past s1 (the last block's padding)
-        // multiply a zeroed A fragment, so the scheduler can hoist every LDS read
-        const int nblk = (diag & 2) ? 0 : (s1 - s0 + D - 1) / D;
-        for (int blk = 0; blk < nblk; ++blk) {
-            const int s = s0 + blk * D;
+        // step j of a block: B fragments from LDS, three MFMAs (split-f16)
+        auto step = [&](int gj, int j) {
+            const int k = j % KT;   // static: blocks start at multiples of KT
+            half8_t bq[NR], bl[NR];
 #pragma unroll
-            for (int j = 0; j < D; ++j) {
-                load_a(s + j + D - 1, ra[(j + D - 1) % D]);
-                const int st = max(s0, min(s + j, s1 - 1));
-                const bool live = s + j < s1;
-                const int g = st / KT, k = st - (st / KT) * KT;
-                half8_t a0 = ra[j][0], a1 = ra[j][1];
-                if (!live) a0 = half8_t{}, a1 = half8_t{};
-                half8_t bq[NR], bl[NR];
+            for (int nr = 0; nr < NR; ++nr) {
+                const _Float16* qq = xrow[nr][k] + 8 * gj;
+                bq[nr] = *(const half8_t*)qq;
+                if constexpr (P == 1) bl[nr] = *(const half8_t*)(qq + plane);
+            }
 #pragma unroll
-                for (int nr = 0; nr < NR; ++nr) {
-                    const _Float16* qq = xp + (nr * 32 + k) * SX + 8 * g;
-                    bq[nr] = *(const half8_t*)qq;
-                    if constexpr (P == 1) bl[nr] = *(const half8_t*)(qq + plane);
-                }
-#pragma unroll
-                for (int nr = 0; nr < NR; ++nr) {
-                    acc[0][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bq[nr], acc[0][nr], 0, 0, 0);
-                    if constexpr (P == 1) {
-                        accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bl[nr], accx[nr], 0, 0, 0);
-                        accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bq[nr], accx[nr], 0, 0, 0);
-                    }
+            for (int nr = 0; nr < NR; ++nr) {
+                acc[0][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[j][0], bq[nr], acc[0][nr], 0, 0, 0);
+                if constexpr (P == 1) {
+                    accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[j][0], bl[nr], accx[nr], 0, 0, 0);
+                    accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[j][1], bq[nr], accx[nr], 0, 0, 0);
                 }
             }
+        };
+        const int nn = (diag & 2) ? 0 : n;
+        // whole blocks: branch-free, every load unconditional (step index
+        // clamped to the last one: a few redundant loads at the end), so the
+        // compiler counts vmcnt exactly and waits only for the slot in use
+        int ib = 0;
+        for (; ib + DR <= nn; ib += DR) {
+            const int gb = ib / KT;
+#pragma unroll
+            for (int j = 0; j < DR; ++j) {
+                load_a(min(ib + j + DR - 1, nn - 1), ra[(j + DR - 1) % DR]);
+                step(gb + j / KT, j);
+            }
         }
+        // ragged last block (n % DR steps; none when DR divides n): its
+        // fragments are already in the ring
+        if (ib < nn) {
+            const int gb = ib / KT;
+#pragma unroll
+            for (int j = 0; j < DR - 1; ++j)
+                if (ib + j < nn) step(gb + j / KT, j);
+        }
+        OU_CSTAMP(3);
     }
     if (__any(ovf) && lane == 0 && d.status) atomicOr(d.status, 1);
     const float su = d.w_unscale, sx = su * (1.f / 2048.f);
@@ -942,6 +979,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
                 for (int r = 0; r < 16; ++r) red[((((wk - 1) * WM + wm) * NR + nr) * 16 + r) * 64 + lane] = acc[0][nr][r];
         }
         __syncthreads();
+        OU_CSTAMP(4);
         if (wk > 0) return;
         for (int j = 1; j < WK; ++j)
 #pragma unroll
@@ -958,7 +996,10 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
             for (int r = 0; r < 16; ++r) pw[(nr * 16 + r) * 64] = acc[0][nr][r];
         return;
     }
+    OU_CSTAMP(4);
     conv_epilogue<1, NR>(d, b, mtu, n0, acc, lane, bx + by + bz);
+    OU_CSTAMP(5);
+    OU_CSTAMP_SAVE;
 }
 
 // Second launch of a K-sliced register-streamed conv: one wave per m-tile of

@@ -193,7 +193,14 @@ def main():
             st = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8).astype(np.float64)
             st = st[st.sum(1) > 0]
             names = ("prologue", "load_issue", "mfma", "store", "barrier", "epilogue")
+            if (res[0][1] if a.tile is None else a.tile) & E.RS_BIT:
+                names = ("ring_issue", "staging", "barrier", "mfma", "reduce", "epilogue")
             mean = st.mean(0)
+            rt0, rt1 = st[:, 6], st[:, 7]
+            print(f"      realtime (us, 100 MHz): WG duration mean {(rt1 - rt0).mean() / 100:.2f} "
+                  f"min {(rt1 - rt0).min() / 100:.2f} max {(rt1 - rt0).max() / 100:.2f}; starts spread "
+                  f"{(rt0.max() - rt0.min()) / 100:.2f}, first start -> last end {(rt1.max() - rt0.min()) / 100:.2f}",
+                  flush=True)
             print(f"      stamps over {len(st)} WGs (cycles): " +
                   " ".join(f"{nm}={mean[i]:.0f}" for i, nm in enumerate(names)) +
                   f" total={mean[:6].sum():.0f} (min {st[:, :6].sum(1).min():.0f} max {st[:, :6].sum(1).max():.0f})",

@@ -1,20 +1,35 @@
 #!/usr/bin/env bash
-# GPU (round 4, call A): the new GPU tests, then the C2 profile (kernel trace +
-# PMC of this library) and the per-op PMC table of C2.
+# GPU (round 4, call A): targeted GPU tests (incl. every conv tile), the
+# register-streamed conv A/B (new scalar-indexed K loop vs the previous one),
+# C2 bench A/B, then the C2 profile (kernel trace + PMC of this library), the
+# per-op PMC table and the lane timeline of C2.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out; mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 TAG=${1:-r04a}
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu \
+V=$PWD/open_universe_amd/variants
+timeout -k 10 420 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+    tests/test_gpu_conv_tiles.py \
     "tests/test_gpu_parity.py::test_gru_ws_zeroed_short_launches_back_to_back" \
-    "tests/test_gpu_parity.py::test_gru_layer" \
-    "tests/test_gpu_parity_sizes.py::test_c3_real_shape_item0_vs_oracle" \
-    "tests/test_gpu_parity_sizes.py::test_full_width_pp24_enhance" \
-    "tests/test_gpu_audio.py::test_enhance_cli_outputs_independent_of_world_size" \
+    "tests/test_gpu_parity.py::test_same_conv_layer" "tests/test_gpu_parity.py::test_down_conv_layer" \
+    "tests/test_gpu_parity.py::test_up_conv_layer" \
+    "tests/test_gpu_parity_sizes.py::test_c2_size_enhance_vs_oracle" \
     > $O/tests_$TAG.log 2>&1 || { tail -30 $O/tests_$TAG.log; exit 1; }
 tail -3 $O/tests_$TAG.log
+for lib in new old; do
+  L=$PWD/open_universe_amd/libouhip.so; [ $lib = old ] && L=$V/libouhip_oldrk.so
+  OUHIP_LIB=$L timeout -k 10 200 python3 tools/conv_bench.py --layer L4k3,L4k5,GI,U3,L3k3,D3,D2,ST0 --reps 20 \
+      > $O/cb_${TAG}_$lib.txt 2>&1 || { tail -5 $O/cb_${TAG}_$lib.txt; exit 1; }
+done
+head -20 $O/cb_${TAG}_new.txt $O/cb_${TAG}_old.txt
+for lib in new old new; do
+  L=$PWD/open_universe_amd/libouhip.so; [ $lib = old ] && L=$V/libouhip_oldrk.so
+  OUHIP_LIB=$L timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-f32-pass --no-queued \
+      --traffic-json "" > $O/ab_${TAG}_$lib.json 2> $O/ab_${TAG}_$lib.err || { tail -5 $O/ab_${TAG}_$lib.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/ab_${TAG}_$lib.json')); print('$lib', d['value'], d['ms_per_step'], d['profile'])"
+done
+timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 --ops --out $O/cp_$TAG.json > $O/cp_$TAG.txt 2>&1 || { tail -20 $O/cp_$TAG.txt; exit 1; }
+head -70 $O/cp_$TAG.txt
 bash tools/gpu_profile.sh $TAG c2 || exit 1
 bash tools/gpu_level_pmc.sh ${TAG}_lv c2 || exit 1
-timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 --ops --out $O/cp_$TAG.json > $O/cp_$TAG.txt 2>&1 || { tail -20 $O/cp_$TAG.txt; exit 1; }
-head -60 $O/cp_$TAG.txt
