@@ -1545,7 +1545,7 @@ class Engine:
         bufs["TB"] = [new_act(B, self.c_dec[l].C, Ts[min(n_lvl - 1 - l, len(rates))], dev) for l in range(n_lvl)]
         return bufs
 
-    def rec_cond(self, prog, bufs, x: Act, need_aux=False, after_level=None, st_lane=None):
+    def rec_cond(self, prog, bufs, x: Act, need_aux=False, after_level=None, st_lane=None, enc_done=None):
         """ConditionerNetwork.forward (condition.py:346-377).  ``after_level(l,
         cond_l)`` runs right after decoder level l has produced its condition.
         With ``st_lane`` (recording on a side lane) the strided st_convs, which
@@ -1562,10 +1562,18 @@ class Engine:
         # residual), so with ``st_lane`` it is recorded there too: the
         # conditioner's encoder -- the first step's critical path -- starts
         # without waiting for it
-        mel_lane = st_lane if os.environ.get("OUHIP_MEL_LANE", "1") != "0" else None
+        # OUHIP_MEL_LANE: "1" (default) the st lane, "0" in line on the
+        # conditioner lane, "2" / "3" a side lane of its own (the st_convs then
+        # do not queue behind it)
+        ml = os.environ.get("OUHIP_MEL_LANE", "1")
+        mel_lane = None if ml == "0" or st_lane is None else (st_lane if ml == "1" else int(ml))
+        if mel_lane is not None and mel_lane not in (st_lane, 0):
+            ev_m = prog.signal()   # a side lane starts by waiting on the conditioner lane
         if mel_lane is not None:
             side = _LANE
             set_lane(prog, mel_lane)
+            if mel_lane not in (st_lane, 0):
+                prog.wait(ev_m)
         prog.label = "cond mel"
         prog.add(L.OP_CONV, conv_desc(self.c_stft, x, bufs["SPEC"], n_frames=U))
         pa = L.PowerArgs(x=bufs["SPEC"].ptr, y=bufs["POW"].ptr, batch=B, nf=self.mel_nfreq, frames=U)
@@ -1576,7 +1584,10 @@ class Engine:
         prog.add(L.OP_INV_RMS, ra)
         prog.add(L.OP_CONV, conv_desc(self.c_melconv, bufs["MEL"], bufs["M0"], in_scale=bufs["INV"].data_ptr()))
         rec_block(prog, self.c_melblock, bufs["M0"], bufs["XMEL"], bufs["MA"], bufs["MB"])
+        ev_mel = None
         if mel_lane is not None:
+            if mel_lane not in (st_lane, 0):
+                ev_mel = prog.signal()   # the level-0 st_conv reads XMEL
             set_lane(prog, side)
         # encoder (condition.py:189-220)
         prog.label = "cond enc L0"
@@ -1595,6 +1606,8 @@ class Engine:
                         ev = prog.signal()
                         set_lane(prog, st_lane)
                         prog.wait(ev)
+                        if nsum == 0 and ev_mel is not None:
+                            prog.wait(ev_mel)
                     prog.label = f"cond st{i}"
                     prog.add(L.OP_CONV, conv_desc(self.c_st[i], bufs[f"V{i}"], bufs["SUM"],
                                                   n_frames=U, res1=prev, s1=1.0))
@@ -1617,6 +1630,8 @@ class Engine:
             raise NotImplementedError("conditioner without extra_conv_block")
         prog.label = "cond cb1"
         rec_block(prog, self.c_cb1, bufs["OUT"], bufs["CB1"], bufs["LA"], bufs["LB"])
+        if enc_done is not None:
+            enc_done()
         prog.label = "cond gru1"
         rec_gru(prog, self.c_gru, 0, bufs["CB1"], bufs["GI"], bufs["G1"], bufs["gran"], self.status)
         res = bufs["CB1"] if self.c_gru_res else None

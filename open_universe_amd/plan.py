@@ -11,6 +11,7 @@ replayed as a single hipGraph.  All arithmetic on the sampler's scalars
 float32 exactly as the reference's tensor ops round them.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -193,8 +194,16 @@ class EnhancePlan(_PlanBase):
                 p.label = f"cond sc{l}"
                 p.add(L.OP_CONV, E.conv_desc(eng.s_sc[l], cond, self.SC[l]))
                 ev_cond[l] = p.signal()
+        # OUHIP_SCORE_AFTER_CENC=1: the first score pass starts once the
+        # conditioner's encoder is done (its GRU then runs beside the score
+        # encoder), so the conditioner's encoder -- the first step's critical
+        # path -- does not share the chip with the score encoder
+        ev_cenc = []
+        enc_done = None
+        if self.overlap and os.environ.get("OUHIP_SCORE_AFTER_CENC", "0") == "1":
+            enc_done = lambda: ev_cenc.append(p.signal())
         conds, yaux = eng.rec_cond(p, cb, self.XN, need_aux=use_aux_signal or warm_start is not None,
-                                   after_level=after_level,
+                                   after_level=after_level, enc_done=enc_done,
                                    st_lane=0 if (self.overlap and st_lane and E.st_lane_enabled()) else None)
         if use_aux_signal or warm_start is not None:
             self.AUXT = new_act(B, yaux.C, Tp, dev)
@@ -208,6 +217,8 @@ class EnhancePlan(_PlanBase):
         else:
             if self.overlap:
                 E.set_lane(p, 0)
+                for ev in ev_cenc:
+                    p.wait(ev)
             else:
                 self.SC = eng.alloc_sc(B, Tp)
                 eng.rec_sc(p, conds, self.SC)

@@ -60,3 +60,25 @@ def test_enhance_plan_records_onto_an_arena():
     lo, hi = ar.buf.data_ptr(), ar.buf.data_ptr() + ar.nbytes
     for t in (plan.MIX, plan.NZ, plan.OUT, plan.X.t, plan.sb["E0"].t, plan.cb["SPEC"].t):
         assert lo <= t.data_ptr() < hi
+
+
+@pytest.mark.parametrize("env", [{}, {"OUHIP_MEL_LANE": "2"}, {"OUHIP_MEL_LANE": "0"},
+                                 {"OUHIP_SCORE_AFTER_CENC": "1"},
+                                 {"OUHIP_MEL_LANE": "2", "OUHIP_SCORE_AFTER_CENC": "1"}])
+def test_lane_schedule_variants_validate(monkeypatch, env):
+    """Every lane schedule of the first step (mel branch in line, on the st
+    lane or a lane of its own; the score pass started after the
+    conditioner's encoder) records a program whose lane structure
+    ou_program_validate accepts (host-only: joins, signal-before-wait, no
+    side-lane wait cycles), with the same ops as the default schedule."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    d = load_golden("pp16_c4")
+    eng = Engine(get_config("pp16", 4), golden_state_dict(d), "cpu", _record_only=True)
+    plan = EnhancePlan(eng, 1, 3000, 8, 1.3)
+    plan.prog.validate()
+    kinds = [k for k in plan.prog.op_kinds() if k not in (L.OP_LANE, L.OP_SIGNAL, L.OP_WAIT)]
+    for k in env:
+        monkeypatch.delenv(k)
+    ref = EnhancePlan(eng, 1, 3000, 8, 1.3)
+    assert kinds == [k for k in ref.prog.op_kinds() if k not in (L.OP_LANE, L.OP_SIGNAL, L.OP_WAIT)]

@@ -23,13 +23,19 @@ for lib in new old; do
       > $O/cb_${TAG}_$lib.txt 2>&1 || { tail -5 $O/cb_${TAG}_$lib.txt; exit 1; }
 done
 head -20 $O/cb_${TAG}_new.txt $O/cb_${TAG}_old.txt
-for lib in new old new; do
-  L=$PWD/open_universe_amd/libouhip.so; [ $lib = old ] && L=$V/libouhip_oldrk.so
-  OUHIP_LIB=$L timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-f32-pass --no-queued \
-      --traffic-json "" > $O/ab_${TAG}_$lib.json 2> $O/ab_${TAG}_$lib.err || { tail -5 $O/ab_${TAG}_$lib.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/ab_${TAG}_$lib.json')); print('$lib', d['value'], d['ms_per_step'], d['profile'])"
-done
+ab() {   # ab NAME LIB [ENV...]
+  local name=$1 lib=$2; shift 2
+  env "$@" OUHIP_LIB=$lib OUHIP_TUNE_CACHE=$O/tune_${TAG}_$(basename $lib .so).json timeout -k 10 200 \
+      python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-f32-pass --no-queued \
+      --traffic-json "" > $O/ab_${TAG}_$name.json 2> $O/ab_${TAG}_$name.err || { tail -5 $O/ab_${TAG}_$name.err; return 1; }
+  python3 -c "import json; d=json.load(open('$O/ab_${TAG}_$name.json')); print('$name', d['value'], d['ms_per_step'], d['profile'])"
+}
+NEW=$PWD/open_universe_amd/libouhip.so
+ab new $NEW && ab old $V/libouhip_oldrk.so && ab new2 $NEW && ab mel2 $NEW OUHIP_MEL_LANE=2 &&
+ab after $NEW OUHIP_SCORE_AFTER_CENC=1 && ab both $NEW OUHIP_MEL_LANE=2 OUHIP_SCORE_AFTER_CENC=1 && ab new3 $NEW || exit 1
 timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 --ops --out $O/cp_$TAG.json > $O/cp_$TAG.txt 2>&1 || { tail -20 $O/cp_$TAG.txt; exit 1; }
 head -70 $O/cp_$TAG.txt
+OUHIP_MEL_LANE=2 OUHIP_SCORE_AFTER_CENC=1 timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 --ops \
+    --out $O/cp_${TAG}_both.json > $O/cp_${TAG}_both.txt 2>&1 || { tail -20 $O/cp_${TAG}_both.txt; exit 1; }
+head -50 $O/cp_${TAG}_both.txt
 bash tools/gpu_profile.sh $TAG c2 || exit 1
-bash tools/gpu_level_pmc.sh ${TAG}_lv c2 || exit 1
