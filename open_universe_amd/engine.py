@@ -1558,14 +1558,14 @@ class Engine:
         n_lvl = len(self.c_enc)
         B, U = x.B, bufs["U"]
         # MelAdapter (condition.py:85-114): |STFT|^2 -> mel -> global norm -> conv -> ConvBlock.
-        # Its output is first read by the level-0 st_conv (as that conv's
-        # residual), so with ``st_lane`` it is recorded there too: the
-        # conditioner's encoder -- the first step's critical path -- starts
-        # without waiting for it
-        # OUHIP_MEL_LANE: "1" (default) the st lane, "0" in line on the
-        # conditioner lane, "2" / "3" a side lane of its own (the st_convs then
-        # do not queue behind it)
-        ml = os.environ.get("OUHIP_MEL_LANE", "1")
+        # Its output is read only by the last st_conv (as a residual), so with
+        # ``st_lane`` it runs on a side lane of its own: neither the
+        # conditioner's encoder -- the first step's critical path -- nor the
+        # earlier st_convs wait for it
+        # OUHIP_MEL_LANE: "2" (default) / "3" a side lane of its own, so the
+        # st_convs do not queue behind it; "1" the st lane; "0" in line on the
+        # conditioner lane
+        ml = os.environ.get("OUHIP_MEL_LANE", "2")
         mel_lane = None if ml == "0" or st_lane is None else (st_lane if ml == "1" else int(ml))
         if mel_lane is not None and mel_lane not in (st_lane, 0):
             ev_m = prog.signal()   # a side lane starts by waiting on the conditioner lane
@@ -1587,7 +1587,7 @@ class Engine:
         ev_mel = None
         if mel_lane is not None:
             if mel_lane not in (st_lane, 0):
-                ev_mel = prog.signal()   # the level-0 st_conv reads XMEL
+                ev_mel = prog.signal()   # the last st_conv adds XMEL
             set_lane(prog, side)
         # encoder (condition.py:189-220)
         prog.label = "cond enc L0"
@@ -1600,17 +1600,28 @@ class Engine:
                 rec_block(prog, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
                           e_out=bufs[f"E{i+1}"])
                 if i < nr - 1:
-                    prev = bufs["XMEL"] if nsum == 0 else bufs["SUM"]
+                    # SUM = x_mel + st_0 + st_1 + ... (condition.py:208-215),
+                    # accumulated in the st_convs' epilogues.  The mel branch
+                    # is added by the LAST st_conv, so the earlier ones run as
+                    # soon as their encoder level is done instead of queueing
+                    # behind the mel front end (a reassociated fp32 sum)
+                    last_st = i == nr - 2
+                    if nr - 1 == 1:
+                        res_a, res_b = bufs["XMEL"], None
+                    elif nsum == 0:
+                        res_a, res_b = None, None
+                    else:
+                        res_a, res_b = bufs["SUM"], (bufs["XMEL"] if last_st else None)
                     if st_lane is not None:
                         side = _LANE
                         ev = prog.signal()
                         set_lane(prog, st_lane)
                         prog.wait(ev)
-                        if nsum == 0 and ev_mel is not None:
+                        if ev_mel is not None and (res_a is bufs["XMEL"] or res_b is not None):
                             prog.wait(ev_mel)
                     prog.label = f"cond st{i}"
                     prog.add(L.OP_CONV, conv_desc(self.c_st[i], bufs[f"V{i}"], bufs["SUM"],
-                                                  n_frames=U, res1=prev, s1=1.0))
+                                                  n_frames=U, res1=res_a, s1=1.0, res2=res_b, s2=1.0))
                     prog.label = f"cond enc L{i}"
                     if st_lane is not None:
                         set_lane(prog, side)

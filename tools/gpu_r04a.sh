@@ -33,9 +33,11 @@ ab() {   # ab NAME LIB [ENV...]
 NEW=$PWD/open_universe_amd/libouhip.so
 ab new $NEW && ab old $V/libouhip_oldrk.so && ab new2 $NEW && ab mel2 $NEW OUHIP_MEL_LANE=2 &&
 ab after $NEW OUHIP_SCORE_AFTER_CENC=1 && ab both $NEW OUHIP_MEL_LANE=2 OUHIP_SCORE_AFTER_CENC=1 && ab new3 $NEW || exit 1
+export OUHIP_TUNE_CACHE=$O/tune_${TAG}_libouhip.json
 timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 --ops --out $O/cp_$TAG.json > $O/cp_$TAG.txt 2>&1 || { tail -20 $O/cp_$TAG.txt; exit 1; }
 head -70 $O/cp_$TAG.txt
 OUHIP_MEL_LANE=2 OUHIP_SCORE_AFTER_CENC=1 timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 --ops \
     --out $O/cp_${TAG}_both.json > $O/cp_${TAG}_both.txt 2>&1 || { tail -20 $O/cp_${TAG}_both.txt; exit 1; }
 head -50 $O/cp_${TAG}_both.txt
+unset OUHIP_TUNE_CACHE
 bash tools/gpu_profile.sh $TAG c2 || exit 1
