@@ -176,6 +176,241 @@ __device__ __forceinline__ void ou_row_map(int m, int rout, int cout, int& co, i
 // bias, zero-fill past valid_len, residual 1, FiLM, residual 2, the rout
 // pixel shuffle and the store.  mtb: the wave's first 32-row m-tile; ub: the
 // first output frame of its columns; slot: amax_out slot seed.
+//
+// Two phases: conv_epi_load issues every load the tile's epilogue needs (bias,
+// FiLM, both residuals) into registers, conv_epi_store finishes and stores.
+// Branch-free: every out-of-range element gets a sentinel offset, so its
+// buffer load returns 0 and its buffer store is dropped.  A kernel with work
+// between the two (conv_rkernel's K-split reduction through LDS) issues the
+// loads first, so their latency overlaps that work; conv_epilogue runs both.
+struct EpiCtx {
+    int M, rout, cout, ylen;
+    __amdgpu_buffer_rsrc_t ys, r1s, r2s, bs, fs;
+    bool has_r1, has_r2, has_fm, vec;
+    float s1e, s2e, fadd;
+};
+
+__device__ __forceinline__ EpiCtx epi_ctx(const ou_conv_desc& d, int b)
+{
+    EpiCtx c;
+    c.M = d.m;
+    c.rout = d.rout < 0 ? -d.rout : d.rout;   // output samples per frame
+    c.cout = c.M / c.rout;
+    const int yrows = c.cout;
+    c.ylen = d.out_len;
+    c.ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)yrows * d.y_cstride * 4);
+    c.r1s = ou_rsrc(d.res1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y, d.res1 ? (int64_t)yrows * d.r1_cstride * 4 : 0);
+    c.r2s = ou_rsrc(d.res2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y, d.res2 ? (int64_t)yrows * d.r2_cstride * 4 : 0);
+    // absent operands get zero-size resources (their loads return 0): every
+    // load is unconditional -- a per-element `ptr ? load : default` makes hipcc
+    // branch around each load and drain vmcnt(0) per element
+    c.has_r1 = d.res1 != nullptr, c.has_r2 = d.res2 != nullptr, c.has_fm = d.film != nullptr;
+    // branch-free epilogue: an absent operand loads 0 and meets a unit scale
+    c.s1e = c.has_r1 ? d.s1 : 1.f, c.s2e = c.has_r2 ? d.s2 : 1.f, c.fadd = c.has_fm ? 0.f : 1.f;
+    c.bs = ou_rsrc(d.bias, d.bias ? (int64_t)c.cout * 4 : 0);
+    c.fs = ou_rsrc(c.has_fm ? d.film + (int64_t)b * d.film_bstride : d.y, c.has_fm ? (int64_t)c.cout * 8 : 0);
+    // vector path: channel-major rows at rout 2 / 4 with every row start
+    // (4 rout)-byte aligned (uniform over the launch)
+    const int rout = c.rout;
+    auto al = [&](const float* p, int64_t bst, int64_t cst) {
+        return !p || (((uintptr_t)p % (4 * rout)) == 0 && bst % rout == 0 && cst % rout == 0);
+    };
+    c.vec = d.rout < 0 && (rout == 2 || rout == 4) && c.M % 4 == 0 && al(d.y, d.y_bstride, d.y_cstride) &&
+            al(d.res1, d.r1_bstride, d.r1_cstride) && al(d.res2, d.r2_bstride, d.r2_cstride);
+    return c;
+}
+
+template <int MR, int NR>
+struct EpiPre {
+    float bias[MR][16], fa[MR][16], fb[MR][16];
+    float v1[MR][NR][16], v2[MR][NR][16];
+    bool vec[MR][NR];   // this (m-tile, frame tile) takes the vector path
+};
+
+template <int MR, int NR>
+__device__ __forceinline__ void conv_epi_load(const ou_conv_desc& d, const EpiCtx& c, int mtb, int ub, int lane,
+                                              EpiPre<MR, NR>& e)
+{
+    const int h = lane >> 5, l32 = lane & 31;
+    const int M = c.M, rout = c.rout, cout = c.cout, ylen = c.ylen;
+#pragma unroll
+    for (int mr = 0; mr < MR; ++mr) {
+        const int mt = mtb + mr;
+        int co[16], ph[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = min(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
+            ou_row_map(m, d.rout, cout, co[r], ph[r]);
+        }
+        // absent operands: one uniform branch around the whole group of loads
+        // (never a per-element select between a load and a default)
+        if (d.bias) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) e.bias[mr][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.bs, co[r] * 4, 0, 0));
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) e.bias[mr][r] = 0.f;
+        }
+        if (c.has_fm) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                e.fa[mr][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.fs, co[r] * 4, 0, 0));
+                e.fb[mr][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.fs, (cout + co[r]) * 4, 0, 0));
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) e.fa[mr][r] = 0.f, e.fb[mr][r] = 0.f;
+        }
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+            const int u = ub + nr * 32 + l32;
+            e.vec[mr][nr] = false;
+            if (c.vec) {
+                // channel-major rows at rout 4 / 2: register group g (rows
+                // 8 g + 4 h + j, j < 4) holds samples u rout .. u rout + rout - 1
+                // of 4 / rout channels -- one 16-B or two 8-B accesses per
+                // group and tensor, consecutive lanes on consecutive frames
+                const int t0 = u * rout;
+                const bool uok = u < d.f0 + d.n_frames && t0 < ylen;
+                if (__all(!uok || t0 + rout <= ylen)) {
+                    e.vec[mr][nr] = true;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const bool ok = uok && mt * 32 + 8 * g + 4 * h < M;
+#pragma unroll
+                        for (int sv = 0; sv < 4 / 4 + (rout == 2); ++sv) {
+                            const int cc = co[4 * g + 2 * sv];
+                            const int o1 = ok ? (cc * (int)d.r1_cstride + t0) * 4 : kSentinel;
+                            const int o2 = ok ? (cc * (int)d.r2_cstride + t0) * 4 : kSentinel;
+                            if (rout == 4) {
+                                const auto a1 = __builtin_amdgcn_raw_buffer_load_b128(c.r1s, o1, 0, 0);
+                                const auto a2 = __builtin_amdgcn_raw_buffer_load_b128(c.r2s, o2, 0, 0);
+#pragma unroll
+                                for (int j = 0; j < 4; ++j)
+                                    e.v1[mr][nr][4 * g + j] = __uint_as_float(a1[j]), e.v2[mr][nr][4 * g + j] = __uint_as_float(a2[j]);
+                            } else {
+                                const auto a1 = __builtin_amdgcn_raw_buffer_load_b64(c.r1s, o1, 0, 0);
+                                const auto a2 = __builtin_amdgcn_raw_buffer_load_b64(c.r2s, o2, 0, 0);
+#pragma unroll
+                                for (int j = 0; j < 2; ++j)
+                                    e.v1[mr][nr][4 * g + 2 * sv + j] = __uint_as_float(a1[j]),
+                                    e.v2[mr][nr][4 * g + 2 * sv + j] = __uint_as_float(a2[j]);
+                            }
+                        }
+                    }
+                    continue;
+                }
+            }
+            int off[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int t = u * rout + ph[r];
+                const bool ok = m < M && u < d.f0 + d.n_frames && t < ylen;
+                off[r] = ok ? t : -1;   // column; row offsets differ per tensor
+            }
+            if (c.has_r1) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    e.v1[mr][nr][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        c.r1s, off[r] >= 0 ? (co[r] * (int)d.r1_cstride + off[r]) * 4 : kSentinel, 0, 0));
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) e.v1[mr][nr][r] = 0.f;
+            }
+            if (c.has_r2) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    e.v2[mr][nr][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        c.r2s, off[r] >= 0 ? (co[r] * (int)d.r2_cstride + off[r]) * 4 : kSentinel, 0, 0));
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) e.v2[mr][nr][r] = 0.f;
+            }
+        }
+    }
+}
+
+template <int MR, int NR>
+__device__ __forceinline__ void conv_epi_store(const ou_conv_desc& d, const EpiCtx& c, int mtb, int ub,
+                                               floatx16 (&acc)[MR][NR], const EpiPre<MR, NR>& e, int lane, int slot)
+{
+    const int h = lane >> 5, l32 = lane & 31;
+    const int M = c.M, rout = c.rout, cout = c.cout, ylen = c.ylen;
+    float ymax = 0.f;   // max |stored y| of this wave (d.amax_out)
+#pragma unroll
+    for (int mr = 0; mr < MR; ++mr) {
+        const int mt = mtb + mr;
+        int co[16], ph[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = min(mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, M - 1);
+            ou_row_map(m, d.rout, cout, co[r], ph[r]);
+        }
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+            const int u = ub + nr * 32 + l32;
+            if (e.vec[mr][nr]) {
+                const int t0 = u * rout;
+                const bool uok = u < d.f0 + d.n_frames && t0 < ylen;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const bool ok = uok && mt * 32 + 8 * g + 4 * h < M;
+                    float val[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int r = 4 * g + j;
+                        float v = acc[mr][nr][r] + e.bias[mr][r];
+                        if (t0 + ph[r] >= d.valid_len) v = 0.f;
+                        v = (v + e.v1[mr][nr][r]) * c.s1e;
+                        v = (e.fa[mr][r] + c.fadd) * v + e.fb[mr][r];
+                        v = (v + e.v2[mr][nr][r]) * c.s2e;
+                        ymax = fmaxf(ymax, ok ? fabsf(v) : 0.f);
+                        val[j] = v;
+                    }
+#pragma unroll
+                    for (int sv = 0; sv < 4 / 4 + (rout == 2); ++sv) {
+                        const int cc = co[4 * g + 2 * sv];
+                        const int oy = ok ? (cc * (int)d.y_cstride + t0) * 4 : kSentinel;
+                        if (rout == 4)
+                            __builtin_amdgcn_raw_buffer_store_b128(
+                                ou_u32x4{__float_as_uint(val[0]), __float_as_uint(val[1]), __float_as_uint(val[2]),
+                                         __float_as_uint(val[3])},
+                                c.ys, oy, 0, 0);
+                        else
+                            __builtin_amdgcn_raw_buffer_store_b64(
+                                ou_u32x2{__float_as_uint(val[2 * sv]), __float_as_uint(val[2 * sv + 1])}, c.ys, oy, 0, 0);
+                    }
+                }
+                continue;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int t = u * rout + ph[r];
+                const bool ok = m < M && u < d.f0 + d.n_frames && t < ylen;
+                float v = acc[mr][nr][r] + e.bias[mr][r];
+                if ((ok ? t : -1) >= d.valid_len) v = 0.f;
+                v = (v + e.v1[mr][nr][r]) * c.s1e;
+                v = (e.fa[mr][r] + c.fadd) * v + e.fb[mr][r];
+                v = (v + e.v2[mr][nr][r]) * c.s2e;
+                ymax = fmaxf(ymax, ok ? fabsf(v) : 0.f);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), c.ys,
+                                                      ok ? (co[r] * (int)d.y_cstride + t) * 4 : kSentinel, 0, 0);
+            }
+        }
+    }
+    if (d.amax_out) {   // wave max, then one atomic per wave into 64 spread slots
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) ymax = fmaxf(ymax, __shfl_xor(ymax, o));
+        if (lane == 0)
+            atomicMax((unsigned int*)d.amax_out + (slot & 63), __float_as_uint(ymax));
+    }
+}
+
+// The one-phase epilogue of the chunked / persistent kernels: per m-tile
+// and frame tile, its loads then its stores (live ranges stay one tile's
+// worth -- those kernels hold MR x NR tiles).
 template <int MR, int NR>
 __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int mtb, int ub,
                                               floatx16 (&acc)[MR][NR], int lane, int slot)
@@ -834,8 +1069,9 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     const __amdgpu_buffer_rsrc_t ars = ou_rsrc((const char*)d.w + (int64_t)mt * a_mt_stride * 4, a_mt_stride * 4);
     const unsigned avoff = (unsigned)lane * 16u;
     half8_t ra[DR][2];
-    const float* xb = d.x + (int64_t)b * d.x_bstride;
     const int64_t xc = d.x_cstride;
+    // the batch item's input (cin rows of x_cstride floats)
+    const __amdgpu_buffer_rsrc_t xrs = ou_rsrc(d.x + (int64_t)b * d.x_bstride, (int64_t)cin * xc * 4);
     const float scale = d.in_scale ? d.in_scale[b] : 1.f, slope = d.slope;
     constexpr float xsc = 1.f / (1 << kSplitShift);
     const int in_len = d.in_len;
@@ -869,33 +1105,40 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
         // ---- stage the chunk: item = (8 channels c0 + 8 g .., sample j of the
         // chunk's window): consecutive lanes load consecutive samples of PC
         // phases (the whole frame when PC = R); sample j is frame j / PC, phase
-        // p0 + j % PC, i.e. chunk K channels (j % PC) cin + 8 g .. + 7 of row j / PC
+        // p0 + j % PC, i.e. chunk K channels (j % PC) cin + 8 g .. + 7 of row j / PC.
+        // Buffer loads at one per-item voffset (the 8 channels are scalar
+        // soffsets i * xc; a sample outside [0, in_len) gets the sentinel
+        // voffset and loads 0), items advanced incrementally (no per-item
+        // integer division), PC > 1 frames by a float reciprocal (exact for
+        // the sample counts a window has), packed f16 conversion.
         const int t0 = (n0 - d.pad) * RF + d.shift + p0;   // first sample of frame 0, phase p0
-        // up to kStageItems items per thread in flight at once
         constexpr int IPT = kStageItems;
+        const int dq = 256 / WS, dr = 256 - dq * WS;          // item += 256: g += dq, sm += dr (carry)
+        int g_it = tid / WS, sm_it = tid - g_it * WS;
+        const float rpc = 1.f / (float)PC;
+        const int xoff0 = c0 * (int)xc * 4;
         for (int base = 0; base < NI; base += IPT * 256) {
             float v[IPT][8];
-#pragma unroll
-            for (int it = 0; it < IPT; ++it) {
-                const int item = min(base + tid + 256 * it, NI - 1);
-                const int g = item / WS, sm = item - g * WS;
-                const int w = sm / PC, pl = sm - w * PC;
-                const int t = t0 + w * RF + pl;
-                const int tc = min(max(t, 0), in_len - 1);
-                const float* src = xb + (int64_t)(c0 + 8 * g) * xc + tc;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) v[it][i] = (diag & 1) ? 0.f : src[i * xc];
-                if (t != tc) {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) v[it][i] = 0.f;
-                }
-            }
+            int dsto[IPT];
 #pragma unroll
             for (int it = 0; it < IPT; ++it) {
                 const int item = base + tid + 256 * it;
-                if (item >= NI) break;
-                const int g = item / WS, sm = item - g * WS;
-                const int w = sm / PC, pl = sm - w * PC;
+                const int g = g_it, sm = sm_it;
+                sm_it += dr, g_it += dq;
+                if (sm_it >= WS) sm_it -= WS, ++g_it;
+                const int w = PC == 1 ? sm : (int)(((float)sm + 0.5f) * rpc);
+                const int pl = sm - w * PC;
+                const int t = t0 + __mul24(w, RF) + pl;
+                const bool ok = item < NI && (unsigned)t < (unsigned)in_len && !(diag & 1);
+                const int vo = ok ? xoff0 + (__mul24(8 * g, (int)xc) + t) * 4 : kSentinel;   // 24-bit products: full rate
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    v[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, vo, i * (int)xc * 4, 0));
+                dsto[it] = item < NI ? __mul24(w, SX) + ((__mul24(pl, cin) + 8 * g) >> 1) : -1;
+            }
+#pragma unroll
+            for (int it = 0; it < IPT; ++it) {
+                if (dsto[it] < 0) break;   // items run in order: the rest are past NI too
                 float x[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
@@ -905,7 +1148,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
                 half4_t he, le, ho, lo;
                 split4r<P>(x[0], x[2], x[4], x[6], he, le, ovf);
                 split4r<P>(x[1], x[3], x[5], x[7], ho, lo, ovf);
-                _Float16* dst = xs + w * SX + (pl * cin + 8 * g) / 2;
+                _Float16* dst = xs + dsto[it];
                 *(half4_t*)dst = he;
                 *(half4_t*)(dst + HALF) = ho;
                 if constexpr (P == 1) {
@@ -968,6 +1211,11 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
         for (int r = 0; r < 16; ++r)
             acc[0][nr][r] = P == 1 ? fmaf(accx[nr][r], sx, acc[0][nr][r] * su) : acc[0][nr][r] * su;
 
+    // the epilogue's loads (bias, FiLM, residuals) go out before the K-split
+    // reduction, so their latency overlaps it (wave wk = 0 finishes the tile)
+    const EpiCtx ec = epi_ctx(d, b);
+    EpiPre<1, NR> ep;
+    if (S == 1 && wk == 0) conv_epi_load<1, NR>(d, ec, mtu, n0, lane, ep);
     // ---- K-split reduction in wave order (deterministic)
     if constexpr (WK > 1) {
         float* red = (float*)lds4;
@@ -997,7 +1245,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
         return;
     }
     OU_CSTAMP(4);
-    conv_epilogue<1, NR>(d, b, mtu, n0, acc, lane, bx + by + bz);
+    conv_epi_store<1, NR>(d, ec, mtu, n0, acc, ep, lane, bx + by + bz);
     OU_CSTAMP(5);
     OU_CSTAMP_SAVE;
 }

@@ -44,6 +44,12 @@ struct float4 {
 };
 inline float4 make_float4(float a, float b, float c, float d) { return {a, b, c, d}; }
 // IEEE round-to-nearest arithmetic (the host's default mode)
+// v_mul_i32_i24: signed 24-bit operands, low 32 bits of the product
+inline int __mul24(int a, int b)
+{
+    const long long sa = (long long)(a << 8) >> 8, sb = (long long)(b << 8) >> 8;
+    return (int)(sa * sb);
+}
 inline float __fadd_rn(float a, float b) { return a + b; }
 inline float __fsub_rn(float a, float b) { return a - b; }
 inline float __fmul_rn(float a, float b) { return a * b; }

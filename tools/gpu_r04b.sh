@@ -24,6 +24,16 @@ cd $GRAFT_REPO_ROOT
 python3 tools/pmc_avg.py "$(find $O/cpmc1_$TAG -name '*counter_collection.csv' | head -n1)" conv_rkernel > $O/cpmc_$TAG.txt 2>&1
 python3 tools/pmc_avg.py "$(find $O/cpmc2_$TAG -name '*counter_collection.csv' | head -n1)" conv_rkernel >> $O/cpmc_$TAG.txt 2>&1
 cat $O/cpmc_$TAG.txt
+# first-step schedule: mel on its own lane + reassociated st sum (default) vs mel on the st lane
+for v in base:OUHIP_MEL_LANE=2 st:OUHIP_MEL_LANE=1 base2:OUHIP_MEL_LANE=2; do
+  n=${v%%:*}; e=${v#*:}
+  env $e OUHIP_TUNE_CACHE=$O/tune_${TAG}_c2.json timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline \
+      --no-f32-pass --no-queued --traffic-json "" > $O/ab_${TAG}_$n.json 2> $O/ab_${TAG}_$n.err || { tail -5 $O/ab_${TAG}_$n.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/ab_${TAG}_$n.json')); print('$n', d['value'], d['ms_per_step'], d['profile'])"
+done
+OUHIP_TUNE_CACHE=$O/tune_${TAG}_c2.json timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 --ops \
+    --out $O/cp_$TAG.json > $O/cp_$TAG.txt 2>&1 || { tail -20 $O/cp_$TAG.txt; exit 1; }
+head -45 $O/cp_$TAG.txt
 # C4 profile (kernel trace + PMC of this library) and per-op table
 bash tools/gpu_profile.sh ${TAG}_c4 c4 --steps 4 --warmup 1 --no-f32-pass --no-queued || exit 1
 bash tools/gpu_level_pmc.sh ${TAG}_c4lv c4 || exit 1
