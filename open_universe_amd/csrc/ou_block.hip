@@ -437,6 +437,7 @@ template <int C, int NT, int P, int EPI, int R = 1, int KF = 1>
 __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_kernel(ou_block_desc d)
 {
     using K = BCfg<C, NT, P>;
+    ou_kernarg_prefetch8();
     constexpr int MR = K::MR, NR = K::NR, NF = K::NF, SX = K::SX;
     constexpr int OFF = block_off<EPI, R, KF>();   // conv3 starts OFF frames before t0
     constexpr int F = block_f<C, NT, P, EPI, R, KF>();

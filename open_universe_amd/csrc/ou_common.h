@@ -78,6 +78,44 @@ typedef unsigned ou_ldsa_t;
 #define OU_LDS_ADDR(p) __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(const void*)(p))
 #define OU_GLDS4(src, dst) ou_glds4((const void*)(src), (const void*)(dst))
 #define OU_GLDS16(src, dst) ou_glds16((const void*)(src), (const void*)(dst))
+// Kernel-argument prefetch: one scalar load per 64-B line of the kernarg
+// segment (the explicit descriptor and the hidden block counts after it), all
+// issued before one wait.  The compiler loads the descriptor's fields where
+// they are first used, behind branches and arithmetic, so a kernel's start
+// otherwise pays a chain of dependent scalar-cache misses on the same few
+// lines; afterwards every field load hits the scalar cache.  Reads only.
+__device__ __forceinline__ void ou_kernarg_prefetch6()
+{
+    const auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+    unsigned a, b, c, d, e, f;
+    asm volatile("s_load_dword %0, %[kp], 0x0\n\t"
+                 "s_load_dword %1, %[kp], 0x40\n\t"
+                 "s_load_dword %2, %[kp], 0x80\n\t"
+                 "s_load_dword %3, %[kp], 0xc0\n\t"
+                 "s_load_dword %4, %[kp], 0x100\n\t"
+                 "s_load_dword %5, %[kp], 0x140\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b), "=&s"(c), "=&s"(d), "=&s"(e), "=&s"(f)
+                 : [kp] "s"(kp)
+                 : "memory");
+}
+__device__ __forceinline__ void ou_kernarg_prefetch8()
+{
+    const auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+    unsigned a, b, c, d, e, f, g, h;
+    asm volatile("s_load_dword %0, %[kp], 0x0\n\t"
+                 "s_load_dword %1, %[kp], 0x40\n\t"
+                 "s_load_dword %2, %[kp], 0x80\n\t"
+                 "s_load_dword %3, %[kp], 0xc0\n\t"
+                 "s_load_dword %4, %[kp], 0x100\n\t"
+                 "s_load_dword %5, %[kp], 0x140\n\t"
+                 "s_load_dword %6, %[kp], 0x180\n\t"
+                 "s_load_dword %7, %[kp], 0x1c0\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b), "=&s"(c), "=&s"(d), "=&s"(e), "=&s"(f), "=&s"(g), "=&s"(h)
+                 : [kp] "s"(kp)
+                 : "memory");
+}
 #define OU_WAIT_VMCNT0() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
 #define OU_WAIT_VMCNT(n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory")
 #endif

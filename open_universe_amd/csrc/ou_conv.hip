@@ -599,6 +599,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     using C = Cfg<KT, CC, WM, WN, WK, MR, NR, P>;
     static_assert(CC % 8 == 0 && C::HQ % WK == 0, "chunk must split into 4-pair groups per wave");
     static_assert(WM * WN * WK == 4, "4 waves per workgroup");
+    ou_kernarg_prefetch6();
     static_assert(P || (C::SX / 4) % 2 == 1, "X row stride must be an odd number of 16-B slots");
     static_assert(!P || (CC % 16 == 0 && C::HQ8 % WK == 0 && (C::SX / 8) % 2 == 1),
                   "split-f16: chunk must split into 8-pair groups per wave, odd 16-B row stride");
@@ -1017,6 +1018,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     using R = RCfg<KT, WM, WK, NR>;
     constexpr int W = R::W;
     OU_CSTAMP_INIT
+    ou_kernarg_prefetch6();
     OU_DYNAMIC_LDS(float4, lds4);
     _Float16* xs = (_Float16*)lds4;
     // K channels: the frame view's cin * R (phase-major: ph * cin + ci), in

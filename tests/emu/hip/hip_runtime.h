@@ -431,6 +431,8 @@ inline void emu_blds(emu_rsrc r, unsigned voff, unsigned soff, uintptr_t lds, in
 #define ou_blds16(r, v, s, l) emu_blds((r), (v), (s), (l), 16)
 typedef uintptr_t ou_ldsa_t;
 #define OU_LDS_ADDR(p) ((uintptr_t)(const void*)(p))
+inline void ou_kernarg_prefetch6() {}
+inline void ou_kernarg_prefetch8() {}
 #define OU_WAIT_VMCNT0() emu_wave_sync()
 #define OU_WAIT_VMCNT(n) emu_wave_sync()
 

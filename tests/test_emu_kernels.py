@@ -71,15 +71,19 @@ def _mutant(tmp_path, src, old, new):
 def _must_fail(cmd, env=None):
     e = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", **(env or {}))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=e)
-    assert r.returncode != 0 and "AddressSanitizer" in r.stderr, (r.stdout[-1000:], r.stderr[-2000:])
+    # raw pointer overruns: AddressSanitizer; buffer-resource overruns: the
+    # shim's range check (voffset + soffset past the resource)
+    assert r.returncode != 0 and ("AddressSanitizer" in r.stderr or "EMU:" in r.stderr), (r.stdout[-1000:],
+                                                                                           r.stderr[-2000:])
 
 
 def test_emulator_catches_the_reverted_rkernel_clamp(tmp_path):
     """The round-2 GPU fault (commit b31c724): a conv_rkernel wave with no K
-    steps read the weight ring below its range.  With the clamp reverted the
-    emulator must report it."""
-    src = _mutant(tmp_path, "ou_conv.hip", "const int sc = max(s0, min(s, s1 - 1));",
-                  "const int sc = min(s, s1 - 1);")
+    steps read the weight ring below its range.  The K loop now guards its
+    prologue with n > 0 (the clamped step index min(j, n - 1) is -1 without
+    it); with the guard removed the emulator must report the read."""
+    src = _mutant(tmp_path, "ou_conv.hip", "        if (n > 0) {   // uniform; clamped",
+                  "        if (true) {   // uniform; clamped")
     exe = str(tmp_path / "conv_emu_rev")
     _build("conv_emu.cpp", exe, *ASAN, f'-DOU_EMU_CONV_SRC="{src}"')
     _must_fail([exe, "12"], env={"OUHIP_EMU_RS_ONLY": "1"})
