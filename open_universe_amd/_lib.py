@@ -383,6 +383,23 @@ def block_pack(w_logical):
     return out, float(un.value)
 
 
+# tile bit 16 (ou_conv.hip kMajBit): m-groups fastest in the workgroup order,
+# so every input window is fetched from HBM once and re-read by its other
+# m-groups from the XCD's L2.  Chosen for inputs too large to stay in the
+# caches between m-groups (OUHIP_MMAJOR_MB, default 128 MB of input per
+# launch; OUHIP_MMAJOR=0 never): the batched long-signal levels (C4).
+MAJ_BIT = 1 << 16
+_MMAJOR = os.environ.get("OUHIP_MMAJOR", "1") != "0"
+_MMAJOR_BYTES = float(os.environ.get("OUHIP_MMAJOR_MB", "128")) * 2**20
+
+
+def mmajor_order(desc):
+    if not _MMAJOR or desc.tile & ((3 << 8) | (1 << 10)):   # one-tile and register-streamed kernels only
+        return False
+    in_bytes = 4.0 * desc.batch * desc.cin * desc.frame * desc.n_frames
+    return in_bytes > _MMAJOR_BYTES
+
+
 # Optional per-layer tile autotuner for ou_conv (set by the engine on a GPU):
 # called with a ConvDesc whose tile is -1, returns the tile id to record.
 TUNER = None
@@ -410,6 +427,8 @@ class Program:
             self.cur_lane = desc.id
         if op == OP_CONV and desc.tile < 0 and TUNER is not None:
             desc.tile = TUNER(desc)
+        if op == OP_CONV and desc.tile >= 0 and mmajor_order(desc):
+            desc.tile |= MAJ_BIT
         check(self.lib.ou_program_add(self.h, op, ctypes.byref(desc), ctypes.sizeof(desc)),
               f"program_add(op={op})")
         self.flops.append(float(getattr(desc, "_flops", 0.0)))

@@ -143,6 +143,23 @@ __device__ __forceinline__ void ou_xcd_block(int& bx, int& by, int& bz)
 #endif
 }
 
+// The same bijection with y (the m-groups of a conv) fastest: the workgroups
+// that read one input window (all its m-groups) run back to back on one XCD,
+// so the window is fetched from HBM once and re-read from that XCD's L2 --
+// for inputs far larger than the weights (batched, long signals), where the
+// x-fastest order re-reads every window once per m-group from HBM.
+__device__ __forceinline__ void ou_xcd_block_m(int& bx, int& by, int& bz)
+{
+    const int gx = (int)gridDim.x, gy = (int)gridDim.y;
+    const int n = gx * gy * (int)gridDim.z;
+    const int p = (int)blockIdx.x + gx * ((int)blockIdx.y + gy * (int)blockIdx.z);
+    const int x = p & 7, k = p >> 3, q = n >> 3, r = n & 7;
+    const int l = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+    by = l % gy;
+    bx = (l / gy) % gx;
+    bz = l / (gx * gy);
+}
+
 // dynamic LDS of a kernel (tests/emu replaces it with a bounds-checked block)
 #ifndef OU_DYNAMIC_LDS
 #define OU_DYNAMIC_LDS(T, name) extern __shared__ T name[]

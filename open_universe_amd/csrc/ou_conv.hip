@@ -82,6 +82,9 @@ struct Cfg {
 };
 
 constexpr int kSentinel = 0x7ffffff0;   // byte offset past any buffer: loads return 0
+// tile bit 16: m-groups fastest in the workgroup order (ou_xcd_block_m), for
+// inputs much larger than the weights; the one-tile and register-streamed kernels
+constexpr int kMajBit = 1 << 16;
 
 // Diagnostic build only (-DOU_CONV_STAMPS, tools/conv_bench.py --stamps):
 // thread 0 of each of the first kStampWGs workgroups sums s_memtime deltas
@@ -614,7 +617,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const int wk = wave / (WN * WM);
     const int nks = ksmode ? 1 << ((d.tile >> 12) & 3) : 1;   // K slices per output tile
     int bx, by, bz;
-    ou_xcd_block(bx, by, bz);
+    if (d.tile & kMajBit) ou_xcd_block_m(bx, by, bz); else ou_xcd_block(bx, by, bz);
     const int b = ksmode == 1 ? bz / nks : bz;
     const int ks = ksmode == 1 ? bz - b * nks : 0;
     const int q0 = ksmode == 1 ? ks * nchunks / nks : 0;
@@ -1032,7 +1035,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     const int wm = wave % WM, wk = wave / WM;
     const int h = lane >> 5, l32 = lane & 31;
     int bx, by, bz;
-    ou_xcd_block(bx, by, bz);
+    if (d.tile & kMajBit) ou_xcd_block_m(bx, by, bz); else ou_xcd_block(bx, by, bz);
     // K slices (S > 1, tile bits 12-13): grid z = batch x S, slice ks walks
     // chunks [ks nchunks / S, (ks + 1) nchunks / S) and stores its partial
     // sums to d.ks_ws; conv_rreduce adds them in slice order (deterministic)
@@ -2544,13 +2547,13 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
         d.frame <= 0 || d.rout == 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0 || d.f0 < 0)
         return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d frame=%d f0=%d)", d.m, d.rout, d.frame, d.f0);
     if (d.tile >= 0 && (d.tile & kRsBit)) {   // register-streamed kernel (bits 0-7: RTILES shape)
-        if ((d.tile & ~(kRsBit | 0x3ff | (3 << 12))) || (d.tile & 0xff) >= kNumRTiles)
+        if ((d.tile & ~(kRsBit | kMajBit | 0x3ff | (3 << 12))) || (d.tile & 0xff) >= kNumRTiles)
             return ou_fail(-2, "conv: bad register-streamed tile 0x%x", d.tile);
         if ((d.prec != 1 && d.prec != 2) || d.cin % 16 || d.amax_in)
             return ou_fail(-2, "conv: the register-streamed kernel needs prec 1/2, cin %% 16 == 0, no amax_in");
         if (!(d.w_unscale > 0.f)) return ou_fail(-1, "conv: split-f16 needs the w_unscale of ou_conv_pack_split");
         hipStream_t rs = (hipStream_t)stream;
-        const int t = d.tile & (0xff | kRsBit);   // bits 8-9 (diagnostics) and 12-13 (K slices) travel in d.tile
+        const int t = d.tile & (0xff | kRsBit);   // bits 8-9 (diagnostics), 12-13 (K slices), 16 travel in d.tile
         switch (d.kt) {
         case 1: return OU_LAUNCH_KT(1, d, t, 1, false, rs);
         case 3: return OU_LAUNCH_KT(3, d, t, 1, false, rs);
@@ -2567,6 +2570,8 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     const int kslices = d.tile >= 0 ? 1 << ((d.tile >> 12) & 3) : 1;
     if (kslices > 1 && (ws || tpw > 1))
         return ou_fail(-2, "conv: K slices need the one-tile kernel (tile 0x%x)", d.tile);
+    if (d.tile >= 0 && (d.tile & kMajBit) && (ws || tpw > 1))
+        return ou_fail(-2, "conv: the m-major order needs the one-tile kernel (tile 0x%x)", d.tile);
     if (ws && d.rout != 1) return ou_fail(-2, "conv: the warp-specialised kernel has no transposed (rout %d) form", d.rout);
     if (d.prec < 0 || d.prec > 2) return ou_fail(-1, "conv: bad precision %d", d.prec);
     if (d.amax_out && (ws || tpw > 1))
@@ -2613,8 +2618,11 @@ extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile_f
 extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int ou_conv_tile_ok(int kt, int tile)
 {
-    if (tile & kRsBit)   // register-streamed: shape id (+ K slices); LDS and chunks checked at launch
-        return !(tile & ~(kRsBit | 0xff | (3 << 12))) && (tile & 0xff) < kNumRTiles && (kt == 1 || kt == 3 || kt == 5);
+    if (tile & kRsBit)   // register-streamed: shape id (+ K slices, m-major order); LDS and chunks checked at launch
+        return !(tile & ~(kRsBit | kMajBit | 0xff | (3 << 12))) && (tile & 0xff) < kNumRTiles &&
+               (kt == 1 || kt == 3 || kt == 5);
+    if ((tile & kMajBit) && (tile & (kWsBit | (3 << 8)))) return 0;   // one-tile kernels only
+    tile &= ~kMajBit;
     if (tile & kSplitBit) {   // split-f16 (d.prec = 1): one-tile workgroups, no other bits
         if (tile & ~(kSplitBit | 0xff)) return 0;
         if ((tile & 0xff) >= kNumTiles) return 0;
