@@ -212,13 +212,14 @@ __device__ __forceinline__ EpiCtx epi_ctx(const ou_conv_desc& d, int b)
     c.s1e = c.has_r1 ? d.s1 : 1.f, c.s2e = c.has_r2 ? d.s2 : 1.f, c.fadd = c.has_fm ? 0.f : 1.f;
     c.bs = ou_rsrc(d.bias, d.bias ? (int64_t)c.cout * 4 : 0);
     c.fs = ou_rsrc(c.has_fm ? d.film + (int64_t)b * d.film_bstride : d.y, c.has_fm ? (int64_t)c.cout * 8 : 0);
-    // vector path: channel-major rows at rout 2 / 4 with every row start
-    // (4 rout)-byte aligned (uniform over the launch)
+    // vector path: channel-major rows at rout 2 or a multiple of 4, with every
+    // row start 8-B / 16-B aligned (uniform over the launch)
     const int rout = c.rout;
     auto al = [&](const float* p, int64_t bst, int64_t cst) {
-        return !p || (((uintptr_t)p % (4 * rout)) == 0 && bst % rout == 0 && cst % rout == 0);
+        const int A = rout == 2 ? 2 : 4;   // 8-B (rout 2) / 16-B accesses
+        return !p || (((uintptr_t)p % (4 * A)) == 0 && bst % A == 0 && cst % A == 0);
     };
-    c.vec = d.rout < 0 && (rout == 2 || rout == 4) && c.M % 4 == 0 && al(d.y, d.y_bstride, d.y_cstride) &&
+    c.vec = d.rout < 0 && (rout == 2 || rout % 4 == 0) && c.M % 4 == 0 && al(d.y, d.y_bstride, d.y_cstride) &&
             al(d.res1, d.r1_bstride, d.r1_cstride) && al(d.res2, d.r2_bstride, d.r2_cstride);
     return c;
 }
@@ -269,10 +270,11 @@ __device__ __forceinline__ void conv_epi_load(const ou_conv_desc& d, const EpiCt
             const int u = ub + nr * 32 + l32;
             e.vec[mr][nr] = false;
             if (c.vec) {
-                // channel-major rows at rout 4 / 2: register group g (rows
-                // 8 g + 4 h + j, j < 4) holds samples u rout .. u rout + rout - 1
-                // of 4 / rout channels -- one 16-B or two 8-B accesses per
-                // group and tensor, consecutive lanes on consecutive frames
+                // channel-major rows at rout 2 or 4 k: register group g (rows
+                // m0 = 8 g + 4 h + j, j < 4) holds 4 consecutive samples
+                // u rout + ph(m0) .. of one channel (rout 4 k) or 2 + 2 of two
+                // channels (rout 2) -- one 16-B or two 8-B accesses per group
+                // and tensor, consecutive lanes on consecutive frames
                 const int t0 = u * rout;
                 const bool uok = u < d.f0 + d.n_frames && t0 < ylen;
                 if (__all(!uok || t0 + rout <= ylen)) {
@@ -283,9 +285,9 @@ __device__ __forceinline__ void conv_epi_load(const ou_conv_desc& d, const EpiCt
 #pragma unroll
                         for (int sv = 0; sv < 4 / 4 + (rout == 2); ++sv) {
                             const int cc = co[4 * g + 2 * sv];
-                            const int o1 = ok ? (cc * (int)d.r1_cstride + t0) * 4 : kSentinel;
-                            const int o2 = ok ? (cc * (int)d.r2_cstride + t0) * 4 : kSentinel;
-                            if (rout == 4) {
+                            const int o1 = ok ? (cc * (int)d.r1_cstride + t0 + ph[4 * g + 2 * sv]) * 4 : kSentinel;
+                            const int o2 = ok ? (cc * (int)d.r2_cstride + t0 + ph[4 * g + 2 * sv]) * 4 : kSentinel;
+                            if (rout != 2) {
                                 const auto a1 = __builtin_amdgcn_raw_buffer_load_b128(c.r1s, o1, 0, 0);
                                 const auto a2 = __builtin_amdgcn_raw_buffer_load_b128(c.r2s, o2, 0, 0);
 #pragma unroll
@@ -374,8 +376,8 @@ __device__ __forceinline__ void conv_epi_store(const ou_conv_desc& d, const EpiC
 #pragma unroll
                     for (int sv = 0; sv < 4 / 4 + (rout == 2); ++sv) {
                         const int cc = co[4 * g + 2 * sv];
-                        const int oy = ok ? (cc * (int)d.y_cstride + t0) * 4 : kSentinel;
-                        if (rout == 4)
+                        const int oy = ok ? (cc * (int)d.y_cstride + t0 + ph[4 * g + 2 * sv]) * 4 : kSentinel;
+                        if (rout != 2)
                             __builtin_amdgcn_raw_buffer_store_b128(
                                 ou_u32x4{__float_as_uint(val[0]), __float_as_uint(val[1]), __float_as_uint(val[2]),
                                          __float_as_uint(val[3])},
@@ -440,12 +442,13 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
     const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
     const __amdgpu_buffer_rsrc_t fs = ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y,
                                               has_fm ? (int64_t)cout * 8 : 0);
-    // vector path: channel-major rows at rout 2 / 4 with every row start
-    // (4 rout)-byte aligned (uniform over the launch)
+    // vector path: channel-major rows at rout 2 or a multiple of 4, with every
+    // row start 8-B / 16-B aligned (uniform over the launch)
     auto al = [&](const float* p, int64_t bst, int64_t cst) {
-        return !p || (((uintptr_t)p % (4 * rout)) == 0 && bst % rout == 0 && cst % rout == 0);
+        const int A = rout == 2 ? 2 : 4;   // 8-B (rout 2) / 16-B accesses
+        return !p || (((uintptr_t)p % (4 * A)) == 0 && bst % A == 0 && cst % A == 0);
     };
-    const bool vec = d.rout < 0 && (rout == 2 || rout == 4) && M % 4 == 0 && al(d.y, d.y_bstride, d.y_cstride) &&
+    const bool vec = d.rout < 0 && (rout == 2 || rout % 4 == 0) && M % 4 == 0 && al(d.y, d.y_bstride, d.y_cstride) &&
                      al(d.res1, d.r1_bstride, d.r1_cstride) && al(d.res2, d.r2_bstride, d.r2_cstride);
     float ymax = 0.f;   // max |stored y| of this wave (d.amax_out)
 #pragma unroll
@@ -484,10 +487,11 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
         for (int nr = 0; nr < NR; ++nr) {
             const int u = ub + nr * 32 + l32;
             if (vec) {
-                // channel-major rows at rout 4 / 2: register group g (rows
-                // 8 g + 4 h + j, j < 4) holds samples u rout .. u rout + rout - 1
-                // of 4 / rout channels -- one 16-B or two 8-B accesses per
-                // group and tensor, consecutive lanes on consecutive frames
+                // channel-major rows at rout 2 or 4 k: register group g (rows
+                // m0 = 8 g + 4 h + j, j < 4) holds 4 consecutive samples
+                // u rout + ph(m0) .. of one channel (rout 4 k) or 2 + 2 of two
+                // channels (rout 2) -- one 16-B or two 8-B accesses per group
+                // and tensor, consecutive lanes on consecutive frames
                 const int t0 = u * rout;
                 const bool uok = u < d.f0 + d.n_frames && t0 < ylen;
                 if (__all(!uok || t0 + rout <= ylen)) {
@@ -498,9 +502,9 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
 #pragma unroll
                         for (int sv = 0; sv < 4 / 4 + (rout == 2); ++sv) {
                             const int c = co[4 * g + 2 * sv];
-                            const int o1 = ok ? (c * (int)d.r1_cstride + t0) * 4 : kSentinel;
-                            const int o2 = ok ? (c * (int)d.r2_cstride + t0) * 4 : kSentinel;
-                            if (rout == 4) {
+                            const int o1 = ok ? (c * (int)d.r1_cstride + t0 + ph[4 * g + 2 * sv]) * 4 : kSentinel;
+                            const int o2 = ok ? (c * (int)d.r2_cstride + t0 + ph[4 * g + 2 * sv]) * 4 : kSentinel;
+                            if (rout != 2) {
                                 const auto a1 = __builtin_amdgcn_raw_buffer_load_b128(r1s, o1, 0, 0);
                                 const auto a2 = __builtin_amdgcn_raw_buffer_load_b128(r2s, o2, 0, 0);
 #pragma unroll
@@ -527,8 +531,8 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
 #pragma unroll
                         for (int sv = 0; sv < 4 / 4 + (rout == 2); ++sv) {
                             const int c = co[4 * g + 2 * sv];
-                            const int oy = ok ? (c * (int)d.y_cstride + t0) * 4 : kSentinel;
-                            if (rout == 4)
+                            const int oy = ok ? (c * (int)d.y_cstride + t0 + ph[4 * g + 2 * sv]) * 4 : kSentinel;
+                            if (rout != 2)
                                 __builtin_amdgcn_raw_buffer_store_b128(
                                     ou_u32x4{__float_as_uint(val[0]), __float_as_uint(val[1]), __float_as_uint(val[2]),
                                              __float_as_uint(val[3])},
@@ -799,14 +803,20 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     }
 
     OU_CSTAMP_INIT
+    // phase-major frame views (one phase of CC channels per chunk): walk the
+    // chunks phase-fastest, so the R chunks that read the same input lines
+    // (every R-th sample, each phase in turn) run back to back and hit the
+    // caches, instead of R passes over the whole window
+    const int cpb = cin / CC;   // channel blocks per phase
+    auto qperm = [&](int k) { return (R > 1 && cin % CC == 0) ? (k % R) * cpb + k / R : k; };
     if (ksmode != 2) {
-    OU_LOAD_CHUNK(q0);
+    OU_LOAD_CHUNK(qperm(q0));
     OU_STORE_CHUNK(0);
     __syncthreads();
     OU_CSTAMP(0);
     for (int q = q0; q < q1; ++q) {
         const int cur = (q - q0) & 1;
-        if (q + 1 < q1) OU_LOAD_CHUNK(q + 1);
+        if (q + 1 < q1) OU_LOAD_CHUNK(qperm(q + 1));
         OU_CSTAMP(1);
         if constexpr (P) {
             // one step = 8 channel pairs (16 k) at one tap: 3 f16 MFMAs per

@@ -33,6 +33,7 @@ int main(int argc, char** argv)
         {64, 48, 1, 3, 29, 2, 4, true, false, false, false, true},   // channel-major rows: 16-B epilogue
         {32, 64, 1, 3, 45, 1, 2, true, true, true, false, true},     // channel-major, 2 phases: 8-B epilogue
         {24, 32, 1, 1, 37, 2, 5, true, false, false, false, true},   // channel-major, 5 phases: scalar epilogue
+        {16, 32, 1, 3, 27, 2, 8, true, true, false, false, true},    // channel-major, 8 phases: two 16-B groups a channel
     };
     const int only = argc > 1 ? std::atoi(argv[1]) : -1;
     int bad = 0, n = 0;
