@@ -433,6 +433,8 @@ constexpr int block_min_wgs()
     return (C == 96 || C == 192) ? 1 : 2;
 }
 
+constexpr int kBlkSentinel = 0x7ffffff0;   // byte offset past any buffer: loads return 0
+
 template <int C, int NT, int P, int EPI, int R = 1, int KF = 1>
 __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_kernel(ou_block_desc d)
 {
@@ -481,26 +483,31 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
         constexpr int NIT = (NI + K::NTH - 1) / K::NTH;
         const float a1 = d.slope[0];
         float v[NIT][8];
+        // h as a buffer resource: one voffset per item, the 8 channel rows as
+        // scalar soffsets i * h_cstride, frames outside [max(0, h0), min(T, h1))
+        // at the sentinel voffset (they load 0): no per-load address math
+        const int hcs = (int)d.h_cstride;
+        const __amdgpu_buffer_rsrc_t hrs = ou_rsrc(hb, (int64_t)C * d.h_cstride * 4);
+        const int tlo = max(0, hlo), thi = min(T, hhi);
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
-            // out-of-range items / frames load a clamped (valid) address and
-            // are zeroed afterwards: no branches around the loads
             const int item = min(tid + K::NTH * it, NI - 1);
             const int g = item / K::R1, r = item - g * K::R1;
             const int t = t0 - 4 - OFF + r;
-            const int tc = min(max(t, 0), T - 1);
             if constexpr (EPI & kEpiIn) {
                 const float xl = xs(t - 1), xm = xs(t), xr = xs(t + 1);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[it][i] = in_conv(8 * g + i, xl, xm, xr);
+                if (t < tlo || t >= thi || (d.dbg & 1)) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[it][i] = 0.f;
+                }
             } else {
-                const float* src = hb + (int64_t)(8 * g) * d.h_cstride + tc;
+                const bool ok = t >= tlo && t < thi && !(d.dbg & 1);
+                const int vo = ok ? (8 * g * hcs + t) * 4 : kBlkSentinel;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) v[it][i] = src[(int64_t)i * d.h_cstride];
-            }
-            if (t != tc || t < hlo || t >= hhi || (d.dbg & 1)) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) v[it][i] = 0.f;
+                for (int i = 0; i < 8; ++i)
+                    v[it][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(hrs, vo, i * hcs * 4, 0));
             }
         }
 #pragma unroll

@@ -90,10 +90,13 @@ def test_emulator_catches_the_reverted_rkernel_clamp(tmp_path):
 
 
 def test_emulator_catches_an_unclamped_block_read(tmp_path):
-    """ou_block stages PReLU(h) over its halo with clamped frame indices; an
-    unclamped one reads before the tensor at the clip start."""
-    src = _mutant(tmp_path, "ou_block.hip", "            const int tc = min(max(t, 0), T - 1);\n",
-                  "            const int tc = t;\n")
+    """ou_block stages PReLU(h) through a buffer resource: frames outside the
+    clip take the sentinel voffset (range-checked, they load 0), the channel
+    rows are scalar soffsets, which the hardware does NOT range-check.  A
+    staging read one channel group past the tensor (the last group's rows
+    shifted by 8) must be reported by the emulator."""
+    src = _mutant(tmp_path, "ou_block.hip", "__builtin_amdgcn_raw_buffer_load_b32(hrs, vo, i * hcs * 4, 0)",
+                  "__builtin_amdgcn_raw_buffer_load_b32(hrs, vo, (i + 8) * hcs * 4, 0)")
     exe = str(tmp_path / "block_emu_rev")
     _build("block_emu.cpp", exe, *ASAN, f'-DOU_EMU_BLOCK_SRC="{src}"')
     _must_fail([exe])
