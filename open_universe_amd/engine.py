@@ -586,7 +586,7 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
 
 def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film_bs=0,
               sc: Act = None, res2: Act = None, s2=1.0, cond_out: Act = None, skip_tail=False,
-              x_in=None, head=None, e_out: Act = None, rng=None, e_rng=None, share=1.0):
+              x_in=None, head=None, e_out: Act = None, rng=None, e_rng=None, share=1.0, after_c1=None):
     """ConvBlock main stage (blocks.py:393-407):
        cond_out = conv1(h); c = (cond_out + sc)/sqrt2; c = film(c); c = conv3(conv2(c));
        out = (h + c)/sqrt2 [; out = (out + res2) * s2]
@@ -599,7 +599,9 @@ def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film
     [lo / rate, ceil(hi / rate)) where it is fused).  Returns the h frames [a, b) the chunk reads, which
     the caller must have produced.  share: the chunk's share of the whole
     op (rec_block's ops count that fraction of its algorithmic FLOPs and
-    bytes: chunked plans recompute halo frames, which are not counted)."""
+    bytes: chunked plans recompute halo frames, which are not counted).
+    after_c1(): recorded as soon as conv1 (cond_out) is done -- right after
+    conv1's launch in the unfused form, after the block in the fused one."""
     T = h.T
     c1_out = cond_out if cond_out is not None else tA
     if rng is None:
@@ -622,6 +624,8 @@ def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film
     d1 = conv_desc(bw.conv1, h, c1_out, res1=sc, s1=NF2, film=film, film_bs=film_bs, rng=r1)
     if skip_tail:
         add_conv(prog, d1, share)
+        if after_c1 is not None:
+            after_c1()
         return
     d2 = conv_desc(bw.conv2, c1_out, tB, rng=r2)
     d3 = conv_desc(bw.conv3, tB, out, res1=h, s1=NF2, res2=res2, s2=s2, rng=r3)
@@ -645,11 +649,15 @@ def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film
             bd.f0, bd.f1 = r3
             bd.h0, bd.h1 = hn
         prog.add(L.OP_BLOCK, scaled(bd, share))
+        if after_c1 is not None:
+            after_c1()
         if d_rc is not None and not fuse_rc:
             add_conv(prog, d_rc, share)
         return hn if rng is not None else True
     assert x_in is None and head is None, "input / head fusion needs the fused block"
     add_conv(prog, d1, share)
+    if after_c1 is not None:
+        after_c1()
     add_conv(prog, d2, share)
     add_conv(prog, d3, share)
     if d_rc is not None:
@@ -1231,14 +1239,16 @@ class Engine:
         for l in range(n_lvl):
             i = top - l
             bw = self.s_dec[l]
-            if before_level is not None:
-                before_level(l)
             prog.label = f"score dec L{i}"
             if bw.kind == "up":
                 li = min(i, nr)
                 prog.add(L.OP_CONV, conv_desc(bw.rate_conv, h, bufs[f"V{i}"], n_frames=h.T,
                                               out_len=bufs["T"][li], valid_len=bw.rate * h.T,
                                               res1=bufs[f"V{i}"], s1=NF2))
+            # only the block's conv1 reads condition l (its input_cond
+            # residual): the up conv above runs before the wait
+            if before_level is not None:
+                before_level(l)
             last = l == n_lvl - 1
             fuse_head = (last and head is not None and bw.fused is not None and bw.C == 32
                          and fuse_ends_enabled())
@@ -1666,10 +1676,13 @@ class Engine:
                                               out_len=bufs["T"][li], valid_len=bw.rate * h.T))
                 h = hup
             last = l == n_lvl - 1
+            # condition l is conv1's output (blocks.py:402-407): the consumer
+            # hook runs as soon as conv1 is done, before the block's conv2 /
+            # conv3 (unfused 256 / 512-channel levels: the first score
+            # decoder level starts two launches earlier)
+            hook = (lambda l=l: after_level(l, bufs["COND"][l])) if after_level is not None else None
             rec_block(prog, bw, h, bufs["Y"][l], None, bufs["TB"][l], cond_out=bufs["COND"][l],
-                      skip_tail=last and not need_aux)
-            if after_level is not None:
-                after_level(l, bufs["COND"][l])
+                      skip_tail=last and not need_aux, after_c1=hook)
             h = bufs["Y"][l]
         return bufs["COND"], bufs["Y"][-1]
 
