@@ -103,8 +103,14 @@ def main():
     if len(grus) >= 3:
         steady = statistics.median(grus[k + 1]["t0"] - grus[k]["t0"] for k in range(1, len(grus) - 1))
         lines.append(f"first score GRU starts at {grus[0]['t0']:.1f} us, ends {grus[0]['t1']:.1f}; second starts "
-                     f"{grus[1]['t0']:.1f}: first step (replay start -> second GRU start, less one steady "
-                     f"encoder) vs steady step (GRU start to next GRU start) {steady:.1f} us")
+                     f"{grus[1]['t0']:.1f}; steady step (GRU start to next GRU start) {steady:.1f} us")
+        # step k runs from the start of "s{k} enc L0" to the start of the next one
+        e = [phases[f"s{k} enc L0"]["t0"] for k in (1, 2, 3) if f"s{k} enc L0" in phases]
+        if len(e) == 3:
+            lines.append(f"first step: replay start -> s2 encoder start {e[1]:.1f} us "
+                         f"(prep + conditioner + step 1; score step 1 alone {e[1] - e[0]:.1f} us); "
+                         f"steady step (s2 -> s3 encoder start) {e[2] - e[1]:.1f} us; "
+                         f"first-step excess {e[1] - (e[2] - e[1]):.1f} us")
     if a.ops:
         for o in ops:
             lines.append(f"{o['i']:4d} L{o['lane']} {o['t0']:8.1f} {o['t1']:8.1f} {o['t1'] - o['t0']:6.1f} "
