@@ -1,0 +1,70 @@
+#!/usr/bin/env bash
+# The one runner for GPU-box work (gpurun -- 'bash tools/gpu_run.sh TAG STEP...').
+# Every step runs under its own time limit; the first failing step ends the
+# call (no retries).  Outputs go to gpurun_out/*_TAG*.
+#
+#   tests            the whole `pytest -m gpu` suite
+#   tests:FILE[::T]  one test file / test
+#   profile:CFG      tools/gpu_profile.sh (bench line, kernel trace, FETCH/WRITE PMC passes)
+#   levels:CFG       tools/gpu_level_pmc.sh (per-op conv-stack table)
+#   bench:CFG        bench.py --config CFG, default arguments (the driver's line)
+#   shards           C4 at the per-rank batches of 2/4/8 GPUs (B = 16, 8, 4)
+#   critical         tools/critical_path.py --config c2 (lane timeline, first step)
+#   chunk:CFG        whole pass vs chunked pass (OUHIP_CHUNK=0/1) at CFG
+#   ab:VAR=VAL       C2 bench with VAR=0 / VAL / 0 / VAL (same box, alternating)
+#
+#   e.g. tools/gpu_run.sh r04k profile:c2 critical bench:c1 bench:c3 bench:c5
+set -o pipefail
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOT"
+TAG=$1; shift
+O="$ROOT/gpurun_out"; mkdir -p "$O"
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+line() { python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['value'], d['unit'], d['ms_per_step'], d.get('profile'), d.get('fallbacks'))" "$1"; }
+bench() {   # bench OUT LIMIT ARGS...
+    local out=$1 lim=$2; shift 2
+    timeout -k 10 "$lim" python3 bench.py "$@" > "$out.json" 2> "$out.err" || { tail -20 "$out.err"; return 1; }
+    line "$out.json"
+}
+for step in "$@"; do
+    name=${step%%:*}; arg=${step#*:}; [ "$arg" = "$step" ] && arg=""
+    echo "== $step"
+    case $name in
+    tests)
+        timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu ${arg:-tests} \
+            > "$O/tests_$TAG.log" 2>&1 || { tail -40 "$O/tests_$TAG.log"; exit 1; }
+        tail -3 "$O/tests_$TAG.log" ;;
+    profile)
+        if [ "$arg" = c2 ]; then bash tools/gpu_profile.sh "$TAG" c2 || exit 1
+        else bash tools/gpu_profile.sh "${TAG}_$arg" "$arg" --steps 4 --warmup 1 --no-f32-pass --no-queued || exit 1; fi ;;
+    levels)
+        bash tools/gpu_level_pmc.sh "${arg}_$TAG" "$arg" > /dev/null || exit 1
+        head -24 "$O/levels_${arg}_$TAG.txt" ;;
+    bench)
+        OUHIP_TUNE_CACHE="$O/tune_${TAG}_$arg.json" bench "$O/bench_${TAG}_config_$arg" 600 --config "$arg" || exit 1 ;;
+    shards)
+        for b in 16 8 4; do
+            OUHIP_TUNE_CACHE="$O/tune_${TAG}_c4.json" bench "$O/bench_${TAG}_c4_b$b" 300 --config c4 --batch $b \
+                --steps 4 --warmup 1 --no-f32-pass --no-cpu-baseline --traffic-json "" || exit 1
+        done ;;
+    critical)
+        OUHIP_TUNE_CACHE="$O/tune_${TAG}_c2.json" timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 \
+            --ops --out "$O/cp_$TAG.json" > "$O/cp_$TAG.txt" 2>&1 || { tail -20 "$O/cp_$TAG.txt"; exit 1; }
+        grep -v "ou tune\|amdgpu" "$O/cp_$TAG.txt" | grep -B2 -A1 "first step" ;;
+    chunk)
+        for c in 0 1; do
+            OUHIP_CHUNK=$c OUHIP_TUNE_CACHE="$O/tune_${TAG}_$arg.json" bench "$O/bench_${TAG}_${arg}_chunk$c" 300 \
+                --config "$arg" --steps 5 --warmup 2 --no-cpu-baseline || exit 1
+        done ;;
+    ab)
+        var=${arg%%=*}; val=${arg#*=}
+        i=0
+        for v in 0 "$val" 0 "$val"; do
+            i=$((i + 1))
+            env "$var=$v" OUHIP_TUNE_CACHE="$O/tune_${TAG}_c2.json" bench "$O/ab_${TAG}_${var}_${v}_$i" 200 --steps 20 \
+                --warmup 3 --no-cpu-baseline --no-f32-pass --no-queued --traffic-json "" || exit 1
+        done ;;
+    *)
+        echo "unknown step $step"; exit 2 ;;
+    esac
+done
