@@ -297,10 +297,14 @@ def main():
     ap.add_argument("--no-f32-pass", action="store_true",
                     help="skip the second timed pass with f32 conv operands (f32_value)")
     ap.add_argument("--dump-ops", default=None, help="write per-op profile rows (JSON)")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "pmc_latest.json"),
-                    help="per-kernel HBM traffic from tools/pmc_summary.py (rocprofv3 PMC passes)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="per-kernel HBM traffic from tools/pmc_summary.py (rocprofv3 PMC passes); default "
+                         "profiles/pmc_latest.json for c2, profiles/pmc_latest_<config>.json for the others")
     ap.add_argument("--stub-ms", type=float, default=None, help=argparse.SUPPRESS)  # CPU test of the launcher
     args = ap.parse_args()
+    if args.traffic_json is None:
+        args.traffic_json = os.path.join(HERE, "profiles", "pmc_latest.json" if args.config == "c2"
+                                         else f"pmc_latest_{args.config}.json")
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
