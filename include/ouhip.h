@@ -174,7 +174,9 @@ typedef struct ou_gru_desc {
                                /* 128-unit workgroups, bit4 timing diagnostic     */
                                /* (skips the hand-off wait: wrong results), bit8  */
                                /* per-step gi prefetch instead of LDS-staged gi   */
-                               /* chunks (one item per chain)                     */
+                               /* chunks (one item per chain); bits 12-14 XCD     */
+                               /* offset of the bit-0 chain layout, bit 15 keeps  */
+                               /* the defaults of bits 0-11                       */
     uint64_t* granules;        /* workspace: ou_gru_workspace_bytes()             */
     int32_t* status;           /* device int, set nonzero on spin timeout         */
     int32_t t_begin, t_end;    /* steps [t_begin, t_end) of the T-step sequences  */

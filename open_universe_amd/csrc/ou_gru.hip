@@ -83,10 +83,10 @@ __global__ __launch_bounds__(8 * U) void gru_kernel(ou_gru_desc d, int nb, int n
 
     const int bid = blockIdx.x;
     int chain, member;
-    if (flags & 1) {
+    if (flags & 1) {   // bits 12-14: chain c on blockIdx % 8 == (c + offset) % 8
         const int c8 = bid & 7, rest = bid >> 3;
         member = rest % G;
-        chain = (rest / G) * 8 + c8;
+        chain = (rest / G) * 8 + ((c8 - (flags >> 12)) & 7);
     } else {
         chain = bid / G;
         member = bid % G;
@@ -316,10 +316,10 @@ __global__ __launch_bounds__(64 * kKsWaves) void gru_ks_kernel(ou_gru_desc d, in
 
     const int bid = blockIdx.x;
     int chain, member;
-    if (flags & 1) {
+    if (flags & 1) {   // bits 12-14: chain c on blockIdx % 8 == (c + offset) % 8
         const int c8 = bid & 7, rest = bid >> 3;
         member = rest % G;
-        chain = (rest / G) * 8 + c8;
+        chain = (rest / G) * 8 + ((c8 - (flags >> 12)) & 7);
     } else {
         chain = bid / G;
         member = bid % G;
@@ -883,10 +883,14 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
         return ou_fail(-1, "gru: invalid descriptor");
     hipStream_t s = (hipStream_t)stream;
     const bool split = d.t_begin != 0 || (d.t_end != 0 && d.t_end != d.steps);
+    // flags: bits 0-11 as documented (or the defaults: d.flags < 0, or bit 15
+    // set), bits 12-14 the XCD offset of the chain layout (bit 0)
+    const bool dflt = d.flags < 0 || (d.flags & 0x8000);
+    const int fbits = dflt ? -1 : (d.flags & 0xfff), fofs = d.flags >= 0 ? (d.flags & 0x7000) : 0;
     if (d.t_begin < 0 || (d.t_end != 0 && (d.t_end <= d.t_begin || d.t_end > d.steps)) || (split && !d.hstate))
         return ou_fail(-1, "gru: bad step range [%d, %d) of %d (hstate %p)", d.t_begin, d.t_end, d.steps,
                        (const void*)d.hstate);
-    if (split && (d.w_hh16 || d.hidden % 64 || (d.flags >= 0 && (d.flags & 32))))
+    if (split && (d.w_hh16 || d.hidden % 64 || (fbits >= 0 && (fbits & 32))))
         return ou_fail(-2, "gru: a step range needs the k-split kernel (hidden %% 64 == 0, fp32 weights)");
     if (d.w_hh16) {   // single-CU recurrence on f16 weights (ou_gru_pack_cu16)
         if (d.hidden != kCuH) return ou_fail(-1, "gru: f16 single-CU recurrence needs hidden 256 (got %d)", d.hidden);
@@ -907,8 +911,8 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
         OU_HIP_CHECK(hipMemsetAsync(d.granules, 0, ou_gru_workspace_bytes(d.hidden, d.batch), s), "gru: memset");
     // k-split kernel (default for H % 64 == 0; flags bit5 selects the
     // workgroup-gather kernel below)
-    if (d.hidden % 64 == 0 && !(d.flags >= 0 && (d.flags & 32))) {
-        const int kflags = d.flags >= 0 ? d.flags : 1;
+    if (d.hidden % 64 == 0 && !(fbits >= 0 && (fbits & 32))) {
+        const int kflags = (fbits >= 0 ? fbits : 1) | fofs;
         switch (d.hidden) {
         case 64: launch_ks_all<64>(d, kflags, s); break;
         case 128: launch_ks_all<128>(d, kflags, s); break;
@@ -924,7 +928,7 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
     // default: XCD-local chains; 64-unit workgroups (fewer producers per
     // hand-off) for one item per chain, 32-unit ones when a workgroup carries
     // several items (measured: tools/gru_bench.py)
-    const int flags = d.flags >= 0 ? d.flags : (nb == 1 ? 5 : 1);
+    const int flags = (fbits >= 0 ? fbits : (nb == 1 ? 5 : 1)) | fofs;
     // every workgroup of a chain must be resident at once: a few hundred
     // workgroups at most, far below 256 CUs x 4
     if (nchains * (d.hidden / 32) > 512) return ou_fail(-2, "gru: grid too large for residency");

@@ -760,8 +760,13 @@ def rec_gru_ws_zero(prog, granules):
     prog.add(L.OP_MEMSET, L.MemsetArgs(ptr=granules.data_ptr(), bytes=granules.numel() * granules.element_size()))
 
 
+# XCD offset of the conditioner's GRU chains (ou_gru_desc.flags bits 12-14):
+# they run beside the first score step's GRU, whose chains sit on XCDs 0 and 1
+COND_GRU_XCD = int(os.environ.get("OUHIP_COND_GRU_XCD", "2"))
+
+
 def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, res: Act = None,
-            res_scale=1.0, steps=None, hstate=None, proj_rng=None, share=1.0):
+            res_scale=1.0, steps=None, hstate=None, proj_rng=None, share=1.0, xcd=0):
     """Bidirectional GRU layer (input projection + recurrence, gru.py via
     score.py:117-125).  steps = (t0, t1): only the recurrence steps [t0, t1)
     of both directions (forward frames t0 .. t1 - 1, backward T - t1 .. T - 1
@@ -787,7 +792,7 @@ def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, re
         d.res, d.res_bstride, d.res_cstride, d.res_scale = res.ptr, res.bs, res.cs, res_scale
     d.hidden, d.steps, d.batch = gw.hidden, x.T, x.B
     d.granules, d.status = granules.data_ptr(), status.data_ptr()
-    d.flags = GRU_FLAGS
+    d.flags = GRU_FLAGS if not xcd else (GRU_FLAGS if GRU_FLAGS >= 0 else 0x8000) | ((xcd & 7) << 12)
     d.ws_zeroed = 1 if _GRU_WS_ZEROED else 0
     if steps is not None:
         assert hstate is not None and hstate.numel() >= x.B * 2 * H and 0 <= steps[0] < steps[1] <= x.T
@@ -1654,11 +1659,12 @@ class Engine:
         if enc_done is not None:
             enc_done()
         prog.label = "cond gru1"
-        rec_gru(prog, self.c_gru, 0, bufs["CB1"], bufs["GI"], bufs["G1"], bufs["gran"], self.status)
+        rec_gru(prog, self.c_gru, 0, bufs["CB1"], bufs["GI"], bufs["G1"], bufs["gran"], self.status,
+                xcd=COND_GRU_XCD)
         res = bufs["CB1"] if self.c_gru_res else None
         prog.label = "cond gru2"
         rec_gru(prog, self.c_gru, 1, bufs["G1"], bufs["GI"], bufs["G2"], bufs["gran"], self.status,
-                res=res, res_scale=NF2)
+                res=res, res_scale=NF2, xcd=COND_GRU_XCD)
         prog.label = "cond cb2"
         rec_block(prog, self.c_cb2, bufs["G2"], bufs["H"], bufs["LA"], bufs["LB"])
         # decoder (condition.py:264-270)

@@ -41,6 +41,10 @@ LAYERS = {
     "GI": (1536, 512, 1, 1, 800, 1, False),    # GRU input projection
     "U2": (512, 256, 1, 3, 4000, 4, True),     # up-sampling conv, rate 4 (level 3 -> 2)
     "U1": (256, 128, 1, 3, 16000, 4, True),    # up-sampling conv, rate 4 (level 2 -> 1)
+    # PP24 at C4 (B = 32, 10 s) as one long item: the batch's frames back to back
+    "P3k3": (384, 384, 1, 3, 256256, 1, True),    # 384-channel level, k3
+    "P4k3": (768, 768, 1, 3, 32032, 1, True),     # 768-channel level, k3
+    "PD5": (384, 192, 5, 3, 256256, 1, False),    # down conv rate 5 (192 -> 384 channels)
 }
 
 

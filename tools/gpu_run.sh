@@ -61,8 +61,9 @@ for step in "$@"; do
         i=0
         for v in 0 "$val" 0 "$val"; do
             i=$((i + 1))
-            env "$var=$v" OUHIP_TUNE_CACHE="$O/tune_${TAG}_c2.json" bench "$O/ab_${TAG}_${var}_${v}_$i" 200 --steps 20 \
-                --warmup 3 --no-cpu-baseline --no-f32-pass --no-queued --traffic-json "" || exit 1
+            ( export "$var=$v" OUHIP_TUNE_CACHE="$O/tune_${TAG}_c2.json"
+              bench "$O/ab_${TAG}_${var}_${v}_$i" 200 --steps 20 --warmup 3 --no-cpu-baseline --no-f32-pass \
+                  --no-queued --traffic-json "" ) || exit 1
         done ;;
     *)
         echo "unknown step $step"; exit 2 ;;
