@@ -760,9 +760,11 @@ def rec_gru_ws_zero(prog, granules):
     prog.add(L.OP_MEMSET, L.MemsetArgs(ptr=granules.data_ptr(), bytes=granules.numel() * granules.element_size()))
 
 
-# XCD offset of the conditioner's GRU chains (ou_gru_desc.flags bits 12-14):
-# they run beside the first score step's GRU, whose chains sit on XCDs 0 and 1
-COND_GRU_XCD = int(os.environ.get("OUHIP_COND_GRU_XCD", "2"))
+# XCD offset of the conditioner's GRU chains (ou_gru_desc.flags bits 12-14),
+# which run beside the first score step's GRU (chains on XCDs 0 and 1).  Off:
+# XCDs 2-3 measured the same (conditioner GRU layer 1 664 us either way,
+# profiles/ab_r04_summary.txt)
+COND_GRU_XCD = int(os.environ.get("OUHIP_COND_GRU_XCD", "0"))
 
 
 def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, res: Act = None,
