@@ -85,10 +85,13 @@ int main(int argc, char** argv)
         for (int t = 0; t < ou_conv_num_tiles(); ++t) {
             if (!ou_conv_tile_ok(g.kt, t)) continue;
             // 3: warp-specialised, 4: split-f16, 5: f32 in 2 K slices, 6: split-f16 in 4 K slices,
-            // 7: f16 operands, 8: f16 in 2 K slices, 9: f16 in 4 K slices
-            for (int tpw = 0; tpw < 10; ++tpw) {
+            // 7: f16 operands, 8: f16 in 2 K slices, 9: f16 in 4 K slices,
+            // 10: register-streamed kernel (tile bit 14), split-f16
+            for (int tpw = 0; tpw < 11; ++tpw) {
                 if (tpw == 3 && g.rout != 1) continue;   // warp-specialised: plain convs only
-                if (!ou_conv_tile_ok(g.kt, t | (tpw >= 6 || tpw == 4 ? 2048 : tpw == 3 ? 1024 : tpw == 5 ? 0 : tpw << 8)))
+                if (tpw == 10 ? (t >= 6 || g.cin % 16 || !ou_conv_tile_ok(g.kt, t | (1 << 14)))
+                              : !ou_conv_tile_ok(g.kt, t | (tpw >= 6 || tpw == 4 ? 2048 : tpw == 3 ? 1024
+                                                                                : tpw == 5 ? 0 : tpw << 8)))
                     continue;
                 std::vector<float> y(ref.size(), 1e30f);
                 ou_conv_desc d{};
@@ -101,10 +104,10 @@ int main(int argc, char** argv)
                 d.res1 = g.res1 ? r1.data() : nullptr; d.r1_bstride = d.y_bstride; d.r1_cstride = out_len; d.s1 = 0.7f;
                 d.film = g.film ? fm.data() : nullptr; d.film_bstride = 2 * g.cout;
                 d.res2 = g.res2 ? r2.data() : nullptr; d.r2_bstride = d.y_bstride; d.r2_cstride = out_len; d.s2 = 0.5f;
-                d.tile = t | (tpw == 4 || tpw == 7 ? 0 : tpw == 5 || tpw == 8 ? 1 << 12
+                d.tile = t | (tpw == 10 ? 1 << 14 : tpw == 4 || tpw == 7 ? 0 : tpw == 5 || tpw == 8 ? 1 << 12
                                                     : tpw == 6 || tpw == 9 ? 2 << 12 : tpw == 3 ? 1024 : tpw << 8);
-                const bool f16 = tpw >= 7;
-                if (tpw == 4 || tpw == 6 || f16) {
+                const bool f16 = tpw >= 7 && tpw <= 9;
+                if (tpw == 4 || tpw == 6 || tpw == 10 || f16) {
                     d.prec = f16 ? 2 : 1;
                     d.w = packed_s.data();
                     d.w_unscale = unscale;
@@ -114,6 +117,7 @@ int main(int argc, char** argv)
                 const int rc_ = ou_conv(&d, nullptr);
                 if (rc_ == -2 && tpw >= 5) continue;   // more K slices than chunks
                 if (rc_ == -2 && tpw == 3) continue;   // warp-specialised form refused for this geometry
+                if (rc_ != 0 && tpw == 10) continue;   // register-streamed form refused (window / LDS)
                 if (rc_ != 0) {
                     std::printf("geom %d tile %d tpw %d: launch error\n", gi, t, tpw);
                     ++bad;

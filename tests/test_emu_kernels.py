@@ -127,12 +127,13 @@ def test_conv_values_match_reference(tmp_path):
     exe = str(tmp_path / "conv_emu_values")
     # -O0: -O1 spends minutes compiling every kernel instantiation for the host
     _build("conv_emu_values.cpp", exe, "-O0", "-DOU_EMU_FIBERS")
-    # plain k3 batch 2; 1x1 with FiLM and two residuals; transposed conv;
+    # plain k3 batch 2 (and k5: both with the register-streamed kernel);
+    # 1x1 with FiLM and two residuals; transposed conv;
     # channel-major rows at 2 / 4 / 8 phases (8-B / 16-B epilogue) -- one
     # process each, run side by side
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
     procs = [subprocess.Popen([exe, g], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
-             for g in ("0", "4", "7", "8", "9", "11")]
+             for g in ("0", "2", "4", "7", "8", "9", "11")]
     for p in procs:
         out, err = p.communicate(timeout=900)
         assert p.returncode == 0 and "ok:" in out, (out[-2000:], err[-2000:])

@@ -12,6 +12,8 @@
 #   critical         tools/critical_path.py --config c2 (lane timeline, first step)
 #   chunk:CFG        whole pass vs chunked pass (OUHIP_CHUNK=0/1) at CFG
 #   ab:VAR=VAL       C2 bench with VAR=0 / VAL / 0 / VAL (same box, alternating)
+#   ablib:NAME       C2 bench, in-tree libouhip.so vs variants/libouhip_NAME.so (3 pairs)
+#   convlib:NAME     tools/conv_bench.py deep-level layers, in-tree library vs the variant
 #
 #   e.g. tools/gpu_run.sh r04k profile:c2 critical bench:c1 bench:c3 bench:c5
 set -o pipefail
@@ -64,6 +66,22 @@ for step in "$@"; do
             ( export "$var=$v" OUHIP_TUNE_CACHE="$O/tune_${TAG}_c2.json"
               bench "$O/ab_${TAG}_${var}_${v}_$i" 200 --steps 20 --warmup 3 --no-cpu-baseline --no-f32-pass \
                   --no-queued --traffic-json "" ) || exit 1
+        done ;;
+    ablib)   # C2 bench: the in-tree library vs open_universe_amd/variants/libouhip_ARG.so, alternating
+        for i in 1 2 3; do
+            for lib in main "$arg"; do
+                ( [ "$lib" = main ] || export OUHIP_LIB="$ROOT/open_universe_amd/variants/libouhip_$lib.so"
+                  export OUHIP_TUNE_CACHE="$O/tune_${TAG}_$lib.json"
+                  bench "$O/ab_${TAG}_${lib}_$i" 200 --steps 20 --warmup 3 --no-cpu-baseline --no-f32-pass \
+                      --no-queued --traffic-json "" ) || exit 1
+            done
+        done ;;
+    convlib)   # tools/conv_bench.py on the deep-level layers: in-tree library vs variant ARG
+        for lib in main "$arg"; do
+            ( [ "$lib" = main ] || export OUHIP_LIB="$ROOT/open_universe_amd/variants/libouhip_$lib.so"
+              timeout -k 10 300 python3 tools/conv_bench.py --layer L4k3,L4k5,L3k3,L3k5,GI,U3,U2 --reps 20 \
+                  > "$O/cb_${TAG}_$lib.txt" 2>&1 ) || { tail -20 "$O/cb_${TAG}_$lib.txt"; exit 1; }
+            echo "## $lib"; grep -v amdgpu "$O/cb_${TAG}_$lib.txt" | cut -c1-160
         done ;;
     *)
         echo "unknown step $step"; exit 2 ;;
