@@ -1002,9 +1002,6 @@ __device__ __forceinline__ void split4r(float x0, float x1, float x2, float x3, 
 
 constexpr int kStageItems = 9;   // conv_rkernel: staging items (8 channels x 1 frame) per thread per round trip
 
-#ifndef OU_RS_X4
-#define OU_RS_X4 1   // conv_rkernel: 16-B staging loads for plain convs (0: dword loads, A/B builds)
-#endif
 #ifndef OU_RS_RING
 #define OU_RS_RING 12
 #endif
@@ -1135,70 +1132,6 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
         int g_it = tid / WS, sm_it = tid - g_it * WS;
         const float rpc = 1.f / (float)PC;
         const int xoff0 = c0 * (int)xc * 4;
-        if (OU_RS_X4 && RF == 1 && CCH % 32 == 0) {
-            // plain convs: item = (8 channels c0 + 8 g .., frames 4 wq .. 4 wq + 3):
-            // one 16-B load per channel row (a quarter of the dword loads'
-            // address work), items ordered 4 channel groups fastest so that the
-            // 8-B LDS stores of a 16-lane group hit distinct banks (row stride
-            // 2 SX halves = 16 banks mod 64, groups 2 banks apart).  A quad that
-            // reaches outside [0, in_len) loads its frames one by one (zero
-            // outside); quad frames past the window are loaded and dropped.
-            constexpr int WQ = (W + 3) / 4, IPQ = 3;
-            const int NQ = (CCH / 8) * WQ;
-            for (int base = 0; base < NQ; base += IPQ * 256) {
-                float4 v[IPQ][8];
-                int dsq[IPQ], w4q[IPQ];
-#pragma unroll
-                for (int it = 0; it < IPQ; ++it) {
-                    const int item = base + tid + 256 * it;
-                    const int blk = item / (4 * WQ), rem = item - blk * (4 * WQ);
-                    const int wq = rem >> 2, g = 4 * blk + (rem & 3);
-                    const int t = t0 + 4 * wq;
-                    const bool ok = item < NQ && !(diag & 1);
-                    const int rowo = xoff0 + __mul24(8 * g, (int)xc) * 4;
-                    if (ok && t >= 0 && t + 3 < in_len) {
-#pragma unroll
-                        for (int i = 0; i < 8; ++i)
-                            v[it][i] = __builtin_bit_cast(
-                                float4, __builtin_amdgcn_raw_buffer_load_b128(xrs, rowo + t * 4, i * (int)xc * 4, 0));
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < 8; ++i)
-#pragma unroll
-                            for (int e = 0; e < 4; ++e)
-                                v[it][i][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                    xrs, ok && (unsigned)(t + e) < (unsigned)in_len ? rowo + (t + e) * 4 : kSentinel,
-                                    i * (int)xc * 4, 0));
-                    }
-                    dsq[it] = item < NQ ? __mul24(4 * wq, SX) + 4 * g : -1;
-                    w4q[it] = 4 * wq;
-                }
-#pragma unroll
-                for (int it = 0; it < IPQ; ++it) {
-                    if (dsq[it] < 0) break;   // items run in order: the rest are past NQ too
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        if (e > 0 && w4q[it] + e >= W) break;   // only the last quad is partial
-                        float x[8];
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) {
-                            const float qv = v[it][i][e] * scale;
-                            x[i] = (qv >= 0.f ? qv : qv * slope) * xsc;
-                        }
-                        half4_t he, le, ho, lo;
-                        split4r<P>(x[0], x[2], x[4], x[6], he, le, ovf);
-                        split4r<P>(x[1], x[3], x[5], x[7], ho, lo, ovf);
-                        _Float16* dst = xs + dsq[it] + e * SX;
-                        *(half4_t*)dst = he;
-                        *(half4_t*)(dst + HALF) = ho;
-                        if constexpr (P == 1) {
-                            *(half4_t*)(dst + plane) = le;
-                            *(half4_t*)(dst + plane + HALF) = lo;
-                        }
-                    }
-                }
-            }
-        } else
         for (int base = 0; base < NI; base += IPT * 256) {
             float v[IPT][8];
             int dsto[IPT];
