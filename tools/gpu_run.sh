@@ -11,7 +11,7 @@
 #   shards           C4 at the per-rank batches of 2/4/8 GPUs (B = 16, 8, 4)
 #   critical         tools/critical_path.py --config c2 (lane timeline, first step)
 #   chunk:CFG        whole pass vs chunked pass (OUHIP_CHUNK=0/1) at CFG
-#   ab:VAR=VAL       C2 bench with VAR=0 / VAL / 0 / VAL (same box, alternating)
+#   ab:VAR=[A,]B     C2 bench with VAR=A / B / A / B (A defaults to 0; same box, alternating)
 #   ablib:NAME       C2 bench, in-tree libouhip.so vs variants/libouhip_NAME.so (3 pairs)
 #   convlib:NAME     tools/conv_bench.py deep-level layers, in-tree library vs the variant
 #
@@ -59,9 +59,10 @@ for step in "$@"; do
                 --config "$arg" --steps 5 --warmup 2 --no-cpu-baseline || exit 1
         done ;;
     ab)
-        var=${arg%%=*}; val=${arg#*=}
+        var=${arg%%=*}; val=${arg#*=}; base=0
+        [[ "$val" == *,* ]] && { base=${val%%,*}; val=${val#*,}; }
         i=0
-        for v in 0 "$val" 0 "$val"; do
+        for v in "$base" "$val" "$base" "$val"; do
             i=$((i + 1))
             ( export "$var=$v" OUHIP_TUNE_CACHE="$O/tune_${TAG}_c2.json"
               bench "$O/ab_${TAG}_${var}_${v}_$i" 200 --steps 20 --warmup 3 --no-cpu-baseline --no-f32-pass \
