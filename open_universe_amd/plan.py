@@ -310,8 +310,10 @@ class EnhancePlan(_PlanBase):
             else:
                 torch.randn(shape, generator=rng, out=self.NZ[k])
 
-    def __call__(self, mix, rng=None, use_graph=True):
+    def __call__(self, mix, rng=None, use_graph=True, clone=False):
         out = self.submit(mix, rng, use_graph)
+        if clone:   # queued right behind the replay, before the status check's sync
+            out = out.clone()
         self.check()
         return out
 
