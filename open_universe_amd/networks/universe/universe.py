@@ -30,10 +30,6 @@ from .blocks import PReLU_Conv
 from .condition import ConditionerNetwork
 from .score import ScoreNetwork
 
-# enhance() queues the copy of its result right behind the replay, before the
-# status check synchronises (0: copy after the check, as before; A/B runs)
-_EARLY_CLONE = os.environ.get("OUHIP_EARLY_CLONE", "1") != "0"
-
 
 class AttrDict(dict):
     """dict with attribute access (stands in for the reference's DictConfig)."""
@@ -307,8 +303,7 @@ class Universe(nn.Module):
 
             plan = self._arena_plan(key, 0, make_plan)
             try:
-                x = plan(mix, rng, clone=_EARLY_CLONE)
-                x = (x if _EARLY_CLONE else x.clone())[:, None, :]
+                x = plan(mix, rng).clone()[:, None, :]
             except L.OuRangeError:
                 # a split-f16 conv input left its range (|x| >= 2^21): switch
                 # this model to f32 operands and rerun on the same noise

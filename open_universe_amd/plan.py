@@ -310,10 +310,8 @@ class EnhancePlan(_PlanBase):
             else:
                 torch.randn(shape, generator=rng, out=self.NZ[k])
 
-    def __call__(self, mix, rng=None, use_graph=True, clone=False):
+    def __call__(self, mix, rng=None, use_graph=True):
         out = self.submit(mix, rng, use_graph)
-        if clone:   # queued right behind the replay, before the status check's sync
-            out = out.clone()
         self.check()
         return out
 
