@@ -303,7 +303,7 @@ class Universe(nn.Module):
 
             plan = self._arena_plan(key, 0, make_plan)
             try:
-                x = plan(mix, rng).clone()[:, None, :]
+                x = plan(mix, rng, clone=True)[:, None, :]
             except L.OuRangeError:
                 # a split-f16 conv input left its range (|x| >= 2^21): switch
                 # this model to f32 operands and rerun on the same noise

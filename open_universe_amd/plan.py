@@ -48,6 +48,11 @@ def edm_weights(s, level_db, data_level_db=None):
     }
 
 
+# EnhancePlan.__call__ reads the status word through pinned memory after one
+# stream wait, the result copy queued before it (0: blocking read, then copy)
+PINNED_CHECK = os.environ.get("OUHIP_PINNED_CHECK", "1") != "0"
+
+
 class _PlanBase:
     def __init__(self, eng):
         self.eng = eng
@@ -98,9 +103,20 @@ class _PlanBase:
         else:
             self.prog.run(stream)
 
-    def check(self):
+    def check(self, pinned=False):
         st = self.eng.status
-        flags = st.tolist()
+        if pinned:
+            # one wait: the status word rides to pinned host memory on the
+            # stream behind the replay, instead of a blocking read issued
+            # after it (a second host wake-up per call)
+            hs = getattr(self.eng, "status_host", None)
+            if hs is None:
+                hs = self.eng.status_host = torch.empty(st.shape, dtype=st.dtype, pin_memory=True)
+            hs.copy_(st, non_blocking=True)
+            torch.cuda.current_stream(self.dev).synchronize()
+            flags = hs.tolist()
+        else:
+            flags = st.tolist()
         if any(flags):
             st.zero_()
             if flags[0]:
@@ -310,10 +326,12 @@ class EnhancePlan(_PlanBase):
             else:
                 torch.randn(shape, generator=rng, out=self.NZ[k])
 
-    def __call__(self, mix, rng=None, use_graph=True):
+    def __call__(self, mix, rng=None, use_graph=True, clone=False):
         out = self.submit(mix, rng, use_graph)
-        self.check()
-        return out
+        if clone and PINNED_CHECK:   # the copy of the result queued behind the replay, before the wait
+            out = out.clone()
+        self.check(pinned=PINNED_CHECK)
+        return out.clone() if clone and not PINNED_CHECK else out
 
     def submit(self, mix, rng=None, use_graph=True):
         """Enqueue one enhance on the current stream without waiting for it
