@@ -95,6 +95,13 @@ CONFIGS = {
 }
 
 
+def default_traffic_json(config):
+    """The PMC summary bench quotes `traffic` from (tools/gpu_profile.sh):
+    profiles/pmc_latest.json for the headline config, pmc_latest_<config>.json
+    for the others."""
+    return os.path.join(HERE, "profiles", "pmc_latest.json" if config == "c2" else f"pmc_latest_{config}.json")
+
+
 def build_model(device, nch=None, seed=0, arch="pp16", damped=False):
     import torch
 
@@ -303,8 +310,7 @@ def main():
     ap.add_argument("--stub-ms", type=float, default=None, help=argparse.SUPPRESS)  # CPU test of the launcher
     args = ap.parse_args()
     if args.traffic_json is None:
-        args.traffic_json = os.path.join(HERE, "profiles", "pmc_latest.json" if args.config == "c2"
-                                         else f"pmc_latest_{args.config}.json")
+        args.traffic_json = default_traffic_json(args.config)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))

@@ -43,3 +43,18 @@ def test_rank_batch():
         pass
     else:
         raise AssertionError("32 clips over 3 ranks must be refused")
+
+
+def test_default_traffic_json_per_config():
+    """bench quotes `traffic` from the PMC summary of its own config: the
+    headline's pmc_latest.json, pmc_latest_<config>.json otherwise; the
+    committed files carry the library hash they were counted on."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    assert bench.default_traffic_json("c2").endswith(os.path.join("profiles", "pmc_latest.json"))
+    assert bench.default_traffic_json("c4").endswith(os.path.join("profiles", "pmc_latest_c4.json"))
+    for cfg in ("c2", "c4"):
+        with open(bench.default_traffic_json(cfg)) as fh:
+            doc = json.load(fh)
+        assert doc["config"] == cfg and len(doc["lib_sha16"]) == 16 and doc["enhances_profiled"] >= 1

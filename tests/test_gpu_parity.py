@@ -160,6 +160,29 @@ def test_gru_ws_zeroed_short_launches_back_to_back(pp16, T):
         assert torch.equal(yc, alone)
 
 
+@pytest.mark.parametrize("B,xcd", [(1, 2), (1, 7), (5, 3)])
+def test_gru_xcd_offset_same_result(pp16, B, xcd):
+    """ou_gru_desc.flags bits 12-14 (engine.rec_gru xcd=): the chains' XCD
+    layout rotated by an offset (bit 15 keeps the default bits 0-11) computes
+    the same recurrence bit for bit; B = 5 puts chains in two rows of 8."""
+    d, cfg, m = pp16
+    eng = m._get_engine()
+    T = 97
+    x = torch.randn(B, 512, T, generator=torch.Generator().manual_seed(31)) * 0.5
+    gran = torch.zeros(L.load().ou_gru_workspace_bytes(256, B) // 8, dtype=torch.int64, device=DEV)
+
+    def run(off):
+        prog = L.Program()
+        xa, gi, y = E.Act(x.to(DEV)), E.new_act(B, 1536, T, DEV), E.new_act(B, 512, T, DEV)
+        E.rec_gru(prog, eng.s_gru, 0, xa, gi, y, gran, eng.status, xcd=off)
+        prog.run(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert int(eng.status.max()) == 0
+        return y.t.cpu()
+
+    assert torch.equal(run(xcd), run(0))
+
+
 @pytest.mark.parametrize("B,T", [(1, 301), (2, 57)])
 def test_gru_layer_f16_single_cu(pp16, B, T):
     """The f16 operand mode's recurrence (ou_gru with w_hh16: one 1024-thread
