@@ -142,14 +142,18 @@ def available_cpus():
 
 # CPU sample per config: (clip seconds at B=1, clip seconds at the config's B).
 # Bounded so each leg is a few seconds of oracle work (c2: the full 8 s clip).
-CPU_SAMPLE = {"c1": (4.0, 4.0), "c2": (8.0, 8.0), "c3": (1.0, 0.25), "c4": (2.0, 0.1), "c5": (8.0, 8.0)}
+# clip seconds of the B=1 leg and of the config-B leg (None: no config-B leg;
+# C3 / C4 time one full-length clip instead of short clips at the config's B)
+CPU_SAMPLE = {"c1": (4.0, 4.0), "c2": (8.0, 8.0), "c3": (8.0, None), "c4": (10.0, None), "c5": (8.0, 8.0)}
 
 
 def cpu_baseline(model, cfg, C, config_name):
     """The oracle (CPU restatement of the reference ops, oracle/ou_oracle.py)
     on a bounded sample of the workload: B=1 and the config's B, one warm-up
-    then best of 3.  The headline ``value`` is the
-    config-B leg (the B=1 leg is reported beside it)."""
+    then best of 3 (best of 2 for the 60-step full-length clip; BASELINE.md
+    section 3).  The headline ``value`` is the config-B leg, or for C3 / C4
+    the B=1 leg on the config's full clip length (the B=1 leg is reported
+    beside it)."""
     import numpy as np
     import torch
 
@@ -166,25 +170,28 @@ def cpu_baseline(model, cfg, C, config_name):
     s1, sB = CPU_SAMPLE[config_name]
     Bc = C["batch"]
     for B, secs in ((1, s1), (Bc, sB)):
-        if B in legs:
+        if B in legs or secs is None:
             continue
+        runs = 3 if secs * (C["n_steps"] or 8) >= 400 else 4
         T = int(secs * fs)
         mix = torch.from_numpy(np.stack([synth_audio(T, fs, 99 + j)[0] for j in range(B)]))
         best = float("inf")
         with torch.no_grad():
-            for i in range(4):
+            for i in range(runs):
                 t0 = time.perf_counter()
                 orc.enhance(mix, rng=torch.Generator().manual_seed(1028282), **ekw)
                 dt = time.perf_counter() - t0
                 if i > 0:
                     best = min(best, dt)
         legs[B] = {"value": round(B * secs / best, 4), "batch": B, "clip_s": secs, "best_s": round(best, 3)}
-    head = legs[Bc]
+    head = legs[Bc] if sB is not None else legs[1]
     return {"value": head["value"], "unit": "audio-s/s", "cores": threads, "kind": "port",
             "host_cpus": os.cpu_count(), "cpu_quota": quota, "legs": list(legs.values()),
             "sample": f"oracle/ou_oracle.py Oracle.enhance ({C['arch']}, {C['n_steps'] or 8} steps, fp32), "
-                      f"torch.set_num_threads({threads}); value = the B={Bc} leg ({head['clip_s']:g} s clips), "
-                      f"B=1 leg in legs; 1 warm-up + best of 3 per leg; {cpu_model()}"}
+                      f"torch.set_num_threads({threads}); value = the B={head['batch']} leg ({head['clip_s']:g} s clips)"
+                      + (", B=1 leg in legs" if sB is not None else
+                         f", the config's full clip length; its B={Bc} batch is not run on the CPU")
+                      + f"; 1 warm-up + best of the rest per leg; {cpu_model()}"}
 
 
 def profile_roofline(plan, stream, dump=None):
