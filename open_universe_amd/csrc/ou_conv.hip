@@ -653,6 +653,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
         }
     }
     const float slope = d.slope;
+    const float sxs = scale * xsc;   // xsc is a power of two: x (scale xsc) == (x scale) xsc exactly
     const int t0 = n0 - d.pad;
 
     // ---- staging geometry, fixed for the whole K loop ----------------------
@@ -765,11 +766,16 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
             _Float16* xh_ = (_Float16*)xs_;                                                    \
             _Pragma("unroll") for (int e = 0; e < C::XE; ++e) if (xdst[e] >= 0) {              \
                 half4_t hi_, lo_;                                                              \
+                float v_[4];                                                                   \
                 _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                \
-                    const float v_ = OU_PRELU(xr[4 * e + j]) * xsc;                           \
-                    ovf |= !(__builtin_fabsf(v_) < 32768.f);                                   \
-                    hi_[j] = (_Float16)v_;                                                     \
-                    lo_[j] = (_Float16)((v_ - (float)hi_[j]) * 2048.f);                        \
+                    const float q_ = xr[4 * e + j] * sxs;   /* == PReLU(x scale) xsc: 2^k */   \
+                    v_[j] = q_ >= 0.f ? q_ : q_ * slope;                                       \
+                }                                                                              \
+                ovf |= !(fmaxf(fmaxf(__builtin_fabsf(v_[0]), __builtin_fabsf(v_[1])),          \
+                               fmaxf(__builtin_fabsf(v_[2]), __builtin_fabsf(v_[3]))) < 32768.f); \
+                _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                \
+                    hi_[j] = (_Float16)v_[j];                                                  \
+                    lo_[j] = (_Float16)((v_[j] - (float)hi_[j]) * 2048.f);                     \
                 }                                                                              \
                 *(half4_t*)(xh_ + xdst[e]) = hi_;                                              \
                 if constexpr (P == 1) *(half4_t*)(xh_ + C::W * C::SX + xdst[e]) = lo_;         \
