@@ -458,8 +458,11 @@ def main():
                        "parallelism": f"utterance-shard x{world}"},
             "xrt_per_gpu": round(value / world, 3),
             "fallbacks": fallbacks,
-            "fallbacks_note": "enhance() calls of the timed loop (and warm-up) whose split-f16 conv operands left "
-                              "their range and were rerun with f32 operands; after one, the model stays on f32",
+            "widenings": model.range_widenings,
+            "fallbacks_note": "widenings: enhance() calls of the timed loop (and warm-up) rerun after a split-f16 "
+                              "range flag widened the staging exponents of the layers it named (those layers only; "
+                              "they keep the wider exponent); fallbacks: calls rerun with f32 operands because no "
+                              "widening fixed the range (after one, the model stays on f32)",
         }
         if args.batch is not None:
             out["config"]["batch_override"] = True

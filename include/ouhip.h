@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define OUHIP_ABI_VERSION 5
+#define OUHIP_ABI_VERSION 6
 
 int ou_abi_version(void);
 const char* ou_last_error(void);
@@ -102,16 +102,39 @@ typedef struct ou_conv_desc {
                                /* at the true ends); 0 = from the start.  The    */
                                /* persistent / warp-specialised f32 kernels      */
                                /* (tile bits 8-10) need f0 = 0                   */
-    int32_t* status;           /* prec 1: set to 1 when a staged input exceeds   */
-                               /* the split-f16 range, or NULL                   */
-    float* amax_out;           /* [64] or NULL: running max |y| of the stored    */
-                               /* outputs (atomic max, one slot per workgroup    */
-                               /* id mod 64; zeroed by the caller per enhance)   */
-    const float* amax_in;      /* prec 1: [64] amax_out of x's producer, sets    */
-                               /* the staging exponent; NULL: fixed 2^-6         */
+    int32_t* status;           /* prec 1 / 2: range codes (xs_shift) are OR-ed   */
+                               /* in here, or NULL                               */
     float* ks_ws;              /* K-slice workspace (tile bits 12-13 = log2 S,   */
     int64_t ks_ws_bytes;       /* S > 1): S partial sums per output tile, then   */
                                /* a reduce + epilogue launch; NULL if unused     */
+    /* Split images (prec 1).  The operand of the NEXT conv, stored once by
+     * its producer's epilogue so that the consumer stages it with plain
+     * copies: for every stored y[b][co][t] (rout 1)
+     *   p = prelu_{sy_slope}(y) * 2^-sy_shift,  hi = f16(p),
+     *   lo = f16((p - hi) * 2^11)
+     * at byte (co / 32 * sy_rows + t) * 128 + (co % 32) * 2 (hi) and + 64
+     * (lo) of item b: one 128-B row per 32-channel block and sample, the
+     * channels of a block consecutive.  |p| >= 2^15 sets *status. */
+    uint16_t* sy;              /* producer: also store y's split image, or NULL  */
+                               /* (rout 1, m % 32 == 0, prec 1)                  */
+    int64_t sy_bstride;        /* bytes between batch items                      */
+    int32_t sy_rows;           /* samples per 32-channel block (>= out_len)      */
+    int32_t sy_shift;          /* the consumer's staging exponent                */
+    float sy_slope;            /* the consumer's PReLU slope                     */
+    int32_t sy_pad_;
+    const uint16_t* xs;        /* consumer (tile bit 15, conv_skernel): read the */
+                               /* PReLU'd operand from this split image instead  */
+                               /* of x (x, slope and in_scale unused; weights    */
+                               /* from ou_conv_pack_split_nat; cin % 32 == 0)    */
+    int64_t xs_bstride;        /* bytes between batch items                      */
+    int32_t xs_rows;           /* samples per 32-channel block (>= in_len)       */
+    int32_t xs_shift;          /* staging exponent s of every split-f16 / f16    */
+                               /* kernel: the operand is staged (with xs: was    */
+                               /* stored) as prelu(x) * 2^-s, |.| < 2^15.  A     */
+                               /* larger staged value sets range code 1 in       */
+                               /* *status, a larger split-image value (sy) 2, an */
+                               /* infinite one 4; the engine then widens that    */
+                               /* layer's exponent (default 6)                   */
 } ou_conv_desc;
 
 /* Default channel chunk of the kernel for a tap count (informational: the
@@ -134,6 +157,12 @@ int ou_conv_pack(const float* w_logical, int m, int cin_eff, int kt, int cc,
  * kernel stages the input as x * 2^-6). */
 int ou_conv_pack_split(const float* w_logical, int m, int cin_eff, int kt,
                        float* packed, float* w_unscale);
+/* The same, in the natural channel order of the split-image kernel (tile bit
+ * 15): [m-tile][16-channel group g][hi | lo][tap][lane][8 halves], lane l
+ * holding row l & 31 and channel 16*g + 8*(l >> 5) + j in half j -- a lane's
+ * B operand is then 8 consecutive channels of one split-image row. */
+int ou_conv_pack_split_nat(const float* w_logical, int m, int cin_eff, int kt,
+                           float* packed, float* w_unscale);
 int ou_conv(const ou_conv_desc* d, void* stream);
 /* The tile configuration ou_conv would use for this descriptor when
  * d->tile < 0; ou_conv_num_tiles() configurations exist, ou_conv_tile_ok()
@@ -193,21 +222,9 @@ typedef struct ou_gru_desc {
                                /* T-1, T-2 a launch leaves must not match a new   */
                                /* launch's first two polls, tags 1 and 2)         */
     int32_t _pad;
-    const void* w_hh16;        /* non-NULL: W_hh in f16 packed by                 */
-                               /* ou_gru_pack_cu16 (hidden 256, the f16 operand   */
-                               /* mode): one 1024-thread workgroup per (item,     */
-                               /* direction) holds it in registers and exchanges  */
-                               /* h through LDS -- no cross-CU hand-off; w_hh,    */
-                               /* granules and status are then unused             */
 } ou_gru_desc;
 
 int64_t ou_gru_workspace_bytes(int hidden, int batch);
-/* Pack w_hh [2][3H][H] (f32, host) for the single-CU f16 recurrence: per
- * direction, wave w, lane l (unit pair p = l >> 3, k-slice q = l & 7): the f16
- * weights W[g H + 16 w + 2 p + u][32 q + k], u < 2, g < 3, k < 32, in that
- * order.  out: ou_gru_packed_cu16_bytes(hidden) bytes. */
-int ou_gru_pack_cu16(const float* w_hh, int hidden, void* out);
-int64_t ou_gru_packed_cu16_bytes(int hidden);
 int ou_gru(const ou_gru_desc* d, void* stream);
 
 /* ------------------------------------------------------------------------
@@ -422,6 +439,11 @@ typedef struct ou_block_desc {
      * stages them but stores nothing they feed.                             */
     int32_t f0, f1;
     int32_t h0, h1;
+    /* Staging exponents (prec 1 / 2) of the conv1, conv2, conv3 and rate-
+     * change conv inputs: each is staged as prelu(v) * 2^-shift (|.| < 2^15;
+     * a larger value sets range code 1 / 2 / 8 / 16 in *status, an infinite
+     * one 4).  The engine uses 6 unless a range flag widened a stage. */
+    int32_t shift[4];
 } ou_block_desc;
 
 /* 1 when ou_block handles this channel count and operand precision. */
@@ -528,6 +550,10 @@ ou_program* ou_program_create(void);
 void ou_program_destroy(ou_program* p);
 /* op-specific descriptor, copied into the program. */
 int ou_program_add(ou_program* p, int op, const void* desc, size_t desc_bytes);
+/* Replace the descriptor of op `index` (same kind and size; drops a captured
+ * graph).  The recorder uses it to give a conv's epilogue a split-image
+ * output (ou_conv_desc.sy) once it sees the conv that consumes it. */
+int ou_program_patch(ou_program* p, int index, int op, const void* desc, size_t desc_bytes);
 int ou_program_size(const ou_program* p);
 int ou_program_run(ou_program* p, void* stream);
 /* Capture the program into a hipGraph (on a private stream) and instantiate. */

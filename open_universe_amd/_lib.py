@@ -12,7 +12,7 @@ from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OUHIP_LIB", os.path.join(_HERE, "libouhip.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 fp = c_void_p  # device pointers are passed as integers
 
@@ -38,7 +38,10 @@ class ConvDesc(ctypes.Structure):
         ("film", fp), ("film_bstride", c_int64),
         ("res2", fp), ("r2_bstride", c_int64), ("r2_cstride", c_int64), ("s2", c_float),
         ("tile", c_int32), ("prec", c_int32), ("w_unscale", c_float), ("f0", c_int32),
-        ("status", fp), ("amax_out", fp), ("amax_in", fp), ("ks_ws", fp), ("ks_ws_bytes", c_int64),
+        ("status", fp), ("ks_ws", fp), ("ks_ws_bytes", c_int64),
+        ("sy", fp), ("sy_bstride", c_int64), ("sy_rows", c_int32), ("sy_shift", c_int32),
+        ("sy_slope", c_float), ("sy_pad_", c_int32),
+        ("xs", fp), ("xs_bstride", c_int64), ("xs_rows", c_int32), ("xs_shift", c_int32),
     ]
 
 
@@ -50,7 +53,6 @@ class GruDesc(ctypes.Structure):
         ("res_scale", c_float), ("hidden", c_int32), ("steps", c_int32), ("batch", c_int32),
         ("flags", c_int32), ("granules", fp), ("status", fp), ("t_begin", c_int32), ("t_end", c_int32),
         ("hstate", fp), ("ws_zeroed", c_int32), ("_pad", c_int32),
-        ("w_hh16", fp),
     ]
 
 
@@ -143,6 +145,7 @@ class BlockDesc(ctypes.Structure):
         ("w_down", fp), ("b_down", fp), ("slope_down", c_float), ("w_down_unscale", c_float),
         ("rate", c_int32), ("down_kt", c_int32), ("e", fp), ("e_bstride", c_int64), ("e_cstride", c_int64),
         ("f0", c_int32), ("f1", c_int32), ("h0", c_int32), ("h1", c_int32),
+        ("shift", c_int32 * 4),
     ]
 
 
@@ -163,6 +166,8 @@ EXPORTS = {
     "ou_conv_pack": (c_int, [POINTER(c_float), c_int, c_int, c_int, c_int, POINTER(c_float)]),
     "ou_conv_pack_split": (c_int, [POINTER(c_float), c_int, c_int, c_int, POINTER(c_float),
                                    POINTER(c_float)]),
+    "ou_conv_pack_split_nat": (c_int, [POINTER(c_float), c_int, c_int, c_int, POINTER(c_float),
+                                       POINTER(c_float)]),
     "ou_conv": (c_int, [POINTER(ConvDesc), c_void_p]),
     "ou_conv_pick_tile": (c_int, [POINTER(ConvDesc)]),
     "ou_conv_num_tiles": (c_int, []),
@@ -170,8 +175,6 @@ EXPORTS = {
     "ou_conv_lds_info": (c_int, [c_int, c_int, POINTER(c_int), POINTER(c_int)]),
     "ou_gru_workspace_bytes": (c_int64, [c_int, c_int]),
     "ou_gru": (c_int, [POINTER(GruDesc), c_void_p]),
-    "ou_gru_pack_cu16": (c_int, [c_void_p, c_int, c_void_p]),
-    "ou_gru_packed_cu16_bytes": (c_int64, [c_int]),
     "ou_embed": (c_int, [POINTER(EmbedDesc), c_void_p]),
     "ou_head": (c_int, [POINTER(HeadDesc), c_void_p]),
     "ou_normalize": (c_int, [fp, fp, c_int, c_int64, c_float, c_float, c_void_p]),
@@ -203,6 +206,7 @@ EXPORTS = {
     "ou_program_create": (c_void_p, []),
     "ou_program_destroy": (None, [c_void_p]),
     "ou_program_add": (c_int, [c_void_p, c_int, c_void_p, c_size_t]),
+    "ou_program_patch": (c_int, [c_void_p, c_int, c_int, c_void_p, c_size_t]),
     "ou_program_size": (c_int, [c_void_p]),
     "ou_program_run": (c_int, [c_void_p, c_void_p]),
     "ou_program_capture": (c_int, [c_void_p]),
@@ -222,8 +226,11 @@ class OuHipError(RuntimeError):
 
 
 class OuRangeError(OuHipError):
-    """A split-f16 conv saw an input outside its range (|x| >= 2^21): the
-    result of that launch is not valid; rerun with f32 operands."""
+    """A split-f16 operand left its range (|prelu(x)| 2^-s >= 2^15 for the
+    layer's staging exponent s): the result of that replay is not valid.
+    ``flags``: the (layer slot, range code) pairs that name the layers
+    (Engine.widen_ranges widens their exponents; empty: rerun in f32)."""
+    flags = ()
 
 
 def load():
@@ -311,6 +318,25 @@ def conv_pack_split_np(w_logical):
     return np.ascontiguousarray(out).reshape(-1).view(np.float32), unscale
 
 
+def conv_pack_split_nat_np(w_logical):
+    """ou_conv_pack_split_nat restated with numpy (byte-identical): [mt][g]
+    [hi|lo][k][lane = h*32 + r][j] of a[mt*32 + r][16 g + 8 h + j][k] -- the
+    natural channel order of the split-image kernel (tile bit 15)."""
+    import numpy as np
+
+    w = np.ascontiguousarray(w_logical, dtype=np.float32)
+    m, cin, kt = w.shape
+    sc, unscale = _split_scale(w)
+    mt = (m + 31) // 32
+    cpad = (cin + 63) // 64 * 64
+    a = np.zeros((mt * 32, cpad, kt), dtype=np.float32)
+    a[:m, :cin] = w * sc
+    a = a.reshape(mt, 32, cpad // 16, 2, 8, kt).transpose(0, 2, 5, 3, 1, 4)   # mt, g, k, h, r, j
+    hi, lo = _hi_lo(np.ascontiguousarray(a))
+    out = np.stack([hi, lo], axis=2)                                           # mt, g, part, k, h, r, j
+    return np.ascontiguousarray(out).reshape(-1).view(np.float32), unscale
+
+
 def block_pack_np(w_logical):
     """ou_block_pack restated with numpy (byte-identical): [mt][tap][ks][hi|lo]
     [lane = h*32 + r][i] of a[mt*32 + r][16 ks + 8 h + i][tap]."""
@@ -352,9 +378,9 @@ def block_pack_f32(w_logical):
     return out, float(un.value)
 
 
-def conv_pack_split(w_logical):
+def conv_pack_split(w_logical, natural=False):
     """Split-f16 packing (ConvDesc.prec = 1) through the C ABI: returns
-    (packed, w_unscale)."""
+    (packed, w_unscale); natural: ou_conv_pack_split_nat's channel order."""
     import numpy as np
 
     w = np.ascontiguousarray(w_logical, dtype=np.float32)
@@ -362,9 +388,9 @@ def conv_pack_split(w_logical):
     n = load().ou_conv_packed_size(m, cin, kt, 0)
     out = np.empty(n, dtype=np.float32)
     un = c_float(0.0)
-    check(load().ou_conv_pack_split(w.ctypes.data_as(POINTER(c_float)), m, cin, kt,
-                                    out.ctypes.data_as(POINTER(c_float)), ctypes.byref(un)),
-          "conv_pack_split")
+    fn = load().ou_conv_pack_split_nat if natural else load().ou_conv_pack_split
+    check(fn(w.ctypes.data_as(POINTER(c_float)), m, cin, kt, out.ctypes.data_as(POINTER(c_float)),
+             ctypes.byref(un)), "conv_pack_split")
     return out, float(un.value)
 
 
@@ -405,6 +431,10 @@ def mmajor_order(desc):
 TUNER = None
 
 
+ADD_HOOK = None   # engine.split_hook while a plan records: links a conv to its producer's split image
+SS_BIT = 1 << 15  # ConvDesc.tile bit: the split-image kernel (conv_skernel), bits 0-7 = NR - 1
+
+
 class Program:
     """A recorded launch list (ou_program) with optional hipGraph replay."""
 
@@ -420,17 +450,24 @@ class Program:
         self.lanes = []         # lane of each op
         self.label = ""         # phase label recorded with each op (engine sets it; reports only)
         self.labels = []
+        self.prev_conv = {}     # lane -> (op index, ConvDesc): the lane's last op, when it is a conv
 
     def add(self, op, desc):
         assert isinstance(desc, OP_STRUCT[op])
         if op == OP_LANE:
             self.cur_lane = desc.id
+        if op == OP_CONV and ADD_HOOK is not None:
+            ADD_HOOK(self, desc)   # may link it to the lane's previous conv (split image)
         if op == OP_CONV and desc.tile < 0 and TUNER is not None:
             desc.tile = TUNER(desc)
         if op == OP_CONV and desc.tile >= 0 and mmajor_order(desc):
             desc.tile |= MAJ_BIT
         check(self.lib.ou_program_add(self.h, op, ctypes.byref(desc), ctypes.sizeof(desc)),
               f"program_add(op={op})")
+        if op == OP_CONV:
+            self.prev_conv[self.cur_lane] = (len(self.flops), desc)
+        elif op not in (OP_LANE, OP_SIGNAL):   # a wait may hand over data another lane wrote
+            self.prev_conv.pop(self.cur_lane, None)
         self.flops.append(float(getattr(desc, "_flops", 0.0)))
         self.bytes.append(float(getattr(desc, "_bytes", 0.0)))
         self.lanes.append(self.cur_lane)
@@ -463,6 +500,11 @@ class Program:
 
     def wait(self, ev):
         self.add(OP_WAIT, SyncArgs(id=ev))
+
+    def patch(self, index, op, desc):
+        """Re-send op ``index``'s descriptor after changing it (before capture)."""
+        check(self.lib.ou_program_patch(self.h, index, op, ctypes.byref(desc), ctypes.sizeof(desc)),
+              f"program_patch({index})")
 
     def __len__(self):
         return self.lib.ou_program_size(self.h)

@@ -56,7 +56,12 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 namespace {
 
-constexpr int kStageShift = 6;   // activations are staged as x * 2^-6 (ou_conv's kSplitShift)
+constexpr int kStageShift = 6;   // the exponent ou_block_pack's w_unscale assumes (ou_conv's kSplitShift)
+
+__device__ __forceinline__ float ou_bexp2i(int e)   // 2^e, |e| <= 126 (exact)
+{
+    return __uint_as_float((unsigned)(127 + e) << 23);
+}
 #ifndef OU_BLOCK_NT32
 #define OU_BLOCK_NT32 4
 #endif
@@ -341,10 +346,10 @@ constexpr int block_f()
 typedef float float2_t __attribute__((ext_vector_type(2)));
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 
-// x (already scaled by 2^-6) -> hi (+ lo) halves of 4 consecutive channels;
-// ovf |= any |x| >= 2^15
+// x (already scaled by the stage's 2^-shift) -> hi (+ lo) halves of 4
+// consecutive channels; omax = max(omax, |x|) (the stage's range flag)
 template <int P>
-__device__ __forceinline__ void split4(float x0, float x1, float x2, float x3, half4_t& hi, half4_t& lo, bool& ovf)
+__device__ __forceinline__ void split4(float x0, float x1, float x2, float x3, half4_t& hi, half4_t& lo, float& omax)
 {
     const float2_t a = {x0, x1}, b = {x2, x3};
     const half2_t ha = __builtin_convertvector(a, half2_t), hb = __builtin_convertvector(b, half2_t);
@@ -356,7 +361,7 @@ __device__ __forceinline__ void split4(float x0, float x1, float x2, float x3, h
     }
     const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(x0), __builtin_fabsf(x1)),
                                     __builtin_fmaxf(__builtin_fabsf(x2), __builtin_fabsf(x3)));
-    ovf |= !(m < 32768.f);
+    omax = __builtin_fmaxf(omax, m);
 }
 
 // kEpiDown's fourth stage: e = conv(PReLU_down(y)) over region A (rows w <->
@@ -375,7 +380,7 @@ __device__ __forceinline__ void down_stage(const ou_block_desc& d, const _Float1
     const half8_t* wp = (const half8_t*)d.w_down;
     const int TE = (TS + R - 1) / R;   // e stored for output frames < ceil(TS / R)
     const int e0 = t0 / R;
-    const float un = d.w_down_unscale;
+    const float un = d.w_down_unscale * ou_bexp2i(d.shift[3] - kStageShift);
     for (int tile = wave; tile < M4 * N4; tile += 4) {
         const int m4 = tile % M4, n4 = tile / M4;
         const int u = n4 * 32 + l32;
@@ -443,7 +448,9 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     constexpr int MR = K::MR, NR = K::NR, NF = K::NF, SX = K::SX;
     constexpr int OFF = block_off<EPI, R, KF>();   // conv3 starts OFF frames before t0
     constexpr int F = block_f<C, NT, P, EPI, R, KF>();
-    constexpr float kIn = 1.f / (1 << kStageShift);
+    // per-stage staging exponents (the host widens one whose range flag trips)
+    const float kIn0 = ou_bexp2i(-d.shift[0]), kIn1 = ou_bexp2i(-d.shift[1]), kIn2 = ou_bexp2i(-d.shift[2]),
+                kInD = ou_bexp2i(-d.shift[3]);
     OU_DYNAMIC_LDS(half8_t, lds8);
     using E = typename K::E;
     E* lds = (E*)lds8;
@@ -458,7 +465,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     const int TS = d.f1 > 0 ? min(d.f1, T) : T;   // outputs stored for frames < TS
     const int hlo = d.h0, hhi = d.h1 > 0 ? min(d.h1, T) : T;   // h frames the caller produced
     const float* __restrict__ hb = d.h + (int64_t)b * d.h_bstride;
-    bool ovf = false;
+    float om0 = 0.f, om1 = 0.f, om2 = 0.f, omd = 0.f;   // max |staged value| of the conv1 / 2 / 3 / down inputs
     // weight-fragment ring shared by the three split-f16 / f16 stages; conv1's
     // first fragments are requested before the input staging
     constexpr bool early = OU_BLOCK_RING_EARLY && P != 0;
@@ -517,15 +524,15 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
             const int g = item / K::R1, r = item - g * K::R1;
             float x[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) x[i] = (v[it][i] >= 0.f ? kIn : a1 * kIn) * v[it][i];
+            for (int i = 0; i < 8; ++i) x[i] = (v[it][i] >= 0.f ? kIn0 : a1 * kIn0) * v[it][i];
             if constexpr (P == 0) {   // f32, pair-split channel order (ch_pos)
                 E* row = xa + r * SX;
                 *(f32x4_t*)(row + 4 * g) = f32x4_t{x[0], x[2], x[4], x[6]};
                 *(f32x4_t*)(row + C / 2 + 4 * g) = f32x4_t{x[1], x[3], x[5], x[7]};
             } else {
                 half4_t h0, h1, l0, l1;
-                split4<P>(x[0], x[1], x[2], x[3], h0, l0, ovf);
-                split4<P>(x[4], x[5], x[6], x[7], h1, l1, ovf);
+                split4<P>(x[0], x[1], x[2], x[3], h0, l0, om0);
+                split4<P>(x[4], x[5], x[6], x[7], h1, l1, om0);
                 E* dst = xa + r * SX + 8 * g;
                 *(half8_t*)dst = half8_t{h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
                 if constexpr (P == 1)
@@ -546,13 +553,13 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     auto gok = [&](int mr, int j) { return !PADM || (wm * MR + mr) * 32 + 8 * j + 4 * h < C; };
     // a stage output: channels c0 .. c0 + 3 (c0 % 4 == 0) of one LDS row, as
     // the next stage's operand (split halves, or f32 in ch_pos order)
-    auto put4 = [&](E* row, int c0, const float (&x)[4], int pstride) {
+    auto put4 = [&](E* row, int c0, const float (&x)[4], int pstride, float& om) {
         if constexpr (P == 0) {
             *(float2_t*)(row + (c0 >> 1)) = float2_t{x[0], x[2]};
             *(float2_t*)(row + C / 2 + (c0 >> 1)) = float2_t{x[1], x[3]};
         } else {
             half4_t hi, lo;
-            split4<P>(x[0], x[1], x[2], x[3], hi, lo, ovf);
+            split4<P>(x[0], x[1], x[2], x[3], hi, lo, om);
             *(half4_t*)(row + c0) = hi;
             if constexpr (P == 1) *(half4_t*)(row + c0 + pstride) = lo;
         }
@@ -593,7 +600,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                     }
                 }
             }
-        const float un = d.w_unscale[0];
+        const float un = d.w_unscale[0] * ou_bexp2i(d.shift[0] - kStageShift);
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
@@ -625,9 +632,9 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const float q = o[4 * j + i];
-                        x[i] = (q >= 0.f ? kIn : a2 * kIn) * q;
+                        x[i] = (q >= 0.f ? kIn1 : a2 * kIn1) * q;
                     }
-                    put4(xbuf + u * SX, (wm * MR + mr) * 32 + 8 * j + 4 * h, x, K::PB);
+                    put4(xbuf + u * SX, (wm * MR + mr) * 32 + 8 * j + 4 * h, x, K::PB, om1);
                 }
             }
         // rows NF, NF + 1 feed only discarded conv2 columns: keep them zero
@@ -639,7 +646,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     run_stage<3, C, NT, P>(d.w[1], xbuf, K::PB, wm, wn, lane, d.dbg, acc, accx, ring, early);
     if (early) ring_pro<3, C, NT, P>(d.w[2], wm, lane, ring);   // conv3's first fragments
     {
-        const float a3 = d.slope[2], un = d.w_unscale[1];
+        const float a3 = d.slope[2], un = d.w_unscale[1] * ou_bexp2i(d.shift[1] - kStageShift);
         float bia[MR][16];
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
@@ -651,7 +658,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
             for (int nr = 0; nr < NR; ++nr) {
                 const int v_ = (wn * NR + nr) * 32 + l32;
                 const int t = t0 - 1 - OFF + v_;
-                const float keep = (t >= 0 && t < T) ? kIn : 0.f;
+                const float keep = (t >= 0 && t < T) ? kIn2 : 0.f;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if (!gok(mr, j)) continue;
@@ -663,7 +670,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                                                        un, bia[mr][r]);
                         x[i] = (q >= 0.f ? keep : a3 * keep) * q;
                     }
-                    put4(xa + v_ * SX, (wm * MR + mr) * 32 + 8 * j + 4 * h, x, K::PA);
+                    put4(xa + v_ * SX, (wm * MR + mr) * 32 + 8 * j + 4 * h, x, K::PA, om2);
                 }
             }
         for (int e = tid; e < 2 * (C / 8); e += K::NTH) zero8(xa + (NF + e / (C / 8)) * SX, 8 * (e % (C / 8)), K::PA);
@@ -713,7 +720,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     run_stage<3, C, NT, P>(d.w[2], xa, K::PA, wm, wn, lane, d.dbg, acc, accx, ring, early);
     if constexpr (!(OU_BLOCK_HV_EARLY && !(EPI & kEpiIn))) load_res();
     {
-        const float un = d.w_unscale[2];
+        const float un = d.w_unscale[2] * ou_bexp2i(d.shift[2] - kStageShift);
         float bia[MR][16];
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
@@ -794,7 +801,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                     }
                     if constexpr (EPI & kEpiDown) {
                         constexpr int RH = R * (KF - 1 - (KF - 1) / 2);
-                        const float keep = (t >= 0 && t < T && w < F + OFF + RH) ? kIn : 0.f;
+                        const float keep = (t >= 0 && t < T && w < F + OFF + RH) ? kInD : 0.f;
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             float x[4];
@@ -804,7 +811,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                                 x[i] = (q >= 0.f ? keep : ad * keep) * q;
                             }
                             half4_t hi, lo;
-                            split4<P>(x[0], x[1], x[2], x[3], hi, lo, ovf);
+                            split4<P>(x[0], x[1], x[2], x[3], hi, lo, omd);
                             if (!gok(mr, j)) continue;
                             _Float16* dst = xa + w * SX + (wm * MR + mr) * 32 + 8 * j + 4 * h;
                             *(half4_t*)dst = hi;
@@ -818,7 +825,14 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
             }
         }
     }
-    if (__any(ovf) && lane == 0 && d.status) atomicOr(d.status, 1);
+    // range codes: 1 / 2 / 8 / 16 the conv1 / conv2 / conv3 / down input's
+    // exponent is too small, 4 an infinite input (ou_range_flag)
+    if constexpr (P != 0) {
+        ou_range_flag(d.status, om0, 1, lane);
+        ou_range_flag(d.status, om1, 2, lane);
+        ou_range_flag(d.status, om2, 8, lane);
+        if constexpr ((EPI & kEpiDown) != 0) ou_range_flag(d.status, omd, 16, lane);
+    }
 }
 
 template <int C, int NT, int P, int EPI, int R = 1, int KF = 1>

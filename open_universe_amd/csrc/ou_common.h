@@ -116,9 +116,27 @@ __device__ __forceinline__ void ou_kernarg_prefetch8()
                  : [kp] "s"(kp)
                  : "memory");
 }
+// A wave reads LDS rows its own lanes just stored: in hardware the wave's
+// LDS instructions run in order (nothing to do); the CPU fiber emulator runs
+// lanes one after another and needs a rendezvous here (tests/emu).
+#define OU_WAVE_SYNC() do { } while (0)
 #define OU_WAIT_VMCNT0() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
 #define OU_WAIT_VMCNT(n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n) : "memory")
 #endif
+
+// Range flag of a split-f16 operand.  omax: the running max |staged value|
+// of a lane (fmaxf: a NaN input is skipped).  Sets bit `big` when a finite
+// value reached 2^15 (this operand's exponent is too small: the host widens
+// it) and bit 4 when a value was infinite (an overflow upstream propagating).
+#define OU_RANGE_FINITE_MAX 3.4028235e38f
+__device__ __forceinline__ void ou_range_flag(int* status, float omax, int big, int lane)
+{
+    if (__any(omax >= 32768.f) && status) {
+        const int code = (__any(omax >= 32768.f && omax <= OU_RANGE_FINITE_MAX) ? big : 0) |
+                         (__any(omax > OU_RANGE_FINITE_MAX) ? 4 : 0);
+        if (lane == 0) atomicOr(status, code);
+    }
+}
 
 // XCD-aware workgroup order (speed only, never correctness).  Workgroups
 // are dealt round-robin over the 8 XCDs, so the neighbouring workgroups that

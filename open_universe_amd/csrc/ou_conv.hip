@@ -145,14 +145,13 @@ __device__ uint64_t g_conv_stamps[kStampWGs * kStampPhases];
 // form for the STFT and mel layers, whose inputs are unbounded powers).
 // LDS planes: X [frame][h * HALF + p] of hi, then of lo (halves); A the packed
 // global order [m-tile][8-pair group][hi | lo][tap][lane][8 halves].
-// Input exponent.  The input is staged as x * 2^-s (exact).  By default
-// s = kSplitShift: |x| < 2^21 stays in f16's range, |x| >= 2^-8 keeps the full
-// 2^-22 relative precision and smaller values an absolute error <= 2^-29.
-// With d.amax_in (the running max |x| its producing conv recorded, times 4
-// for writers the slot does not see) s puts that bound just below 2^15
-// instead (the atomics cost 1-11 us per producing launch, so the engine
-// enables it only on request).  A staged |x| >= 2^15 sets *d.status: the host
-// reruns the enhance with f32 operands.
+// Input exponent.  The input is staged as x * 2^-s (exact), s = the layer's
+// d.xs_shift (the engine's default 6 = kSplitShift: |x| < 2^21 stays in f16's
+// range, |x| >= 2^-8 keeps the full 2^-22 relative precision and smaller
+// values an absolute error <= 2^-29).  A staged finite |x| 2^-s >= 2^15 sets
+// range code 1 in *d.status (ou_range_flag): the host widens that layer's s
+// and reruns the enhance.  ou_conv_pack_split's w_unscale assumes s = 6; a
+// kernel scales its result by 2^(s - 6) more.
 constexpr int kSplitShift = 6;
 typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t ou_u32x2 __attribute__((ext_vector_type(2)));
@@ -178,7 +177,7 @@ __device__ __forceinline__ void ou_row_map(int m, int rout, int cout, int& co, i
 // Epilogue of one wave's MR x NR accumulator tiles (scaled, K complete):
 // bias, zero-fill past valid_len, residual 1, FiLM, residual 2, the rout
 // pixel shuffle and the store.  mtb: the wave's first 32-row m-tile; ub: the
-// first output frame of its columns; slot: amax_out slot seed.
+// first output frame of its columns.
 //
 // Two phases: conv_epi_load issues every load the tile's epilogue needs (bias,
 // FiLM, both residuals) into registers, conv_epi_store finishes and stores.
@@ -186,11 +185,57 @@ __device__ __forceinline__ void ou_row_map(int m, int rout, int cout, int& co, i
 // buffer load returns 0 and its buffer store is dropped.  A kernel with work
 // between the two (conv_rkernel's K-split reduction through LDS) issues the
 // loads first, so their latency overlaps that work; conv_epilogue runs both.
+// Split-image output (ou_conv_desc.sy): the next conv's operand, PReLU'd,
+// scaled by 2^-sy_shift and split into f16 hi / lo, in the blocked layout
+// [c / 32][t][hi | lo][c % 32] (one 128-B row per 32-channel block and sample).
+struct SplitOut {
+    __amdgpu_buffer_rsrc_t rs;
+    int rows;
+    float scale, slope;
+};
+
+__device__ __forceinline__ float ou_exp2i(int e)   // 2^e, |e| <= 126 (exact)
+{
+    return __uint_as_float((unsigned)(127 + e) << 23);
+}
+
+__device__ __forceinline__ SplitOut split_ctx(const ou_conv_desc& d, int b, int cout)
+{
+    SplitOut s;
+    const bool on = d.sy != nullptr;
+    s.rs = ou_rsrc(on ? (const char*)d.sy + (int64_t)b * d.sy_bstride : (const char*)d.y,
+                   on ? (int64_t)((cout + 31) / 32) * d.sy_rows * 128 : 0);
+    s.rows = d.sy_rows;
+    s.scale = ou_exp2i(-d.sy_shift);
+    s.slope = d.sy_slope;
+    return s;
+}
+
+// 4 consecutive channels co0 .. co0 + 3 (co0 % 4 == 0) of sample t: 8 B of
+// hi and 8 B of lo (the two lane halves of an accumulator register group
+// hold channels co0 and co0 + 4: one 16-B piece of the row per instruction)
+__device__ __forceinline__ void split_store4(const SplitOut& s, int co0, int t, bool ok, float v0, float v1,
+                                             float v2, float v3, float& omax)
+{
+    float p[4] = {v0 * s.scale, v1 * s.scale, v2 * s.scale, v3 * s.scale};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = p[j] >= 0.f ? p[j] : p[j] * s.slope;
+    const half4_t hi = {(_Float16)p[0], (_Float16)p[1], (_Float16)p[2], (_Float16)p[3]};
+    const half4_t lo = {(_Float16)((p[0] - (float)hi[0]) * 2048.f), (_Float16)((p[1] - (float)hi[1]) * 2048.f),
+                        (_Float16)((p[2] - (float)hi[2]) * 2048.f), (_Float16)((p[3] - (float)hi[3]) * 2048.f)};
+    const float m = fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fmaxf(fabsf(p[2]), fabsf(p[3])));
+    omax = fmaxf(omax, ok ? m : 0.f);
+    const int off = ok ? ((co0 >> 5) * s.rows + t) * 128 + (co0 & 31) * 2 : kSentinel;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(ou_u32x2, hi), s.rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(ou_u32x2, lo), s.rs, off, 64, 0);
+}
+
 struct EpiCtx {
     int M, rout, cout, ylen;
     __amdgpu_buffer_rsrc_t ys, r1s, r2s, bs, fs;
-    bool has_r1, has_r2, has_fm, vec;
+    bool has_r1, has_r2, has_fm, vec, has_sy;
     float s1e, s2e, fadd;
+    SplitOut so;
 };
 
 __device__ __forceinline__ EpiCtx epi_ctx(const ou_conv_desc& d, int b)
@@ -221,6 +266,8 @@ __device__ __forceinline__ EpiCtx epi_ctx(const ou_conv_desc& d, int b)
     };
     c.vec = d.rout < 0 && (rout == 2 || rout % 4 == 0) && c.M % 4 == 0 && al(d.y, d.y_bstride, d.y_cstride) &&
             al(d.res1, d.r1_bstride, d.r1_cstride) && al(d.res2, d.r2_bstride, d.r2_cstride);
+    c.has_sy = d.sy != nullptr;   // host-checked: rout 1, m % 32 == 0
+    c.so = split_ctx(d, b, c.cout);
     return c;
 }
 
@@ -338,11 +385,11 @@ __device__ __forceinline__ void conv_epi_load(const ou_conv_desc& d, const EpiCt
 
 template <int MR, int NR>
 __device__ __forceinline__ void conv_epi_store(const ou_conv_desc& d, const EpiCtx& c, int mtb, int ub,
-                                               floatx16 (&acc)[MR][NR], const EpiPre<MR, NR>& e, int lane, int slot)
+                                               floatx16 (&acc)[MR][NR], const EpiPre<MR, NR>& e, int lane)
 {
     const int h = lane >> 5, l32 = lane & 31;
     const int M = c.M, rout = c.rout, cout = c.cout, ylen = c.ylen;
-    float ymax = 0.f;   // max |stored y| of this wave (d.amax_out)
+    float somax = 0.f;  // max |split-image value| (range flag)
 #pragma unroll
     for (int mr = 0; mr < MR; ++mr) {
         const int mt = mtb + mr;
@@ -370,7 +417,6 @@ __device__ __forceinline__ void conv_epi_store(const ou_conv_desc& d, const EpiC
                         v = (v + e.v1[mr][nr][r]) * c.s1e;
                         v = (e.fa[mr][r] + c.fadd) * v + e.fb[mr][r];
                         v = (v + e.v2[mr][nr][r]) * c.s2e;
-                        ymax = fmaxf(ymax, ok ? fabsf(v) : 0.f);
                         val[j] = v;
                     }
 #pragma unroll
@@ -389,6 +435,7 @@ __device__ __forceinline__ void conv_epi_store(const ou_conv_desc& d, const EpiC
                 }
                 continue;
             }
+            float sv[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -399,18 +446,20 @@ __device__ __forceinline__ void conv_epi_store(const ou_conv_desc& d, const EpiC
                 v = (v + e.v1[mr][nr][r]) * c.s1e;
                 v = (e.fa[mr][r] + c.fadd) * v + e.fb[mr][r];
                 v = (v + e.v2[mr][nr][r]) * c.s2e;
-                ymax = fmaxf(ymax, ok ? fabsf(v) : 0.f);
+                sv[r] = v;
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), c.ys,
                                                       ok ? (co[r] * (int)d.y_cstride + t) * 4 : kSentinel, 0, 0);
             }
+            if (c.has_sy) {   // rout 1: row m = channel, sample u
+                const bool ok = mt * 32 < M && u < d.f0 + d.n_frames && u < ylen;
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    split_store4(c.so, mt * 32 + 8 * g + 4 * h, u, ok, sv[4 * g], sv[4 * g + 1], sv[4 * g + 2],
+                                 sv[4 * g + 3], somax);
+            }
         }
     }
-    if (d.amax_out) {   // wave max, then one atomic per wave into 64 spread slots
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) ymax = fmaxf(ymax, __shfl_xor(ymax, o));
-        if (lane == 0)
-            atomicMax((unsigned int*)d.amax_out + (slot & 63), __float_as_uint(ymax));
-    }
+    if (c.has_sy) ou_range_flag(d.status, somax, 2, lane);
 }
 
 // The one-phase epilogue of the chunked / persistent kernels: per m-tile
@@ -418,7 +467,7 @@ __device__ __forceinline__ void conv_epi_store(const ou_conv_desc& d, const EpiC
 // worth -- those kernels hold MR x NR tiles).
 template <int MR, int NR>
 __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int mtb, int ub,
-                                              floatx16 (&acc)[MR][NR], int lane, int slot)
+                                              floatx16 (&acc)[MR][NR], int lane)
 {
     const int h = lane >> 5, l32 = lane & 31;
     // Branch-free: every out-of-range element gets a sentinel offset, so its
@@ -450,7 +499,8 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
     };
     const bool vec = d.rout < 0 && (rout == 2 || rout % 4 == 0) && M % 4 == 0 && al(d.y, d.y_bstride, d.y_cstride) &&
                      al(d.res1, d.r1_bstride, d.r1_cstride) && al(d.res2, d.r2_bstride, d.r2_cstride);
-    float ymax = 0.f;   // max |stored y| of this wave (d.amax_out)
+    const SplitOut so = split_ctx(d, b, cout);
+    float somax = 0.f;
 #pragma unroll
     for (int mr = 0; mr < MR; ++mr) {
         const int mt = mtb + mr;
@@ -525,8 +575,7 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
                             v = (v + v1[j]) * s1e;
                             v = (fa[r] + fadd) * v + fb[r];
                             v = (v + v2[j]) * s2e;
-                            ymax = fmaxf(ymax, ok ? fabsf(v) : 0.f);
-                            val[j] = v;
+                                val[j] = v;
                         }
 #pragma unroll
                         for (int sv = 0; sv < 4 / 4 + (rout == 2); ++sv) {
@@ -572,6 +621,7 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
 #pragma unroll
                 for (int r = 0; r < 16; ++r) v2[r] = 0.f;
             }
+            float sv[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 float v = acc[mr][nr][r] + bias[r];
@@ -579,18 +629,20 @@ __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int 
                 v = (v + v1[r]) * s1e;
                 v = (fa[r] + fadd) * v + fb[r];
                 v = (v + v2[r]) * s2e;
-                ymax = fmaxf(ymax, off[r] >= 0 ? fabsf(v) : 0.f);
+                sv[r] = v;
                 __builtin_amdgcn_raw_buffer_store_b32(
                     __float_as_uint(v), ys, off[r] >= 0 ? (co[r] * (int)d.y_cstride + off[r]) * 4 : kSentinel, 0, 0);
             }
+            if (d.sy) {   // split image of the next conv's operand (rout 1: row m = channel, sample u)
+                const bool ok = mt * 32 < M && u < d.f0 + d.n_frames && u < ylen;
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    split_store4(so, mt * 32 + 8 * g + 4 * h, u, ok, sv[4 * g], sv[4 * g + 1], sv[4 * g + 2],
+                                 sv[4 * g + 3], somax);
+            }
         }
     }
-    if (d.amax_out) {   // wave max, then one atomic per wave into 64 spread slots
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) ymax = fmaxf(ymax, __shfl_xor(ymax, o));
-        if (lane == 0)
-            atomicMax((unsigned int*)d.amax_out + (slot & 63), __float_as_uint(ymax));
-    }
+    if (d.sy) ou_range_flag(d.status, somax, 2, lane);
 }
 
 //
@@ -636,22 +688,8 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     const int xc = (int)d.x_cstride;
     const float* xb = d.x + (int64_t)b * d.x_bstride;
     const float scale = d.in_scale ? d.in_scale[b] : 1.0f;
-    float xsc = 1.f / (1 << kSplitShift), su = d.w_unscale;   // split-f16 staging / result scales
-    if constexpr (P) {
-        if (d.amax_in) {
-            float mx = 0.f;
-#pragma unroll 8
-            for (int i = 0; i < 64; ++i) mx = fmaxf(mx, d.amax_in[i]);
-            mx *= 4.f * fmaxf(1.f, fabsf(d.slope)) * fabsf(scale);
-            if (mx > 0.f) {
-                int ex = 0;
-                frexpf(mx, &ex);                          // mx < 2^ex
-                const int sh = min(60, max(-60, ex - 15));
-                xsc = ldexpf(1.f, -sh);
-                su = d.w_unscale * ldexpf(1.f, sh - kSplitShift);
-            }
-        }
-    }
+    // split-f16 staging / result scales: the layer's staging exponent
+    const float xsc = ou_exp2i(-d.xs_shift), su = d.w_unscale * ou_exp2i(d.xs_shift - kSplitShift);
     const float slope = d.slope;
     const float sxs = scale * xsc;   // xsc is a power of two: x (scale xsc) == (x scale) xsc exactly
     const int t0 = n0 - d.pad;
@@ -771,8 +809,8 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
                     const float q_ = xr[4 * e + j] * sxs;   /* == PReLU(x scale) xsc: 2^k */   \
                     v_[j] = q_ >= 0.f ? q_ : q_ * slope;                                       \
                 }                                                                              \
-                ovf |= !(fmaxf(fmaxf(__builtin_fabsf(v_[0]), __builtin_fabsf(v_[1])),          \
-                               fmaxf(__builtin_fabsf(v_[2]), __builtin_fabsf(v_[3]))) < 32768.f); \
+                omax = fmaxf(omax, fmaxf(fmaxf(__builtin_fabsf(v_[0]), __builtin_fabsf(v_[1])),    \
+                                         fmaxf(__builtin_fabsf(v_[2]), __builtin_fabsf(v_[3]))));   \
                 _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                \
                     hi_[j] = (_Float16)v_[j];                                                  \
                     lo_[j] = (_Float16)((v_[j] - (float)hi_[j]) * 2048.f);                     \
@@ -792,7 +830,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 
     floatx16 acc[MR][NR];
     floatx16 accx[P == 1 ? MR : 1][P == 1 ? NR : 1];   // split-f16 cross terms
-    bool ovf = false;                        // split-f16: staged input out of range
+    float omax = 0.f;                        // split-f16: max |staged input| (range flag)
 #pragma unroll
     for (int i = 0; i < MR; ++i)
 #pragma unroll
@@ -904,7 +942,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 #undef OU_STORE_CHUNK
 #undef OU_PRELU
     if constexpr (P) {   // range flag, then combine the split-f16 terms (exact powers of two)
-        if (__any(ovf) && lane == 0 && d.status) atomicOr(d.status, 1);
+        ou_range_flag(d.status, omax, 1, lane);
         const float sx = su * (1.f / 2048.f);
 #pragma unroll
         for (int i = 0; i < MR; ++i)
@@ -974,7 +1012,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
     }
 
     // ---- epilogue ----
-    conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane, bx + by + bz);
+    conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane);
     OU_CSTAMP(5);
     OU_CSTAMP_SAVE;
 }
@@ -996,14 +1034,13 @@ __global__ __launch_bounds__(256) void conv_kernel(ou_conv_desc d, int nchunks, 
 //   odd number of 16-B slots), lo plane after; staged from consecutive
 //   samples, so the loads are coalesced whatever R is.
 template <int P>
-__device__ __forceinline__ void split4r(float x0, float x1, float x2, float x3, half4_t& hi, half4_t& lo, bool& ovf)
+__device__ __forceinline__ void split4r(float x0, float x1, float x2, float x3, half4_t& hi, half4_t& lo, float& omax)
 {
     hi = half4_t{(_Float16)x0, (_Float16)x1, (_Float16)x2, (_Float16)x3};
     if constexpr (P == 1)
         lo = half4_t{(_Float16)((x0 - (float)hi[0]) * 2048.f), (_Float16)((x1 - (float)hi[1]) * 2048.f),
                      (_Float16)((x2 - (float)hi[2]) * 2048.f), (_Float16)((x3 - (float)hi[3]) * 2048.f)};
-    const float m = fmaxf(fmaxf(fabsf(x0), fabsf(x1)), fmaxf(fabsf(x2), fabsf(x3)));
-    ovf |= !(m < 32768.f);
+    omax = fmaxf(omax, fmaxf(fmaxf(fabsf(x0), fabsf(x1)), fmaxf(fabsf(x2), fabsf(x3))));
 }
 
 constexpr int kStageItems = 9;   // conv_rkernel: staging items (8 channels x 1 frame) per thread per round trip
@@ -1094,11 +1131,11 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
     // the batch item's input (cin rows of x_cstride floats)
     const __amdgpu_buffer_rsrc_t xrs = ou_rsrc(d.x + (int64_t)b * d.x_bstride, (int64_t)cin * xc * 4);
     const float scale = d.in_scale ? d.in_scale[b] : 1.f, slope = d.slope;
-    constexpr float xsc = 1.f / (1 << kSplitShift);
+    const float xsc = ou_exp2i(-d.xs_shift);   // the layer's staging exponent
     const int in_len = d.in_len;
     const int WS = W * PC;                                 // window samples of one chunk, per channel
     const int NI = (CCH / 8) * WS;
-    bool ovf = false;
+    float omax = 0.f;   // max |staged input| (range flag)
     // LDS row bases of this lane's B fragments, per (frame tile, tap), at group g0
     const _Float16* xrow[NR][KT];
 #pragma unroll
@@ -1167,8 +1204,8 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
                     x[i] = (qv >= 0.f ? qv : qv * slope) * xsc;
                 }
                 half4_t he, le, ho, lo;
-                split4r<P>(x[0], x[2], x[4], x[6], he, le, ovf);
-                split4r<P>(x[1], x[3], x[5], x[7], ho, lo, ovf);
+                split4r<P>(x[0], x[2], x[4], x[6], he, le, omax);
+                split4r<P>(x[1], x[3], x[5], x[7], ho, lo, omax);
                 _Float16* dst = xs + dsto[it];
                 *(half4_t*)dst = he;
                 *(half4_t*)(dst + HALF) = ho;
@@ -1224,8 +1261,8 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
         }
         OU_CSTAMP(3);
     }
-    if (__any(ovf) && lane == 0 && d.status) atomicOr(d.status, 1);
-    const float su = d.w_unscale, sx = su * (1.f / 2048.f);
+    ou_range_flag(d.status, omax, 1, lane);
+    const float su = d.w_unscale * ou_exp2i(d.xs_shift - kSplitShift), sx = su * (1.f / 2048.f);
 #pragma unroll
     for (int nr = 0; nr < NR; ++nr)
 #pragma unroll
@@ -1266,7 +1303,7 @@ __global__ __launch_bounds__(256) void conv_rkernel(ou_conv_desc d, int mtiles, 
         return;
     }
     OU_CSTAMP(4);
-    conv_epi_store<1, NR>(d, ec, mtu, n0, acc, ep, lane, bx + by + bz);
+    conv_epi_store<1, NR>(d, ec, mtu, n0, acc, ep, lane);
     OU_CSTAMP(5);
     OU_CSTAMP_SAVE;
 }
@@ -1298,7 +1335,349 @@ __global__ __launch_bounds__(256) void conv_rreduce(ou_conv_desc d, int S, int W
                 acc[0][nr][r] = k == 0 ? v : acc[0][nr][r] + v;
             }
     }
-    conv_epilogue<1, NR>(d, b, mtu, n0, acc, lane, bx + by + bz);
+    conv_epilogue<1, NR>(d, b, mtu, n0, acc, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Split-image kernel (tile bit 15; split-f16, cin a multiple of 32).  The
+// input is not the f32 signal but its split image (ou_conv_desc.xs): the
+// producing conv's epilogue has already applied this conv's PReLU and staging
+// exponent and split the result into f16 hi / lo halves, in the blocked
+// layout [c / 32][t][hi | lo][c % 32] (one 128-B row per 32-channel block and
+// sample).  Staging is a copy -- 16-B loads of whole rows, 16-B LDS stores,
+// no conversion VALU -- so it can run beside the MFMAs:
+//   * K is walked in chunks of one (phase, 32-channel block) x every tap;
+//     chunk c belongs to wave c % 4, which stages and consumes it through
+//     its own two LDS slots (no workgroup barrier before the final
+//     reduction);
+//   * the next chunk's loads are issued before the current chunk's MFMAs
+//     and stored to the other slot halfway through them;
+//   * the weights stream from L2 into a DR-deep register ring across chunk
+//     boundaries (lane-linear ou_conv_pack_split_nat order: lane l holds row
+//     l & 31, channels 16 G + 8 (l >> 5) + j, so the matching B fragment is
+//     8 consecutive channels of one LDS row: one ds_read_b128 per plane);
+//   * the four waves' partial sums are added through LDS in wave order
+//     (deterministic), each wave finishing a quarter of the rows, so the
+//     epilogue is spread over the whole workgroup.
+// One workgroup = one 32-row m-tile x 32 NR frames.  Waves whose chunk
+// count falls short of the unrolled body run zero chunks (their B rows read
+// 0, their A steps are clamped to real ones: +0 exactly).
+#ifndef OU_SK_SETS
+#define OU_SK_SETS 1
+#endif
+#ifndef OU_SK_BPREF   // B fragments read one step ahead of their MFMAs
+#define OU_SK_BPREF 1
+#endif
+#ifndef OU_SK_EPIPRE  // the epilogue's loads issued before the cross-wave reduction
+#define OU_SK_EPIPRE 1
+#endif
+// Diagnostic build (-DOU_SK_STAMPS, tools/conv_bench.py --sstamps): lane 0 of
+// every wave of the first 1024 workgroups sums s_memtime deltas per phase
+// (prologue, main loop, reduction, epilogue; 6/7 realtime) into d.ks_ws as
+// uint64 [workgroup][wave][8] -- the split-image kernel takes no K slices.
+#ifdef OU_SK_STAMPS
+#define OU_SSTAMP_INIT uint64_t sst_[8] = {}; uint64_t stp_ = __builtin_amdgcn_s_memtime(); \
+    sst_[6] = __builtin_amdgcn_s_memrealtime();
+#define OU_SSTAMP(i) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); sst_[i] += n_ - stp_; stp_ = n_; } while (0)
+#define OU_SSTAMP_SAVE                                                                          \
+    do {                                                                                        \
+        sst_[7] = __builtin_amdgcn_s_memrealtime();                                             \
+        const int wg_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);         \
+        if (lane == 0 && d.ks_ws && wg_ < 1024)                                                 \
+            for (int i_ = 0; i_ < 8; ++i_) ((uint64_t*)d.ks_ws)[(wg_ * 4 + wave) * 8 + i_] = sst_[i_]; \
+    } while (0)
+#else
+#define OU_SSTAMP_INIT
+#define OU_SSTAMP(i) do { } while (0)
+#define OU_SSTAMP_SAVE do { } while (0)
+#endif
+
+template <int KT, int NR>
+struct SCfg {
+    static constexpr int W = 32 * NR + KT - 1;      // window frames (LDS rows) of a chunk
+    static constexpr int NL = (W * 8 + 63) / 64;   // 16-B loads per lane per chunk (8 lanes per row)
+    static constexpr int RS = 144;                 // LDS row stride: 128 B + 16 (9 slots: odd, conflict-free)
+    static constexpr int SLOT = W * RS;
+    static constexpr int STEPS = 2 * KT;           // K steps per chunk: 2 groups of 16 channels x taps
+    static constexpr int U = KT == 1 ? 4 : 2;      // chunks per unrolled body
+    // register sets for rows in flight: 1 = the next chunk's rows loaded at a
+    // chunk's start and stored halfway through it; U = loaded SETS - 0.5
+    // chunks ahead (more VGPRs: at 64-frame tiles two waves per SIMD no
+    // longer fit, measured slower on the 4005-frame levels)
+    static constexpr int SETS = OU_SK_SETS == 1 ? 1 : U;
+    static constexpr int DR = KT == 5 ? 10 : U * STEPS;   // weight ring depth (divides U * STEPS)
+    static constexpr int RED = 4 * NR * 16 * 64 * 4;       // the reduction image (bytes)
+    static constexpr int LDS = 8 * SLOT > RED ? 8 * SLOT : RED;
+    static_assert((U * STEPS) % DR == 0, "ring depth must divide the unrolled body");
+    static_assert(U % SETS == 0, "register sets must divide the unrolled body");
+};
+
+// The split-image kernel's epilogue: wave q finishes rows 8 q + 4 h .. + 3
+// (accumulator registers 4 q .. 4 q + 3) of its m-tile.  Two phases: every
+// load (bias, FiLM, residuals) is issued before the cross-wave reduction,
+// which then hides their latency.
+template <int NR>
+struct EpiQ {
+    int m0, co[4], ph[4], off[NR][4];
+    float bias[4], fa[4], fb[4], v1[NR][4], v2[NR][4];
+};
+
+template <int NR>
+__device__ __forceinline__ void conv_epi_q_load(const ou_conv_desc& d, const EpiCtx& c, int mt, int ub, int q, int lane,
+                                                EpiQ<NR>& e)
+{
+    const int h = lane >> 5, l32 = lane & 31;
+    const int M = c.M, rout = c.rout, cout = c.cout, ylen = c.ylen;
+    e.m0 = mt * 32 + 8 * q + 4 * h;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ou_row_map(min(e.m0 + j, M - 1), d.rout, cout, e.co[j], e.ph[j]);
+    if (d.bias) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            e.bias[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.bs, e.co[j] * 4, 0, 0));
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e.bias[j] = 0.f;
+    }
+    if (c.has_fm) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            e.fa[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.fs, e.co[j] * 4, 0, 0));
+            e.fb[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(c.fs, (cout + e.co[j]) * 4, 0, 0));
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e.fa[j] = 0.f, e.fb[j] = 0.f;
+    }
+#pragma unroll
+    for (int nr = 0; nr < NR; ++nr) {
+        const int u = ub + nr * 32 + l32;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = u * rout + e.ph[j];
+            e.off[nr][j] = (e.m0 + j < M && u < d.f0 + d.n_frames && t < ylen) ? t : -1;
+            e.v1[nr][j] = e.v2[nr][j] = 0.f;
+        }
+        if (c.has_r1) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                e.v1[nr][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    c.r1s, e.off[nr][j] >= 0 ? (e.co[j] * (int)d.r1_cstride + e.off[nr][j]) * 4 : kSentinel, 0, 0));
+        }
+        if (c.has_r2) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                e.v2[nr][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    c.r2s, e.off[nr][j] >= 0 ? (e.co[j] * (int)d.r2_cstride + e.off[nr][j]) * 4 : kSentinel, 0, 0));
+        }
+    }
+}
+
+template <int NR>
+__device__ __forceinline__ void conv_epi_q_store(const ou_conv_desc& d, const EpiCtx& c, int ub, const EpiQ<NR>& e,
+                                                 const float (&v)[NR][4], int lane, float& somax)
+{
+    const int l32 = lane & 31;
+#pragma unroll
+    for (int nr = 0; nr < NR; ++nr) {
+        float sv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float x = v[nr][j] + e.bias[j];
+            if (e.off[nr][j] >= d.valid_len) x = 0.f;
+            x = (x + e.v1[nr][j]) * c.s1e;
+            x = (e.fa[j] + c.fadd) * x + e.fb[j];
+            x = (x + e.v2[nr][j]) * c.s2e;
+            sv[j] = x;
+            __builtin_amdgcn_raw_buffer_store_b32(
+                __float_as_uint(x), c.ys, e.off[nr][j] >= 0 ? (e.co[j] * (int)d.y_cstride + e.off[nr][j]) * 4 : kSentinel,
+                0, 0);
+        }
+        if (c.has_sy) {   // rout 1 (host-checked): rows are channels m0 .. m0 + 3, sample u
+            const int u = ub + nr * 32 + l32;
+            split_store4(c.so, e.m0, u, e.off[nr][0] >= 0, sv[0], sv[1], sv[2], sv[3], somax);
+        }
+    }
+}
+
+template <int KT, int NR>
+__global__ __launch_bounds__(256) void conv_skernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride)
+{
+    using S = SCfg<KT, NR>;
+    ou_kernarg_prefetch8();
+    OU_DYNAMIC_LDS(float4, lds4);
+    char* lds = (char*)lds4;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar chunk / step math
+    const int h = lane >> 5, l32 = lane & 31;
+    int bx, by, bz;
+    if (d.tile & kMajBit) ou_xcd_block_m(bx, by, bz); else ou_xcd_block(bx, by, bz);
+    const int b = bz;
+    const int n0 = bx * 32 * NR + d.f0;   // first output frame (global)
+    const int mt = min(by, mtiles - 1);
+    const int cin = d.cin, RF = d.frame;
+    const int ncb = cin / 32, nch = ncb * RF;   // chunks c = ph * ncb + cb (phase-major K)
+    // every wave walks the same number of chunks (a multiple of U): chunk
+    // c = wave + 4 j, zero chunks past nch
+    const int njb = (nch + 4 * S::U - 1) / (4 * S::U);   // unrolled bodies
+    const int nj = njb * S::U;
+    const int n = nj * S::STEPS;                         // K steps of this wave
+
+    // ---- weights: step i = (chunk j, group gg, tap k) -> 16-channel group
+    // G = 2 c + gg of the phase-major K; byte offset in the m-tile's panel
+    const __amdgpu_buffer_rsrc_t ars = ou_rsrc((const char*)d.w + (int64_t)mt * a_mt_stride * 4, a_mt_stride * 4);
+    const unsigned avoff = (unsigned)lane * 16u;
+    half8_t ra[S::DR][2];
+    auto load_a = [&](int i, half8_t (&dst)[2]) {   // i uniform
+        i = min(i, n - 1);
+        const int j = i / S::STEPS, s = i - (i / S::STEPS) * S::STEPS;
+        const int c = min(wave + 4 * j, nch - 1);   // zero chunks: any real step (times B = 0)
+        const int gg = s / KT, k = s - (s / KT) * KT;
+        const unsigned so = (unsigned)(((2 * c + gg) * 2 * KT + k) * 1024);
+        dst[0] = __builtin_bit_cast(half8_t, __builtin_amdgcn_raw_buffer_load_b128(ars, avoff, so, 0));
+        dst[1] = __builtin_bit_cast(half8_t, __builtin_amdgcn_raw_buffer_load_b128(ars, avoff, so + KT * 1024u, 0));
+    };
+
+    // ---- input rows: load l of a lane covers item 64 l + lane = (window
+    // row w = item / 8, 16-B piece ls = item % 8) -- 8 lanes per 128-B row
+    const __amdgpu_buffer_rsrc_t xrs =
+        ou_rsrc((const char*)d.xs + (int64_t)b * d.xs_bstride, (int64_t)ncb * d.xs_rows * 128);
+    const int t0 = (n0 - d.pad) * RF + d.shift;   // sample of window row 0 at phase 0
+    const int in_len = d.in_len;
+    char* myslots = lds + wave * 2 * S::SLOT;
+    const int wr0 = lane >> 3, ls = lane & 7;
+    ou_u32x4 xr[S::SETS][S::NL];   // a chunk's rows are loaded SETS - 0.5 chunks before they are stored
+    auto stage_load = [&](int j, int set) {   // j uniform (j >= nj or a zero chunk: every load reads 0)
+        const int c = wave + 4 * j;
+        const bool real = c < nch;
+        const int ph = real ? c / ncb : 0, cb = real ? c - (c / ncb) * ncb : 0;
+        const unsigned so = (unsigned)(cb * d.xs_rows) * 128u;
+#pragma unroll
+        for (int l = 0; l < S::NL; ++l) {
+            const int w = 8 * l + wr0;
+            const int t = t0 + w * RF + ph;
+            const bool ok = real && w < S::W && (unsigned)t < (unsigned)in_len;
+            xr[set][l] = __builtin_amdgcn_raw_buffer_load_b128(xrs, ok ? t * 128 + ls * 16 : kSentinel, so, 0);
+        }
+    };
+    auto stage_store = [&](int slot, int set) {   // slot, set static
+        char* base = myslots + slot * S::SLOT + wr0 * S::RS + ls * 16;
+#pragma unroll
+        for (int l = 0; l < S::NL; ++l)
+            if (8 * (S::NL - 1) + 7 < S::W || l < S::NL - 1 || 8 * l + wr0 < S::W)
+                *(ou_u32x4*)(base + l * 8 * S::RS) = xr[set][l];
+        OU_WAVE_SYNC();
+    };
+
+    floatx16 acc[NR], accx[NR];
+#pragma unroll
+    for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[nr][r] = 0.f, accx[nr][r] = 0.f;
+
+    // B fragments of (slot, group gg, tap k): LDS row nr * 32 + l32 + k,
+    // 16-B piece 2 gg + h (hi) and + 4 (lo)
+    const char* bbase = myslots + l32 * S::RS + h * 16;
+    half8_t bq[2][NR], bl[2][NR];   // B fragments, double-buffered by step parity
+    auto read_b = [&](int slot, int gg, int k, half8_t (&q)[NR], half8_t (&l)[NR]) {
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+            const char* p = bbase + slot * S::SLOT + (nr * 32 + k) * S::RS + gg * 32;
+            q[nr] = *(const half8_t*)p;
+            l[nr] = *(const half8_t*)(p + 64);
+        }
+    };
+    auto mfmas = [&](const half8_t (&a)[2], const half8_t (&q)[NR], const half8_t (&l)[NR]) {
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+            acc[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], q[nr], acc[nr], 0, 0, 0);
+            accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], l[nr], accx[nr], 0, 0, 0);
+            accx[nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], q[nr], accx[nr], 0, 0, 0);
+        }
+    };
+
+    // Schedule of chunk j (LDS slot j & 1):
+    //   SETS == 1: chunk j + 1's rows are loaded at chunk j's start and stored
+    //     to slot (j + 1) & 1 halfway through it;
+    //   SETS > 1: at chunk j's half, chunk j + SETS's rows are loaded into set
+    //     j % SETS (whose rows, chunk j's, are in LDS already), and at step
+    //     STEPS - 2 set (j + 1) % SETS is stored to slot (j + 1) & 1, one step
+    //     before chunk j + 1 reads it.
+    //   Slot (j + 1) & 1's last reader, chunk j - 1, is done by then.  With
+    //   OU_SK_BPREF the B fragments of step s + 1 are read before step s's
+    //   MFMAs (the next chunk's first ones from the other slot).
+    OU_SSTAMP_INIT
+#pragma unroll
+    for (int i = 0; i < S::DR - 1; ++i) load_a(i, ra[i]);
+#pragma unroll
+    for (int q = 0; q < S::SETS; ++q) stage_load(q, q);
+    stage_store(0, 0);
+    if (OU_SK_BPREF) read_b(0, 0, 0, bq[0], bl[0]);
+    OU_SSTAMP(0);
+    for (int jb = 0; jb < njb; ++jb) {
+#pragma unroll
+        for (int u = 0; u < S::U; ++u) {
+            const int j = jb * S::U + u;
+            if (S::SETS == 1) stage_load(j + 1, 0);
+#pragma unroll
+            for (int s = 0; s < S::STEPS; ++s) {
+                const int ib = (u * S::STEPS + s) % S::DR;   // ring slot of step j * STEPS + s (static)
+                const int par = (u * S::STEPS + s) & 1;      // B buffer of this step
+                if (S::SETS > 1 && s == S::STEPS / 2) stage_load(j + S::SETS, u % S::SETS);
+                load_a(j * S::STEPS + s + S::DR - 1, ra[(ib + S::DR - 1) % S::DR]);
+                if (OU_SK_BPREF) {
+                    // the next step's fragments (the next chunk's first: the other slot)
+                    if (s + 1 < S::STEPS) read_b(u & 1, (s + 1) / KT, (s + 1) % KT, bq[par ^ 1], bl[par ^ 1]);
+                    else read_b((u + 1) & 1, 0, 0, bq[par ^ 1], bl[par ^ 1]);
+                } else {
+                    read_b(u & 1, s / KT, s % KT, bq[par], bl[par]);
+                }
+                mfmas(ra[ib], bq[par], bl[par]);
+                if (S::SETS == 1 ? s == S::STEPS / 2 - 1 : (s == S::STEPS - 2 || (S::STEPS < 2 && s == 0)))
+                    stage_store((u + 1) & 1, S::SETS == 1 ? 0 : (u + 1) % S::SETS);
+            }
+        }
+    }
+    OU_SSTAMP(1);
+
+    // ---- combine the split-f16 terms, then the four waves' partial sums
+    const float su = d.w_unscale * ou_exp2i(d.xs_shift - kSplitShift), sx = su * (1.f / 2048.f);
+#pragma unroll
+    for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[nr][r] = fmaf(accx[nr][r], sx, acc[nr][r] * su);
+    const EpiCtx ec = epi_ctx(d, b);
+    EpiQ<NR> eq;
+    if (OU_SK_EPIPRE) conv_epi_q_load<NR>(d, ec, by, n0, wave, lane, eq);   // latency hidden by the reduction
+    __syncthreads();   // every wave is done with its slots
+    ou_u32x4* red = (ou_u32x4*)lds;   // [wave][nr][register quad][lane]
+#pragma unroll
+    for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+            red[((wave * NR + nr) * 4 + qq) * 64 + lane] =
+                ou_u32x4{__float_as_uint(acc[nr][4 * qq]), __float_as_uint(acc[nr][4 * qq + 1]),
+                         __float_as_uint(acc[nr][4 * qq + 2]), __float_as_uint(acc[nr][4 * qq + 3])};
+    __syncthreads();
+    float v[NR][4];
+#pragma unroll
+    for (int nr = 0; nr < NR; ++nr) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[nr][j] = 0.f;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {   // wave order: deterministic
+            const ou_u32x4 x = red[((p * NR + nr) * 4 + wave) * 64 + lane];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[nr][j] = p == 0 ? __uint_as_float(x[j]) : v[nr][j] + __uint_as_float(x[j]);
+        }
+    }
+    if (!OU_SK_EPIPRE) conv_epi_q_load<NR>(d, ec, by, n0, wave, lane, eq);
+    OU_SSTAMP(2);
+    float somax = 0.f;
+    conv_epi_q_store<NR>(d, ec, n0, eq, v, lane, somax);
+    if (ec.has_sy) ou_range_flag(d.status, somax, 2, lane);
+    OU_SSTAMP(3);
+    OU_SSTAMP_SAVE;
 }
 
 // ---------------------------------------------------------------------------
@@ -2361,9 +2740,50 @@ int launch_rs(const ou_conv_desc& d, int shape, hipStream_t s)
     }
 }
 
+// split-image shapes (tile bit 15): bits 0-7 = NR - 1 (32 NR frames per workgroup)
+constexpr int kSsBit = 1 << 15;
+[[maybe_unused]] constexpr int kNumSTiles = 3;
+
+template <int KT, int NR>
+int launch_s1(const ou_conv_desc& d, hipStream_t s)
+{
+    using S = SCfg<KT, NR>;
+    auto kern = conv_skernel<KT, NR>;
+    static bool attr = false;
+    if (!attr && S::LDS > 64 * 1024) {
+        OU_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS),
+                     "conv: LDS attribute");
+        attr = true;
+    }
+    const int mtiles = (d.m + 31) / 32;
+    const int cin_eff = d.cin * d.frame;
+    const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
+    const int64_t a_mt_stride = (int64_t)cin_pad * KT * 32;
+    dim3 grid((d.n_frames + 32 * NR - 1) / (32 * NR), mtiles, d.batch);
+    hipLaunchKernelGGL(kern, grid, dim3(256), S::LDS, s, d, mtiles, a_mt_stride);
+    return ou_check_launch("conv (split image)");
+}
+
+template <int KT>
+int launch_ss(const ou_conv_desc& d, int shape, hipStream_t s)
+{
+    if constexpr (KT == 1 || KT == 3 || KT == 5) {
+        switch (shape) {
+        case 0: return launch_s1<KT, 1>(d, s);
+        case 1: return launch_s1<KT, 2>(d, s);
+        case 2: return launch_s1<KT, 3>(d, s);
+        }
+        return ou_fail(-2, "conv: bad split-image tile %d", shape);
+    } else {
+        (void)d, (void)shape, (void)s;
+        return ou_fail(-2, "conv: no split-image kernel for kt %d", KT);
+    }
+}
+
 template <int KT>
 int launch_kt(const ou_conv_desc& d, int tile, int tpw, bool ws, hipStream_t s)
 {
+    if (tile & kSsBit) return launch_ss<KT>(d, tile & 0xff, s);
     if (tile & kRsBit) return launch_rs<KT>(d, tile & 0xff, s);
     if (d.prec == 1) {   // split-f16: one-tile workgroups (checked by ou_conv)
         switch (tile) {
@@ -2555,6 +2975,45 @@ extern "C" int ou_conv_pack_split(const float* w, int m, int cin_eff, int kt, fl
     return 0;
 }
 
+// Natural-order split packing (include/ouhip.h): as ou_conv_pack_split with
+// lane l holding channel 16 g + 8 (l >> 5) + j of row l & 31 in half j.
+extern "C" int ou_conv_pack_split_nat(const float* w, int m, int cin_eff, int kt, float* out, float* w_unscale)
+{
+    if (!w || !out || !w_unscale || m <= 0 || cin_eff <= 0 || kt <= 0)
+        return ou_fail(-1, "conv_pack_split_nat: bad arguments");
+    const int64_t n = (int64_t)m * cin_eff * kt;
+    float mx = 0.f;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!std::isfinite(w[i])) return ou_fail(-1, "conv_pack_split_nat: non-finite weight at %lld", (long long)i);
+        mx = std::max(mx, std::fabs(w[i]));
+    }
+    int e = 0;
+    if (mx > 0.f) {
+        int ex = 0;
+        std::frexp(mx, &ex);
+        e = std::min(100, std::max(-100, 10 - ex));
+    }
+    const float sc = std::ldexp(1.f, e);
+    const int mtiles = (m + 31) / 32;
+    const int cin_pad = (cin_eff + kCinAlign - 1) / kCinAlign * kCinAlign;
+    _Float16* o = (_Float16*)out;
+    for (int mt = 0; mt < mtiles; ++mt)
+        for (int g = 0; g < cin_pad / 16; ++g)
+            for (int part = 0; part < 2; ++part)
+                for (int k = 0; k < kt; ++k)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int j = 0; j < 8; ++j) {
+                            const int row = mt * 32 + (lane & 31);
+                            const int c = 16 * g + 8 * (lane >> 5) + j;
+                            const float a =
+                                (row < m && c < cin_eff) ? w[((int64_t)row * cin_eff + c) * kt + k] * sc : 0.f;
+                            const _Float16 hi = (_Float16)a;
+                            *o++ = part == 0 ? hi : (_Float16)((a - (float)hi) * 2048.f);
+                        }
+    *w_unscale = std::ldexp(1.f, kSplitShift - e);
+    return 0;
+}
+
 extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
 {
     if (!dp) return ou_fail(-1, "conv: null descriptor");
@@ -2562,11 +3021,38 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     if (!d.x || !d.w || !d.y || d.m <= 0 || d.batch <= 0 || d.n_frames <= 0 || d.cin <= 0 ||
         d.frame <= 0 || d.rout == 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0 || d.f0 < 0)
         return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d frame=%d f0=%d)", d.m, d.rout, d.frame, d.f0);
+    if (d.sy) {   // split-image output (any split-f16 kernel's epilogue)
+        if (d.prec != 1 || d.rout != 1 || d.m % 32 || d.sy_rows < d.out_len || d.sy_shift < -100 ||
+            d.sy_shift > 100 || (int64_t)(d.m / 32) * d.sy_rows * 128 >= kSentinel)
+            return ou_fail(-1, "conv: split-image output needs prec 1, rout 1, m %% 32 == 0, sy_rows >= out_len "
+                               "(m %d rout %d rows %d out_len %d)", d.m, d.rout, d.sy_rows, d.out_len);
+    }
+    if (d.xs || (d.tile >= 0 && (d.tile & kSsBit))) {   // split-image input (bits 0-7: NR - 1)
+        // static choice: 64-frame workgroups while they still give one per CU
+        const int tile = d.tile >= 0 ? d.tile
+                         : kSsBit | ((int64_t)(d.n_frames + 63) / 64 * ((d.m + 31) / 32) * d.batch >= 256 ? 1 : 0);
+        if (!d.xs || !(tile & kSsBit) || (tile & ~(kSsBit | kMajBit | 0xff)) || (tile & 0xff) >= kNumSTiles)
+            return ou_fail(-2, "conv: a split-image input needs a split-image tile (tile 0x%x)", d.tile);
+        if (d.prec != 1 || d.cin % 32 || d.xs_rows < d.in_len || d.xs_shift < -100 ||
+            d.xs_shift > 100 || (int64_t)(d.cin / 32) * d.xs_rows * 128 >= kSentinel)
+            return ou_fail(-2, "conv: the split-image kernel needs prec 1, cin %% 32 == 0, xs_rows >= in_len, "
+                               "(cin %d rows %d in_len %d)", d.cin, d.xs_rows, d.in_len);
+        if (!(d.w_unscale > 0.f)) return ou_fail(-1, "conv: split-f16 needs the w_unscale of ou_conv_pack_split_nat");
+        hipStream_t ss = (hipStream_t)stream;
+        ou_conv_desc dd = d;   // the kernel reads its order bit from the tile
+        dd.tile = tile;
+        switch (d.kt) {
+        case 1: return OU_LAUNCH_KT(1, dd, tile, 1, false, ss);
+        case 3: return OU_LAUNCH_KT(3, dd, tile, 1, false, ss);
+        case 5: return OU_LAUNCH_KT(5, dd, tile, 1, false, ss);
+        }
+        return ou_fail(-2, "conv: no split-image kernel for kt %d", d.kt);
+    }
     if (d.tile >= 0 && (d.tile & kRsBit)) {   // register-streamed kernel (bits 0-7: RTILES shape)
         if ((d.tile & ~(kRsBit | kMajBit | 0x3ff | (3 << 12))) || (d.tile & 0xff) >= kNumRTiles)
             return ou_fail(-2, "conv: bad register-streamed tile 0x%x", d.tile);
-        if ((d.prec != 1 && d.prec != 2) || d.cin % 16 || d.amax_in)
-            return ou_fail(-2, "conv: the register-streamed kernel needs prec 1/2, cin %% 16 == 0, no amax_in");
+        if ((d.prec != 1 && d.prec != 2) || d.cin % 16)
+            return ou_fail(-2, "conv: the register-streamed kernel needs prec 1/2, cin %% 16 == 0");
         if (!(d.w_unscale > 0.f)) return ou_fail(-1, "conv: split-f16 needs the w_unscale of ou_conv_pack_split");
         hipStream_t rs = (hipStream_t)stream;
         const int t = d.tile & (0xff | kRsBit);   // bits 8-9 (diagnostics), 12-13 (K slices), 16 travel in d.tile
@@ -2590,8 +3076,6 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
         return ou_fail(-2, "conv: the m-major order needs the one-tile kernel (tile 0x%x)", d.tile);
     if (ws && d.rout != 1) return ou_fail(-2, "conv: the warp-specialised kernel has no transposed (rout %d) form", d.rout);
     if (d.prec < 0 || d.prec > 2) return ou_fail(-1, "conv: bad precision %d", d.prec);
-    if (d.amax_out && (ws || tpw > 1))
-        return ou_fail(-2, "conv: amax_out needs the one-tile kernel (tile 0x%x)", d.tile);
     if (d.prec != 0 && (ws || tpw > 1))
         return ou_fail(-2, "conv: the split-f16 form has one-tile workgroups only (tile 0x%x)", d.tile);
     if (d.f0 != 0 && (ws || tpw > 1))
@@ -2634,6 +3118,8 @@ extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile_f
 extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int ou_conv_tile_ok(int kt, int tile)
 {
+    if (tile & kSsBit)   // split-image input: shape = NR - 1 (+ m-major order)
+        return !(tile & ~(kSsBit | kMajBit | 0xff)) && (tile & 0xff) < kNumSTiles && (kt == 1 || kt == 3 || kt == 5);
     if (tile & kRsBit)   // register-streamed: shape id (+ K slices, m-major order); LDS and chunks checked at launch
         return !(tile & ~(kRsBit | kMajBit | 0xff | (3 << 12))) && (tile & 0xff) < kNumRTiles &&
                (kt == 1 || kt == 3 || kt == 5);

@@ -662,160 +662,6 @@ int launch_ks_all(const ou_gru_desc& d, int flags, hipStream_t s)
     return launch_ks_uw<H, 8>(d, flags, s);
 }
 
-// ---------------------------------------------------------------------------
-// Single-CU recurrence with f16 weights (the f16 operand mode, BASELINE
-// configs[4]; d.w_hh16 set, H = 256).  W_hh in f16 is 3 x 256 x 256 x 2 B =
-// 393 KB per direction: it fits one CU's register file, so a direction is ONE
-// 1024-thread workgroup and h_{t-1} is exchanged through LDS with a workgroup
-// barrier instead of the cross-CU granule hand-off (0.79 us per step, the
-// floor of the k-split kernel).  The step is then bound by its own arithmetic:
-// 3 x 256 x 256 f16 MACs on v_dot2_f32_f16 (f32 accumulation).
-//   wave w (16) owns units [16 w, 16 w + 16); lane l: unit pair p = l >> 3
-//   (units 16 w + 2 p, + 1), k-slice q = l & 7 (k in [32 q, 32 q + 32)), holding
-//   W[g H + u][k] of both units and the 3 gates: 96 dwords of f16 pairs,
-//   packed lane-linear by ou_gru_pack_cu16.  h_{t-1} lives in LDS as f16
-//   (double-buffered by step parity); the recurrent state of a unit is kept in
-//   f32 by its writer lane (q == 0: unit 2 p, q == 1: unit 2 p + 1).
-// One CU serves all 256 units, so per-unit global accesses (gi, the residual,
-// y: one 4-B element per unit and step, rows T apart) would cost ~1300 cache-
-// line requests per step on its one address unit.  They are staged instead in
-// blocks of kCuS steps through LDS, with lanes along time (8 lanes per row):
-// gi and the residual of block k + 1 are loaded at block k's first step and
-// written to LDS at its last; y of block k is stored at block k + 1's first.
-constexpr int kCuWaves = 16;
-constexpr int kCuH = 256;
-constexpr int kCuDwords = 96;   // f16 pairs of W per lane
-constexpr int kCuS = 4;         // steps per staged block
-
-typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-
-__global__ __launch_bounds__(64 * kCuWaves) void gru_cu_kernel(ou_gru_desc d)
-{
-    constexpr int H = kCuH, S = kCuS;
-    constexpr int NROW = 4 * H;                 // staged rows: gi of the 3 gates, then the residual
-    constexpr int PER = NROW * S / (64 * kCuWaves);   // staged elements per thread per block
-    static_assert(NROW * S == PER * 64 * kCuWaves && H * S % (64 * kCuWaves) == 0, "staging split");
-    const int dir = blockIdx.x & 1, b = blockIdx.x >> 1;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int q = lane & 7, p = lane >> 3;
-    const int j = wave * 16 + 2 * p + (q & 1);   // the unit whose gates this lane evaluates
-    const bool writer = q < 2;
-    const int T = d.steps;
-    __shared__ __attribute__((aligned(16))) _Float16 hs[2][H];
-    __shared__ __attribute__((aligned(16))) float gbuf[2][NROW * S];
-    __shared__ float ybuf[2][H * (S + 1)];   // rows padded: unit-column writes conflict-free
-
-    uint32_t w[kCuDwords];
-    {
-        const uint4* wp = (const uint4*)d.w_hh16 + ((int64_t)(dir * kCuWaves + wave) * 64 + lane) * (kCuDwords / 4);
-#pragma unroll
-        for (int i = 0; i < kCuDwords / 4; ++i) {
-            const uint4 v = wp[i];
-            w[4 * i] = v.x, w[4 * i + 1] = v.y, w[4 * i + 2] = v.z, w[4 * i + 3] = v.w;
-        }
-    }
-    const float bhr = d.b_hh[dir * 3 * H + 0 * H + j];
-    const float bhz = d.b_hh[dir * 3 * H + 1 * H + j];
-    const float bhn = d.b_hh[dir * 3 * H + 2 * H + j];
-    if (tid < H) hs[0][tid] = (_Float16)0.f;
-
-    // staging: element e = tid + 1024 i of a block is (row e / S, time offset
-    // e % S): consecutive lanes read consecutive times of one row
-    // (uniform buffer resources + 32-bit offsets: 64-bit per-lane addresses
-    // would not fit the 128-register budget of 4 waves per SIMD)
-    const bool has_res = d.res != nullptr;
-    const __amdgpu_buffer_rsrc_t rgi =
-        ou_rsrc(d.gi + (int64_t)b * d.gi_bstride + (int64_t)dir * 3 * H * T, (int64_t)3 * H * T * 4);
-    const __amdgpu_buffer_rsrc_t rres =
-        ou_rsrc(has_res ? d.res + (int64_t)b * d.res_bstride + (int64_t)dir * H * d.res_cstride : d.gi,
-                has_res ? ((int64_t)(H - 1) * d.res_cstride + T) * 4 : 0);
-    const __amdgpu_buffer_rsrc_t ry =
-        ou_rsrc(d.y + (int64_t)b * d.y_bstride + (int64_t)dir * H * d.y_cstride, ((int64_t)(H - 1) * d.y_cstride + T) * 4);
-    const int rcs = has_res ? (int)d.res_cstride : 0, ycs = (int)d.y_cstride;
-    auto block_base = [&](int k) { return dir == 0 ? S * k : T - S * (k + 1); };   // time of offset 0
-    // gi / residual of block k -> gbuf[buf] by LDS-DMA (no registers): element
-    // e = tid + 1024 i = (row e / S, offset e % S) lands at gbuf[buf][e]
-    auto stage = [&](int k, int buf) {
-        const int tb = block_base(k);
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int e = tid + 64 * kCuWaves * i, row = e / S, o = e - row * S;
-            const int tm = min(max(tb + o, 0), T - 1);   // offsets outside [0, T) are never read
-            const unsigned lds = OU_LDS_ADDR(&gbuf[buf][wave * 64 + 64 * kCuWaves * i]);
-            if (row < 3 * H)
-                ou_blds4(rgi, 4u * (uint32_t)(row * T + tm), 0, lds);
-            else   // no residual: a 0-byte resource lands zeros
-                ou_blds4(rres, 4u * (uint32_t)((row - 3 * H) * rcs + tm), 0, lds);
-        }
-    };
-    auto flush_y = [&](int k, int buf) {   // y of block k, lanes along time
-        const int tb = block_base(k);
-#pragma unroll
-        for (int i = 0; i < H * S / (64 * kCuWaves); ++i) {
-            const int e = tid + 64 * kCuWaves * i, row = e / S, o = e - row * S, tm = tb + o;
-            if (tm >= 0 && tm < T)
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ybuf[buf][row * (S + 1) + o]), ry,
-                                                      4u * (uint32_t)(row * ycs + tm), 0, 0);
-        }
-    };
-    const int nblk = (T + S - 1) / S;
-    stage(0, 0);
-    OU_WAIT_VMCNT0();
-    float hp = 0.f;
-    __syncthreads();
-
-    for (int k = 0; k < nblk; ++k) {
-        const int cur = k & 1;
-        for (int s = 0; s < S; ++s) {
-            const int t = S * k + s;
-            if (t >= T) break;   // uniform: the last block may be short
-            if (s == 0) {
-                if (k + 1 < nblk) stage(k + 1, cur ^ 1);
-                if (k > 0) flush_y(k - 1, cur ^ 1);
-            }
-            const int o = dir == 0 ? s : S - 1 - s;
-            // this lane's k-slice of h_{t-1}: 32 halves, read as two halves of
-            // 2 x ds_read_b128 each (16 live registers would spill at 128 VGPRs)
-            const uint4* hq = (const uint4*)(hs[t & 1] + 32 * q);
-            float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-                uint32_t h[8];
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const uint4 v = hq[2 * half + i];
-                    h[4 * i] = v.x, h[4 * i + 1] = v.y, h[4 * i + 2] = v.z, h[4 * i + 3] = v.w;
-                }
-#pragma unroll
-                for (int v = 0; v < 6; ++v)
-#pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        acc[v] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, w[v * 16 + 8 * half + i]),
-                                                        __builtin_bit_cast(h2_t, h[i]), acc[v], false);
-                asm volatile("" ::: "memory");   // keep the second half's reads after the first half's use
-            }
-#pragma unroll
-            for (int v = 0; v < 6; ++v) acc[v] = sum8(acc[v]);   // the 8 k-slices of the unit pair (lane bits 0-2)
-            const int u = q & 1;
-            const float ar = u ? acc[3] : acc[0], az = u ? acc[4] : acc[1], an = u ? acc[5] : acc[2];
-            const float* gb = gbuf[cur];
-            const float cr = gb[(0 * H + j) * S + o], cz = gb[(1 * H + j) * S + o], cn = gb[(2 * H + j) * S + o];
-            const float r = fast_sigmoid(cr + (ar + bhr));
-            const float z = fast_sigmoid(cz + (az + bhz));
-            const float n = fast_tanh(cn + r * (an + bhn));
-            const float hn = (1.0f - z) * n + z * hp;
-            hp = hn;
-            if (writer) {
-                hs[(t + 1) & 1][j] = (_Float16)hn;
-                ybuf[cur][j * (S + 1) + o] = has_res ? (hn + gb[(3 * H + j) * S + o]) * d.res_scale : hn;
-            }
-            if (s == S - 1 || t == T - 1) OU_WAIT_VMCNT0();   // this wave's DMA of the next block has landed
-            __syncthreads();
-        }
-    }
-    flush_y(nblk - 1, (nblk - 1) & 1);
-}
-
 template <int H, int NB, int U>
 void launch_u(const ou_gru_desc& d, int nb, int nchains, int flags, hipStream_t s)
 {
@@ -851,30 +697,6 @@ extern "C" int64_t ou_gru_workspace_bytes(int hidden, int batch)
            (int64_t)sizeof(uint64_t);
 }
 
-extern "C" int ou_gru_pack_cu16(const float* w_hh, int hidden, void* out)
-{
-    if (!w_hh || !out || hidden != kCuH) return ou_fail(-1, "gru_pack_cu16: hidden %d (256 only)", hidden);
-    constexpr int H = kCuH;
-    _Float16* o = (_Float16*)out;
-    for (int dir = 0; dir < 2; ++dir)
-        for (int wave = 0; wave < kCuWaves; ++wave)
-            for (int lane = 0; lane < 64; ++lane) {
-                const int q = lane & 7, p = lane >> 3;
-                for (int u = 0; u < 2; ++u)
-                    for (int g = 0; g < 3; ++g)
-                        for (int k = 0; k < 32; ++k) {
-                            const int row = g * H + wave * 16 + 2 * p + u, col = 32 * q + k;
-                            *o++ = (_Float16)w_hh[((int64_t)dir * 3 * H + row) * H + col];
-                        }
-            }
-    return 0;
-}
-
-extern "C" int64_t ou_gru_packed_cu16_bytes(int hidden)
-{
-    return hidden == kCuH ? (int64_t)2 * 3 * hidden * hidden * 2 : 0;
-}
-
 extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
 {
     if (!dp) return ou_fail(-1, "gru: null descriptor");
@@ -890,13 +712,8 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
     if (d.t_begin < 0 || (d.t_end != 0 && (d.t_end <= d.t_begin || d.t_end > d.steps)) || (split && !d.hstate))
         return ou_fail(-1, "gru: bad step range [%d, %d) of %d (hstate %p)", d.t_begin, d.t_end, d.steps,
                        (const void*)d.hstate);
-    if (split && (d.w_hh16 || d.hidden % 64 || (fbits >= 0 && (fbits & 32))))
-        return ou_fail(-2, "gru: a step range needs the k-split kernel (hidden %% 64 == 0, fp32 weights)");
-    if (d.w_hh16) {   // single-CU recurrence on f16 weights (ou_gru_pack_cu16)
-        if (d.hidden != kCuH) return ou_fail(-1, "gru: f16 single-CU recurrence needs hidden 256 (got %d)", d.hidden);
-        hipLaunchKernelGGL(gru_cu_kernel, dim3(2 * d.batch), dim3(64 * kCuWaves), 0, s, d);
-        return ou_check_launch("gru");
-    }
+    if (split && (d.hidden % 64 || (fbits >= 0 && (fbits & 32))))
+        return ou_fail(-2, "gru: a step range needs the k-split kernel (hidden %% 64 == 0)");
     if (!d.w_hh || !d.granules || !d.status) return ou_fail(-1, "gru: invalid descriptor");
     // the k-split kernel clears its placement slots when it exits.  A launch
     // of T steps leaves the tags T - 1 and T - 2 in the two parity slots (it

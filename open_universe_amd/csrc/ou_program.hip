@@ -300,6 +300,18 @@ int ou_program_add(ou_program* p, int op, const void* desc, size_t bytes)
     return 0;
 }
 
+int ou_program_patch(ou_program* p, int index, int op, const void* desc, size_t bytes)
+{
+    if (!p || !desc) return ou_fail(-1, "program_patch: null");
+    if (index < 0 || index >= (int)p->ops.size()) return ou_fail(-1, "program_patch: no op %d", index);
+    if (p->ops[index].kind != op || bytes != p->ops[index].desc.size())
+        return ou_fail(-1, "program_patch: op %d is kind %d (%zu bytes), not %d (%zu bytes)", index,
+                       p->ops[index].kind, p->ops[index].desc.size(), op, bytes);
+    p->ops[index].desc.assign((const unsigned char*)desc, (const unsigned char*)desc + bytes);
+    drop_graph(p);
+    return 0;
+}
+
 int ou_program_size(const ou_program* p) { return p ? (int)p->ops.size() : -1; }
 
 int ou_program_run(ou_program* p, void* stream)

@@ -44,20 +44,16 @@ def default_conv_prec():
 
 
 _PREP_PREC = None     # set by Engine while it packs its weights
-_PREP_STATUS = 0      # device int32* the split-f16 convs flag range errors into
+_PREP_STATUS = 0      # device int32* the split-f16 convs flag range errors into (outside an Engine)
+_PREP_ENGINE = None   # the Engine packing its weights: hands out per-layer range slots
+RANGE_SLOTS = 1024    # per-layer range-flag words after the engine's 4 status words
+_SPLIT_CONSUMERS = {}   # producer's range slot -> the ConvW whose split image it stores
+MAX_SHIFT = 40        # staging exponents past this fall back to f32 operands
 _PREP_KSWS = (0, 0)   # (device float*, bytes): the engine's K-slice workspace
 KSWS_BYTES = 64 << 20
 RS_BIT = 1 << 14      # ConvDesc.tile bit: the register-streamed conv kernel (conv_rkernel)
 
-# Optional per-tensor input exponents for split-f16 (OUHIP_SPLIT_AMAX=1): every
-# conv of a split engine records max |y| of what it stores (ConvDesc.amax_out,
-# one 64-float slot row per output buffer, zeroed by the plan's first op); a
-# split-f16 conv whose input buffer was produced by an earlier recorded conv
-# reads that row (amax_in) to pick its staging exponent.  Off by default: the
-# fixed exponent covers |x| < 2^21 (a range flag reruns anything beyond in
-# f32) and the atomics cost 1-11 us per launch (tools/conv_bench.py --amax).
-AMAX_SLOTS = 256
-_REC = None
+_REC = None   # set while a plan records (begin_record)
 # lane the recorder is on (plan lanes run concurrently) and the plan slot
 # (plans of one model that may run at the same time on different streams,
 # Universe.enhance_many): convs recorded on (slot, lane) use K-slice workspace
@@ -82,36 +78,74 @@ def overlap_enabled():
     return os.environ.get("OUHIP_OVERLAP", "1") != "0"
 
 
-def st_lane_enabled():
-    """OUHIP_ST_LANE=0 keeps the conditioner's st_convs on its own lane."""
+def split_images_enabled():
+    """OUHIP_SPLIT_IMAGES=0 keeps every conv on its own f32 staging."""
     import os
 
-    return os.environ.get("OUHIP_ST_LANE", "1") != "0"
+    return os.environ.get("OUHIP_SPLIT_IMAGES", "1") != "0"
 
 
-def split_amax_enabled():
-    import os
-
-    return os.environ.get("OUHIP_SPLIT_AMAX", "0") == "1"
+_REC_DEVICE = None   # the recording engine's device (split-image buffers outside an arena)
 
 
-def begin_record(pool, prec):
-    global _REC
-    _REC = {"pool": pool, "slots": {}, "prec": prec} if prec == 1 and split_amax_enabled() else None
+def begin_record(prec, device=None):
+    global _REC, _REC_DEVICE
+    _REC = {"prec": prec}
+    _REC_DEVICE = device
+    L.ADD_HOOK = split_hook if prec == 1 and split_images_enabled() else None
 
 
 def end_record():
     global _REC
     _REC = None
+    L.ADD_HOOK = None
 
 
-def _amax_slot(act):
-    rec = _REC
-    i = rec["slots"].get(act.ptr)
-    if i is None:
-        i = rec["slots"][act.ptr] = len(rec["slots"])
-        assert i < AMAX_SLOTS, "amax slot pool exhausted"
-    return rec["pool"].data_ptr() + 4 * 64 * i
+# Split images (include/ouhip.h, ou_conv_desc.sy / xs).  A conv whose input
+# is the output of the conv recorded just before it on the same lane reads
+# that producer's split image -- the PReLU'd, scaled, f16 hi / lo operand the
+# producer's epilogue stores beside y -- through the split-image kernel (tile
+# bit 15), whose staging is then a plain copy.  The staging exponent of that
+# consumer (ou_conv_desc.xs_shift) defaults to the fixed 2^-6 of the f32
+# staging path.
+SPLIT_SHIFT = 6
+
+
+def split_hook(prog, d):
+    """Program.add hook (split-f16 plans): link conv ``d`` to the split image
+    of the lane's previous op when that op is the conv that produced d's input."""
+    wn = getattr(d, "_w_nat", None)
+    if (wn is None or d.prec != 1 or d.xs or d.in_scale or d.f0 or d.cin % 32
+            or getattr(d, "_full", None) is not None):
+        return
+    pv = prog.prev_conv.get(prog.cur_lane)
+    if pv is None:
+        return
+    idx, p = pv
+    if (p is d or p.prec != 1 or p.rout != 1 or p.m % 32 or p.sy or p.f0
+            or getattr(p, "_full", None) is not None or p.y != d.x or p.y_bstride != d.x_bstride
+            or p.y_cstride != d.x_cstride or p.out_len < d.in_len or p.batch < d.batch or p.m != d.cin):
+        return
+    rows = p.out_len
+    per_item = (p.m // 32) * rows * 128
+    # one image per (activation buffer, lane): every step of the score loop
+    # rewrites the same activations in order on one lane, so their images too
+    key = (p.y, p.y_bstride, p.y_cstride, rows, p.m, p.batch, prog.cur_lane)
+    cache = prog.__dict__.setdefault("split_bufs", {})
+    buf = cache.get(key)
+    if buf is None:
+        buf = cache[key] = empty((p.batch * per_item // 2,), dtype=torch.int16, device=_REC_DEVICE)
+        prog.keep.append(buf)
+    prog.__dict__.setdefault("split_links", []).append((idx, len(prog.flops)))
+    shift = d.xs_shift   # the consumer's exponent
+    if p.status and getattr(d, "_cw", None) is not None:
+        _SPLIT_CONSUMERS[p.status] = d._cw   # a split-image range code 2 of p widens d's layer
+    p.sy, p.sy_bstride, p.sy_rows, p.sy_shift, p.sy_slope = buf.data_ptr(), per_item, rows, shift, d.slope
+    prog.patch(idx, L.OP_CONV, p)
+    d.xs, d.xs_bstride, d.xs_rows, d.xs_shift = p.sy, per_item, rows, shift
+    d.w, d.w_unscale = wn
+    if d.tile >= 0 and not d.tile & L.SS_BIT:
+        d.tile = -1
 
 
 # ---------------------------------------------------------------------------
@@ -152,6 +186,9 @@ class ConvW:
     status: int = 0          # device int32* for the split-f16 range flag (0 = none)
     ks_ws: tuple = (0, 0)    # K-slice workspace (ptr, bytes) shared by the engine's convs
     cm: bool = False         # rout > 1: channel-major rows (m = co * rout + ph; ConvDesc.rout < 0)
+    w_nat: Optional[torch.Tensor] = None   # prec 1, cin % 32 == 0: ou_conv_pack_split_nat (split-image kernel)
+    w_unscale_nat: float = 1.0
+    xshift: int = 6          # split-f16 staging exponent of this conv's input (ConvDesc.xs_shift)
 
     @property
     def cout(self):
@@ -193,9 +230,26 @@ def make_conv(spec, device, prec=None):
         packed_np, unscale = L.conv_pack(w_logical, cc), 1.0
     packed = torch.from_numpy(packed_np).to(device)
     b = None if spec.bias is None else torch.from_numpy(np.ascontiguousarray(spec.bias, np.float32)).to(device)
-    return ConvW(m, spec.cin, kt, spec.frame, spec.pad, spec.rout, float(spec.slope), cc, packed, b,
-                 spec.shift, spec.ref_macs, int(prec), float(unscale), _PREP_STATUS if prec else 0,
-                 _PREP_KSWS, cm=bool(spec.cm))
+    w_nat, unscale_nat = None, 1.0
+    if prec == 1 and spec.cin % 32 == 0 and kt in (1, 3, 5) and split_images_enabled():
+        nat_np, unscale_nat = L.conv_pack_split_nat_np(w_logical)
+        w_nat = torch.from_numpy(nat_np).to(device)
+    cw = ConvW(m, spec.cin, kt, spec.frame, spec.pad, spec.rout, float(spec.slope), cc, packed, b,
+               spec.shift, spec.ref_macs, int(prec), float(unscale), _PREP_STATUS if prec else 0,
+               _PREP_KSWS, cm=bool(spec.cm), w_nat=w_nat, w_unscale_nat=float(unscale_nat))
+    if prec:
+        cw.status = _range_slot(cw) or cw.status
+    return cw
+
+
+def _range_slot(owner):
+    """A range-flag word of its own for a split-f16 layer of the packing
+    Engine (its device address), so that a range error names the layer."""
+    eng = _PREP_ENGINE
+    if eng is None or len(eng.range_owners) >= RANGE_SLOTS:
+        return 0
+    eng.range_owners.append(owner)
+    return eng.status.data_ptr() + 4 * (3 + len(eng.range_owners))
 
 
 def _slope(sd, p):
@@ -244,12 +298,11 @@ def spec_up(sd, p, r, antialias):
     """Transposed PReLU_Conv(2C, C, r, stride=r) (+ FIR after, blocks.py:221-225)
     as a polyphase convolution over input frames producing r*C rows that the
     kernel's epilogue pixel-shuffles.  weight_norm dim 0 of a ConvTranspose1d
-    weight (Cin, Cout, r) is per input channel; fold_weight handles it.  At
-    r >= 2 (OUHIP_UP_CM_MIN_RATE) the rows are channel-major (m = co * r + ph,
-    ConvDesc.rout = -r): a lane's consecutive accumulator rows are consecutive
-    output samples, stored as one 16-B access at r = 4 and completing whole
-    output lines within one wave at r = 5.  OUHIP_UP_CM=0 keeps phase-major
-    rows everywhere."""
+    weight (Cin, Cout, r) is per input channel; fold_weight handles it.  The
+    rows are channel-major (m = co * r + ph, ConvDesc.rout = -r): a lane's
+    consecutive accumulator rows are consecutive output samples, stored as
+    one 16-B access at r = 4 and completing whole output lines within one
+    wave at r = 5 (faster at rate 2 too: profiles/bench_ab_upcm_rate_r03p.txt)."""
     w = fold_weight(sd, p + ".conv").astype(np.float64)  # (Cin, Cout, r)
     cin, cout, _ = w.shape
     if antialias:
@@ -261,22 +314,17 @@ def spec_up(sd, p, r, antialias):
                 d = s_ // r
                 e = s_ - d * r
                 wl[ph, :, :, d + 1] += fir[j] * w[:, :, e].T
-        cm = UP_CM and r >= UP_CM_MIN_RATE
+        cm = r >= 2
         if cm:
             wl = wl.transpose(1, 0, 2, 3)
         return ConvSpec(np.ascontiguousarray(wl).reshape(r * cout, cin, 3), cin, 1, 1, r, _slope(sd, p),
                         _bias(sd, p + ".bias"), ref_macs=float(cin * cout * r + cout * (2 * r + 1) * r), cm=cm)
     wl = w.transpose(2, 1, 0)   # (r, cout, cin)
-    cm = UP_CM and r >= UP_CM_MIN_RATE
+    cm = r >= 2
     if cm:
         wl = wl.transpose(1, 0, 2)
     return ConvSpec(np.ascontiguousarray(wl).reshape(r * cout, cin, 1), cin, 1, 0, r, _slope(sd, p),
                     _bias(sd, p + ".conv.bias"), ref_macs=float(cin * cout * r), cm=cm)
-
-
-UP_CM = os.environ.get("OUHIP_UP_CM", "1") != "0"
-# channel-major rows from this rate on (C2: rate 2 too measured faster, profiles/bench_ab_upcm_rate_r03p.txt)
-UP_CM_MIN_RATE = int(os.environ.get("OUHIP_UP_CM_MIN_RATE", "2"))
 
 
 def prep_same(sd, p, k, device):
@@ -307,6 +355,8 @@ class FusedW:
     offs: tuple              # byte offsets of the three packed convs in w
     unscale: tuple
     prec: int
+    shifts: list = field(default_factory=lambda: [6, 6, 6, 6])   # conv1 / 2 / 3 / down staging exponents
+    status: int = 0          # its range-flag word (ou_block codes 1 / 2 / 8 / 16)
 
 
 @dataclass
@@ -338,7 +388,7 @@ class BlockW:
 def fuse_blocks_enabled():
     import os
 
-    return os.environ.get("OUHIP_FUSE_BLOCKS", "1") != "0" and not split_amax_enabled()
+    return os.environ.get("OUHIP_FUSE_BLOCKS", "1") != "0"
 
 
 def fuse_ends_enabled():
@@ -365,7 +415,10 @@ def prep_fused(specs, C, prec, device):
         uns.append(un)
         off += packed.nbytes
     w = torch.from_numpy(np.concatenate(parts)).to(device)
-    return FusedW(w, tuple(offs), tuple(uns), prec)
+    fw = FusedW(w, tuple(offs), tuple(uns), prec)
+    if prec:
+        fw.status = _range_slot(fw) or _PREP_STATUS
+    return fw
 
 
 def fuse_down_enabled():
@@ -407,34 +460,10 @@ def prep_block(sd, p, kind, rate, antialias, device):
 class GruW:
     hidden: int
     layers: List  # per layer: (ConvW input projection, w_hh dev [2][3H][H], b_hh dev [2][3H])
-    w16: List = field(default_factory=list)   # per layer: ou_gru_pack_cu16 weights (f16 mode) or None
-
-
-def gru_cu16_enabled():
-    """OUHIP_GRU_CU16=1 runs the f16 operand mode's recurrence on the
-    single-CU f16 kernel (ou_gru_pack_cu16).  Off by default: measured
-    1.59 us per step against 0.79 us for the k-split kernel."""
-    import os
-
-    return os.environ.get("OUHIP_GRU_CU16", "0") == "1"
-
-
-def pack_gru_cu16(w_hh, hidden):
-    """w_hh [2][3H][H] f32 (host) -> the single-CU f16 recurrence's packing."""
-    import ctypes
-
-    lib = L.load()
-    n = lib.ou_gru_packed_cu16_bytes(hidden)
-    assert n > 0, hidden
-    w = np.ascontiguousarray(w_hh, dtype=np.float32)
-    out = np.empty(n // 2, dtype=np.float16)
-    L.check(lib.ou_gru_pack_cu16(w.ctypes.data_as(ctypes.c_void_p), hidden, out.ctypes.data_as(ctypes.c_void_p)),
-            "gru_pack_cu16")
-    return out
 
 
 def prep_gru(sd, p, num_layers, device):
-    layers, w16 = [], []
+    layers = []
     for l in range(num_layers):
         s, sr = f"_l{l}", f"_l{l}_reverse"
         w_ih = np.concatenate([_np(sd[p + ".weight_ih" + s]), _np(sd[p + ".weight_ih" + sr])], 0)
@@ -444,15 +473,9 @@ def prep_gru(sd, p, num_layers, device):
         w_hh = torch.stack([sd[p + ".weight_hh" + s], sd[p + ".weight_hh" + sr]]).detach().to(
             "cpu", torch.float32).contiguous()
         b_hh = torch.stack([sd[p + ".bias_hh" + s], sd[p + ".bias_hh" + sr]]).float().contiguous().to(device)
-        # the f16 operand mode (BASELINE configs[4]) runs the recurrence on f16
-        # weights in one CU per direction (ou_gru_pack_cu16, hidden 256)
-        cu16 = None
-        if proj.prec == 2 and w_hh.shape[-1] == 256 and gru_cu16_enabled():
-            cu16 = torch.from_numpy(pack_gru_cu16(w_hh.numpy(), 256)).to(device)
-        w16.append(cu16)
         layers.append((proj, w_hh.to(device), b_hh))
     H = int(sd[p + ".weight_hh_l0"].shape[1])
-    return GruW(H, layers, w16)
+    return GruW(H, layers)
 
 
 # ---------------------------------------------------------------------------
@@ -543,13 +566,12 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
     d.in_scale, d.slope = in_scale or 0, cw.slope
     d.w, d.m, d.kt, d.pad, d.cc = cw.w.data_ptr(), cw.m, cw.kt, cw.pad, cw.cc
     d.prec, d.w_unscale, d.status = cw.prec, cw.w_unscale, cw.status
+    d.xs_shift = cw.xshift
+    d._w_nat = (cw.w_nat.data_ptr(), cw.w_unscale_nat) if cw.w_nat is not None else None
+    d._cw = cw
     d.ks_ws, d.ks_ws_bytes = cw.ks_ws
     if (_LANE or _SLOT) and d.ks_ws:   # the engine allocates MAX_SLOTS x MAX_LANES workspaces
         d.ks_ws += (_SLOT * MAX_LANES + _LANE) * d.ks_ws_bytes
-    if _REC is not None and _REC["prec"] == 1:
-        if cw.prec == 1 and x.ptr in _REC["slots"]:
-            d.amax_in = _amax_slot(x)
-        d.amax_out = _amax_slot(y)
     if n_frames is None:
         n_frames = -(-d.in_len // cw.frame) if cw.rout == 1 else x.T
     d.n_frames = n_frames
@@ -727,7 +749,9 @@ def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film
     if res2 is not None:
         assert res2.C == bw.C and res2.T >= h.T and res2.ptr != out.ptr
         d.res2, d.r2_bstride, d.r2_cstride = res2.ptr, res2.bs, res2.cs
-    d.status = bw.conv1.status or 0
+    d.status = fw.status or bw.conv1.status or 0
+    for i in range(4):
+        d.shift[i] = fw.shifts[i]
     if x_in is not None:
         xa, scale, w_in, b_in = x_in
         assert bw.C == 32 and xa.C == 1 and xa.T == h.T and xa.B >= h.B
@@ -758,13 +782,6 @@ def rec_gru_ws_zero(prog, granules):
     launches recorded after it (with _GRU_WS_ZEROED) then skip their own
     memset (ou_gru_desc.ws_zeroed)."""
     prog.add(L.OP_MEMSET, L.MemsetArgs(ptr=granules.data_ptr(), bytes=granules.numel() * granules.element_size()))
-
-
-# XCD offset of the conditioner's GRU chains (ou_gru_desc.flags bits 12-14),
-# which run beside the first score step's GRU (chains on XCDs 0 and 1).  Off:
-# XCDs 2-3 measured the same (conditioner GRU layer 1 664 us either way,
-# profiles/ab_r04_summary.txt)
-COND_GRU_XCD = int(os.environ.get("OUHIP_COND_GRU_XCD", "0"))
 
 
 def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, res: Act = None,
@@ -799,12 +816,8 @@ def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, re
     if steps is not None:
         assert hstate is not None and hstate.numel() >= x.B * 2 * H and 0 <= steps[0] < steps[1] <= x.T
         d.t_begin, d.t_end, d.hstate = steps[0], steps[1], hstate.data_ptr()
-    if gw.w16 and gw.w16[layer] is not None:
-        d.w_hh16 = gw.w16[layer].data_ptr()
     d._flops = 2.0 * 2 * 3 * H * H * (x.T if steps is None else steps[1] - steps[0]) * x.B
     prog.add(L.OP_GRU, d)
-    if _REC is not None:   # y now holds GRU values its amax row has not seen
-        _REC["slots"].pop(y.ptr, None)
 
 
 def level_lengths(T, rates):
@@ -860,7 +873,7 @@ class ConvTuner:
     def geometry(d):
         # bool(ks_ws): K-slice tiles are only valid with a workspace
         return (d.m, d.cin, d.frame, d.kt, d.pad, d.batch, d.rout, bool(d.res1), bool(d.film), bool(d.res2),
-                bool(d.in_scale), d.prec, bool(d.amax_out), bool(d.ks_ws))
+                bool(d.in_scale), d.prec, bool(d.ks_ws), bool(d.xs))
 
     @classmethod
     def key(cls, d):
@@ -897,22 +910,22 @@ class ConvTuner:
         self.timed += 1
         # tile shape x log2(output tiles per workgroup); > 0 = persistent kernel
         # (bit 10: the warp-specialised persistent kernel)
-        # (split-f16, bit 11 in the query only, and amax tracking: one-tile workgroups)
+        # (split-f16, bit 11 in the query only: one-tile workgroups)
         # K slices (bits 12-13) for one-tile shapes when the engine has a
         # workspace; ou_conv refuses slices beyond the chunk count or workspace
         # only where the grid is small (about 64 x 64 output tiles: under ~4
         # workgroups per CU); elsewhere slices only add traffic
         small = -(-d.n_frames // 64) * -(-d.m // 64) * d.batch <= 1024
         ksl = (0, 1 << 12, 2 << 12, 3 << 12) if d.ks_ws and small else (0,)
-        if d.prec in (1, 2):
+        if d.xs:   # a split-image input: the split-image kernel's shapes only
+            cands = [t | L.SS_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | L.SS_BIT)]
+        elif d.prec in (1, 2):
             cands = [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))
                      for k in ksl]
             # register-streamed kernel (tile bit 14): whole input windows
             # staged once; ou_conv refuses the shapes whose window exceeds LDS
-            if d.cin % 16 == 0 and not d.amax_in:
+            if d.cin % 16 == 0:
                 cands += [t | RS_BIT | k for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | RS_BIT) for k in ksl]
-        elif d.amax_out:
-            cands = [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t) for k in ksl]
         else:
             cands = [t | v for t in range(lib.ou_conv_num_tiles()) for v in (0, 1 << 8, 2 << 8, 1 << 10)
                      if lib.ou_conv_tile_ok(d.kt, t | v)]
@@ -920,8 +933,10 @@ class ConvTuner:
                       for k in ksl[1:]]
         log = os.environ.get("OUHIP_TUNE_LOG")
         # candidates run on whatever the buffers hold at record time: keep
-        # their split-f16 range flags out of the engine's status word
+        # their split-f16 range flags out of the engine's status word (and
+        # the timing programs out of the recorder's split-image linking)
         status, d.status = d.status, None
+        hook, L.ADD_HOOK = L.ADD_HOOK, None
         for t in cands:
             d.tile = t
             if log:   # diagnostics: name every candidate before it runs
@@ -968,6 +983,7 @@ class ConvTuner:
                 best, best_ms = t, ms
         d.tile = -1
         d.status = status
+        L.ADD_HOOK = hook
         self.cache[k] = best
         self.by_geom.setdefault(k[:-1], set()).add(k[-1])
         if os.environ.get("OUHIP_TUNE_VERBOSE", "1") != "0":   # progress (long plan builds)
@@ -1001,7 +1017,7 @@ def enable_autotune(flag=True):
 class Engine:
     def __init__(self, model_cfg, sd, device, parts=("score", "cond", "sdl"), _record_only=False,
                  conv_prec=None):
-        global _PREP_PREC, _PREP_STATUS, _PREP_KSWS
+        global _PREP_PREC, _PREP_STATUS, _PREP_KSWS, _PREP_ENGINE
         self.device = torch.device(device)
         self.conv_prec = default_conv_prec() if conv_prec is None else int(conv_prec)
         if self.device.type != "cuda" and not _record_only:
@@ -1022,14 +1038,17 @@ class Engine:
         sp = "_edm_model" if self.edm is not None else "score_model"
         dev = self.device
         self.has_sdl = False
-        # [0] GRU hand-off timeout, [1] split-f16 conv range error (plan.check)
-        self.status = torch.zeros(4, dtype=torch.int32, device=dev)
+        # [0] GRU hand-off timeout, [1] split-f16 range error of a layer
+        # without a slot of its own; [4 + i] the range codes of layer i
+        # (range_owners[i]: a ConvW or FusedW), see plan.check / widen_ranges
+        self.status = torch.zeros(4 + RANGE_SLOTS, dtype=torch.int32, device=dev)
+        self.range_owners = []
         # K-slice partial sums (ou_conv tile bits 12-13): ops of one lane run
         # one after another, so the convs of a lane share one buffer (one per
         # plan lane: conv_desc offsets by the recording lane)
         self.ks_ws = torch.empty(MAX_SLOTS * MAX_LANES * KSWS_BYTES // 4, dtype=torch.float32, device=dev)
-        saved = _PREP_PREC, _PREP_STATUS, _PREP_KSWS
-        _PREP_PREC, _PREP_STATUS = self.conv_prec, self.status.data_ptr() + 4
+        saved = _PREP_PREC, _PREP_STATUS, _PREP_KSWS, _PREP_ENGINE
+        _PREP_PREC, _PREP_STATUS, _PREP_ENGINE = self.conv_prec, self.status.data_ptr() + 4, self
         _PREP_KSWS = (self.ks_ws.data_ptr(), KSWS_BYTES)
         try:
             with torch.no_grad():
@@ -1040,8 +1059,46 @@ class Engine:
                 if "sdl" in parts:
                     self._prep_sdl(sd, "signal_decoupling_layer", dev)
         finally:
-            _PREP_PREC, _PREP_STATUS, _PREP_KSWS = saved
+            _PREP_PREC, _PREP_STATUS, _PREP_KSWS, _PREP_ENGINE = saved
         enable_autotune(self.device.type == "cuda")
+
+    def widen_ranges(self, flags, step=8):
+        """A range error's per-layer codes [(slot, code)] (plan.check): widen
+        the staging exponent of every operand whose finite values left the
+        split-f16 range by 2^step -- the conv's own input (code 1), the input
+        of the conv it stores a split image for (2), a fused block's conv1 /
+        conv2 / conv3 / down input (1 / 2 / 8 / 16).  Codes 4 alone (an
+        infinite value: an overflow upstream) widen nothing.  Returns the
+        number of exponents widened; 0 (nothing to widen, or an exponent past
+        MAX_SHIFT) means the caller falls back to f32 operands.  Plans must
+        be recorded again: the exponents are read at record time."""
+        n = 0
+        for slot, code in flags:
+            if slot < 0 or slot >= len(self.range_owners):
+                return 0
+            own = self.range_owners[slot]
+            targets = []
+            if isinstance(own, FusedW):
+                targets = [("f", own, i) for i, bit in enumerate((1, 2, 8, 16)) if code & bit]
+            else:
+                if code & 1:
+                    targets.append(("c", own, 0))
+                if code & 2:
+                    cons = _SPLIT_CONSUMERS.get(own.status)
+                    if cons is None:
+                        return 0
+                    targets.append(("c", cons, 0))
+            for kind, o, i in targets:
+                if kind == "f":
+                    o.shifts[i] += step
+                    if o.shifts[i] > MAX_SHIFT:
+                        return 0
+                else:
+                    o.xshift += step
+                    if o.xshift > MAX_SHIFT:
+                        return 0
+                n += 1
+        return n
 
     # -------------------------------------------------------------- weights
     def _prep_score(self, sd, p, dev):
@@ -1294,8 +1351,7 @@ class Engine:
         Ts = level_lengths(T, self.rates)
         T4 = Ts[nr]
         gw = self.s_gru
-        if (T4 < 96 or _REC is not None or gw.hidden % 64 or (GRU_FLAGS >= 0 and GRU_FLAGS & 32)
-                or any(w is not None for w in (gw.w16 or []))):
+        if T4 < 96 or gw.hidden % 64 or (GRU_FLAGS >= 0 and GRU_FLAGS & 32):
             return None
         b0, bl = self.s_enc[0], self.s_dec[-1]
         if not (fuse_ends_enabled() and self.s_in_fusable and b0.fused is not None and b0.C == 32
@@ -1562,7 +1618,7 @@ class Engine:
         bufs["TB"] = [new_act(B, self.c_dec[l].C, Ts[min(n_lvl - 1 - l, len(rates))], dev) for l in range(n_lvl)]
         return bufs
 
-    def rec_cond(self, prog, bufs, x: Act, need_aux=False, after_level=None, st_lane=None, enc_done=None):
+    def rec_cond(self, prog, bufs, x: Act, need_aux=False, after_level=None, st_lane=None):
         """ConditionerNetwork.forward (condition.py:346-377).  ``after_level(l,
         cond_l)`` runs right after decoder level l has produced its condition.
         With ``st_lane`` (recording on a side lane) the strided st_convs, which
@@ -1579,11 +1635,10 @@ class Engine:
         # ``st_lane`` it runs on a side lane of its own: neither the
         # conditioner's encoder -- the first step's critical path -- nor the
         # earlier st_convs wait for it
-        # OUHIP_MEL_LANE: "2" (default) / "3" a side lane of its own, so the
-        # st_convs do not queue behind it; "1" the st lane; "0" in line on the
-        # conditioner lane
-        ml = os.environ.get("OUHIP_MEL_LANE", "2")
-        mel_lane = None if ml == "0" or st_lane is None else (st_lane if ml == "1" else int(ml))
+        # -- lane 2, so the st_convs do not queue behind it either.  It rejoins
+        # through the last st_conv, so without st_convs (one rate factor) it
+        # stays in line.
+        mel_lane = 2 if st_lane is not None and nr >= 2 else None
         if mel_lane is not None and mel_lane not in (st_lane, 0):
             ev_m = prog.signal()   # a side lane starts by waiting on the conditioner lane
         if mel_lane is not None:
@@ -1658,15 +1713,12 @@ class Engine:
             raise NotImplementedError("conditioner without extra_conv_block")
         prog.label = "cond cb1"
         rec_block(prog, self.c_cb1, bufs["OUT"], bufs["CB1"], bufs["LA"], bufs["LB"])
-        if enc_done is not None:
-            enc_done()
         prog.label = "cond gru1"
-        rec_gru(prog, self.c_gru, 0, bufs["CB1"], bufs["GI"], bufs["G1"], bufs["gran"], self.status,
-                xcd=COND_GRU_XCD)
+        rec_gru(prog, self.c_gru, 0, bufs["CB1"], bufs["GI"], bufs["G1"], bufs["gran"], self.status)
         res = bufs["CB1"] if self.c_gru_res else None
         prog.label = "cond gru2"
         rec_gru(prog, self.c_gru, 1, bufs["G1"], bufs["GI"], bufs["G2"], bufs["gran"], self.status,
-                res=res, res_scale=NF2, xcd=COND_GRU_XCD)
+                res=res, res_scale=NF2)
         prog.label = "cond cb2"
         rec_block(prog, self.c_cb2, bufs["G2"], bufs["H"], bufs["LA"], bufs["LB"])
         # decoder (condition.py:264-270)

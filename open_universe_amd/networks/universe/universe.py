@@ -85,8 +85,9 @@ class Universe(nn.Module):
         self._engine = None
         self._plans = collections.OrderedDict()   # LRU of recorded plans, see _plan()
         self._inflight = set()   # plan keys submitted by enhance_many and not yet checked
-        self._conv_prec = None   # None: OUHIP_CONV_PREC; 0 after a split-f16 range error
+        self._conv_prec = None   # None: OUHIP_CONV_PREC; 0 after a range error no exponent widening fixed
         self.range_fallbacks = 0   # enhance()/enhance_many() calls rerun with f32 operands
+        self.range_widenings = 0   # reruns after widening the staging exponents of named layers
 
     def init_losses(self, score_model, condition_model, losses, training):
         """Training losses are out of scope; nothing to build for Universe."""
@@ -304,15 +305,16 @@ class Universe(nn.Module):
             plan = self._arena_plan(key, 0, make_plan)
             try:
                 x = plan(mix, rng, clone=True)[:, None, :]
-            except L.OuRangeError:
-                # a split-f16 conv input left its range (|x| >= 2^21): switch
-                # this model to f32 operands and rerun on the same noise
+            except L.OuRangeError as e:
+                # a split-f16 operand left its range: widen the exponents of
+                # the layers it names and rerun on the same noise
                 nz = plan.NZ.clone()
-                self._conv_prec = 0
-                self.range_fallbacks += 1
-                self.invalidate()
-                plan = self._arena_plan(key, 0, make_plan)
-                x = plan.run_with_noise(mix, nz).clone()[:, None, :]
+
+                def rerun():
+                    p = self._arena_plan(key, 0, make_plan)
+                    return p.run_with_noise(mix, nz).clone()[:, None, :]
+
+                x = self._range_recover(e, rerun)
         if x_ndim == 1:
             x = x[0, 0]
         elif x_ndim == 2:
@@ -385,25 +387,48 @@ class Universe(nn.Module):
                 plan.check()   # synchronises; the status word is shared by the engine's plans
             finally:
                 self._inflight.clear()
-        except L.OuRangeError:
-            # as enhance(): a split-f16 input left its range -> f32 operands,
-            # same noise, every clip of the call
-            self._conv_prec = 0
-            self.range_fallbacks += 1
-            self.invalidate()
-            eng = self._get_engine()
-            outs = []
-            for key, m3, nz in pending:
-                B, _, T = m3.shape
-                p0 = self._arena_plan(key[:-2] + (0,), 0,
-                                      lambda ar: EnhancePlan(eng, B, T, int(n_steps), float(epsilon),
-                                                             keep_rms=bool(keep_rms), diff=dict(self.diff_kwargs),
-                                                             arena=ar))
-                outs.append(p0.run_with_noise(m3, nz).clone())
+        except L.OuRangeError as e:
+            # as enhance(): widen the named layers' exponents (or fall back to
+            # f32 operands) and rerun every clip of the call on its noise
+            def rerun():
+                eng = self._get_engine()
+                res = []
+                for key, m3, nz in pending:
+                    B, _, T = m3.shape
+                    p0 = self._arena_plan(key[:-2] + (0,), 0,
+                                          lambda ar: EnhancePlan(eng, B, T, int(n_steps), float(epsilon),
+                                                                 keep_rms=bool(keep_rms), diff=dict(self.diff_kwargs),
+                                                                 arena=ar))
+                    res.append(p0.run_with_noise(m3, nz).clone())
+                return res
+
+            outs = self._range_recover(e, rerun)
         res = []
         for x, nd in zip(outs, shapes):
             res.append(x[0] if nd == 1 else x if nd == 2 else x[:, None, :])
         return res
+
+    def _range_recover(self, err, rerun, rounds=4):
+        """Recover from a split-f16 range error: widen the staging exponents
+        of the layers ``err`` names (Engine.widen_ranges: only those layers,
+        the rest keep 2^-6) and ``rerun()`` -- the same noise, plans recorded
+        again -- until a replay is clean.  An error that names no layer, an
+        exponent past its limit, or ``rounds`` failed reruns switch the model
+        to f32 operands instead (one counted fallback)."""
+        for _ in range(rounds):
+            eng = self._engine
+            if eng is None or not getattr(err, "flags", ()) or not eng.widen_ranges(err.flags):
+                break
+            self.range_widenings += 1
+            self._plans = collections.OrderedDict()   # exponents are read at record time
+            try:
+                return rerun()
+            except L.OuRangeError as e2:
+                err = e2
+        self._conv_prec = 0
+        self.range_fallbacks += 1
+        self.invalidate()
+        return rerun()
 
     @staticmethod
     def _ensemble_reduce(x, stat):

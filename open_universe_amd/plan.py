@@ -48,9 +48,10 @@ def edm_weights(s, level_db, data_level_db=None):
     }
 
 
-# EnhancePlan.__call__ reads the status word through pinned memory after one
-# stream wait, the result copy queued before it (0: blocking read, then copy)
-PINNED_CHECK = os.environ.get("OUHIP_PINNED_CHECK", "1") != "0"
+# EnhancePlan.__call__ reads the status words through pinned memory after one
+# stream wait, the result copy queued before it (+0.6 % over a blocking read,
+# profiles/ab_r04_summary.txt)
+PINNED_CHECK = True
 
 
 class _PlanBase:
@@ -58,13 +59,7 @@ class _PlanBase:
         self.eng = eng
         self.dev = eng.device
         self.prog = L.Program()
-        # split-f16 input exponents (engine.begin_record): slot rows zeroed
-        # by the first op of every launch
-        self.amax = None
-        if eng.conv_prec == 1 and E.split_amax_enabled():
-            self.amax = torch.zeros((E.AMAX_SLOTS, 64), dtype=torch.float32, device=self.dev)
-            self.prog.add(L.OP_MEMSET, L.MemsetArgs(ptr=self.amax.data_ptr(), bytes=self.amax.numel() * 4))
-        E.begin_record(self.amax, eng.conv_prec)
+        E.begin_record(eng.conv_prec, eng.device)
 
     def __init_subclass__(cls, **kw):
         # every subclass records in its __init__: close the recording context
@@ -104,13 +99,17 @@ class _PlanBase:
             self.prog.run(stream)
 
     def check(self, pinned=False):
-        st = self.eng.status
+        """Raise on a GRU hand-off timeout (status word 0) or a split-f16
+        range error: OuRangeError.flags lists the (layer slot, range code)
+        pairs of the engine's per-layer words (Engine.widen_ranges)."""
+        n = 4 + len(self.eng.range_owners)
+        st = self.eng.status[:n]
         if pinned:
-            # one wait: the status word rides to pinned host memory on the
+            # one wait: the status words ride to pinned host memory on the
             # stream behind the replay, instead of a blocking read issued
             # after it (a second host wake-up per call)
             hs = getattr(self.eng, "status_host", None)
-            if hs is None:
+            if hs is None or hs.numel() != n:
                 hs = self.eng.status_host = torch.empty(st.shape, dtype=st.dtype, pin_memory=True)
             hs.copy_(st, non_blocking=True)
             torch.cuda.current_stream(self.dev).synchronize()
@@ -121,7 +120,11 @@ class _PlanBase:
             st.zero_()
             if flags[0]:
                 raise L.OuHipError("GRU recurrence timed out (workgroup hand-off never completed)")
-            raise L.OuRangeError("split-f16 conv input out of range (|x| >= 2^21)")
+            per_layer = [(i - 4, f) for i, f in enumerate(flags) if i >= 4 and f]
+            e = L.OuRangeError("split-f16 operand out of range (range codes %s%s)"
+                               % (per_layer[:8], ", shared word %d" % flags[1] if flags[1] else ""))
+            e.flags = per_layer if not flags[1] else []   # a shared-word flag names no layer
+            raise e
 
 
 class EnhancePlan(_PlanBase):
@@ -210,17 +213,8 @@ class EnhancePlan(_PlanBase):
                 p.label = f"cond sc{l}"
                 p.add(L.OP_CONV, E.conv_desc(eng.s_sc[l], cond, self.SC[l]))
                 ev_cond[l] = p.signal()
-        # OUHIP_SCORE_AFTER_CENC=1: the first score pass starts once the
-        # conditioner's encoder is done (its GRU then runs beside the score
-        # encoder), so the conditioner's encoder -- the first step's critical
-        # path -- does not share the chip with the score encoder
-        ev_cenc = []
-        enc_done = None
-        if self.overlap and os.environ.get("OUHIP_SCORE_AFTER_CENC", "0") == "1":
-            enc_done = lambda: ev_cenc.append(p.signal())
         conds, yaux = eng.rec_cond(p, cb, self.XN, need_aux=use_aux_signal or warm_start is not None,
-                                   after_level=after_level, enc_done=enc_done,
-                                   st_lane=0 if (self.overlap and st_lane and E.st_lane_enabled()) else None)
+                                   after_level=after_level, st_lane=0 if (self.overlap and st_lane) else None)
         if use_aux_signal or warm_start is not None:
             self.AUXT = new_act(B, yaux.C, Tp, dev)
             self.SIG = new_act(B, 1, Tp, dev)
@@ -233,8 +227,6 @@ class EnhancePlan(_PlanBase):
         else:
             if self.overlap:
                 E.set_lane(p, 0)
-                for ev in ev_cenc:
-                    p.wait(ev)
             else:
                 self.SC = eng.alloc_sc(B, Tp)
                 eng.rec_sc(p, conds, self.SC)

@@ -435,6 +435,7 @@ inline void ou_kernarg_prefetch6() {}
 inline void ou_kernarg_prefetch8() {}
 #define OU_WAIT_VMCNT0() emu_wave_sync()
 #define OU_WAIT_VMCNT(n) emu_wave_sync()
+#define OU_WAVE_SYNC() emu_wave_sync()
 
 // the product's uniform-resource helper (ou_common.h), host version
 inline emu_rsrc ou_rsrc(const void* p, long long bytes)

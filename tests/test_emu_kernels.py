@@ -152,3 +152,20 @@ def test_block_values_match_reference(tmp_path):
     for p in procs:
         out, err = p.communicate(timeout=1200)
         assert p.returncode == 0 and "ok:" in out, (out[-2000:], err[-2000:])
+
+
+def test_split_image_values_match_reference(tmp_path):
+    """Fiber emulation of the split-image path, under AddressSanitizer: the
+    consumer kernel (tile bit 15) against a double-precision evaluation at
+    every NR shape (k1/k3/k5, frame views at rates 4 and 5, a transposed
+    channel-major output, a one-chunk layer whose other waves run zero
+    chunks), and the split image every producer kernel family stores
+    (ou_conv_desc.sy) against prelu(y) * 2^-s element by element."""
+    exe = str(tmp_path / "conv_emu_split")
+    _build("conv_emu_split.cpp", exe, *ASAN, "-DOU_EMU_FIBERS")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    procs = [subprocess.Popen([exe, g], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+             for g in ("0", "1", "2", "3", "4", "5", "6", "100")]
+    for p in procs:
+        out, err = p.communicate(timeout=900)
+        assert p.returncode == 0 and "ok:" in out, (out[-2000:], err[-2000:])

@@ -183,36 +183,6 @@ def test_gru_xcd_offset_same_result(pp16, B, xcd):
     assert torch.equal(run(xcd), run(0))
 
 
-@pytest.mark.parametrize("B,T", [(1, 301), (2, 57)])
-def test_gru_layer_f16_single_cu(pp16, B, T):
-    """The f16 operand mode's recurrence (ou_gru with w_hh16: one 1024-thread
-    workgroup per direction, f16 weights and h, f32 accumulation and state)
-    against the fp32 oracle: f16-class agreement (rel-RMS <= 5e-3), with the
-    fused residual."""
-    d, cfg, m = pp16
-    sd = {kk: v.cpu() for kk, v in m.state_dict().items()}
-    saved, E._PREP_PREC = E._PREP_PREC, 2
-    try:
-        with pytest.MonkeyPatch.context() as mp:
-            mp.setenv("OUHIP_GRU_CU16", "1")
-            gw = E.prep_gru(sd, "_edm_model.encoder.gru", 1, DEV)
-    finally:
-        E._PREP_PREC = saved
-    assert gw.w16[0] is not None
-    status = torch.zeros(4, dtype=torch.int32, device=DEV)
-    x = torch.randn(B, 512, T, generator=torch.Generator().manual_seed(9)) * 0.5
-    res = torch.randn(B, 512, T, generator=torch.Generator().manual_seed(10))
-    xa, gi, y = E.Act(x.to(DEV)), E.new_act(B, 1536, T, DEV), E.new_act(B, 512, T, DEV)
-    gran = torch.zeros(L.load().ou_gru_workspace_bytes(256, B) // 8, dtype=torch.int64, device=DEV)
-    prog = L.Program()
-    E.rec_gru(prog, gw, 0, xa, gi, y, gran, status, res=E.Act(res.to(DEV)), res_scale=0.5)
-    prog.run(torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    ref = (O.gru(sd, "_edm_model.encoder.gru", x, 1) + res) * 0.5
-    err = rel_rms(y.t.cpu(), ref)
-    assert err < 5e-3, err
-
-
 # ----------------------------------------------------------------- networks
 @pytest.mark.parametrize("tag,name,nch", [("pp16", "pp16", None), ("pp16_c4", "pp16", 4),
                                           ("orig16_c4", "orig16", 4), ("pp24_c4", "pp24", 4)])
@@ -339,17 +309,23 @@ def test_split_and_f32_operands_agree_full_size(pp16, monkeypatch):
     assert rel_rms(a, b) < 1e-3 and si_sdr(a, b) > 60
 
 
-def test_enhance_split_amax_exponents_vs_reference(monkeypatch):
-    """OUHIP_SPLIT_AMAX=1: split-f16 convs take their staging exponent from the
-    running max their producer recorded (ConvDesc.amax_in/amax_out)."""
-    monkeypatch.setenv("OUHIP_SPLIT_AMAX", "1")
+@pytest.mark.parametrize("shift", [4, 13])
+def test_enhance_widened_exponents_vs_reference(shift):
+    """Every split-f16 operand staged at a non-default exponent (ConvDesc
+    xs_shift / sy_shift, ou_block_desc.shift -- what Engine.widen_ranges
+    moves a flagged layer to): the result scaling 2^(s - 6) is right in every
+    kernel family, and the enhance still matches the reference."""
     d, cfg, m = _model("pp16_c4", "pp16", 4)
+    eng = m._get_engine()
+    for o in eng.range_owners:
+        if hasattr(o, "xshift"):
+            o.xshift = shift
+        else:
+            o.shifts = [shift] * 4
     mix = _dev(d["enh_mix"])
     with torch.no_grad():
         out = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
-    plan = next(iter(m._plans.values()))
-    assert plan.amax is not None and float(plan.amax.max()) > 0
-    assert m._get_engine().conv_prec == 1
+    assert eng.conv_prec == 1 and m.range_fallbacks == 0 and m.range_widenings == 0
     assert rel_rms(out, d["enh_out"]) < 1e-3
     assert si_sdr(out, d["enh_out"]) > 60
 

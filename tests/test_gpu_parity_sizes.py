@@ -163,20 +163,26 @@ def test_full_width_orig16_enhance_8_and_60_steps():
 def test_full_width_pp24_enhance():
     """PP24 at full width (48..768 channels, GRU H = 384).  With the seeded
     synthetic weights the reference's activations reach ~8e6 (fixture
-    enh_peak_activation), beyond the split-f16 range: the range flag fires and
-    the model reruns the same enhance with f32 operands, which must match the
-    reference."""
+    enh_peak_activation), beyond the split-f16 range at the default 2^-6
+    staging exponent: the range flags name the layers, the engine widens only
+    their exponents and reruns the same enhance on split-f16 operands (no f32
+    fallback), which must match the reference."""
     d, cfg, m = _golden_model("pp24", "pp24")
     assert float(d["enh_peak_activation"]) > 2.0**21
     mix = _t(d["enh_mix"]).to(DEV)
     with torch.no_grad():
         out = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
-    assert m._get_engine().conv_prec == 0   # the f32 rerun happened
-    assert m.range_fallbacks == 1            # once, and reported (bench.py "fallbacks")
+    eng = m._get_engine()
+    assert eng.conv_prec == 1 and m.range_fallbacks == 0   # still split-f16
+    assert 1 <= m.range_widenings <= 2                      # reported (bench.py "widenings")
+    wide = [o for o in eng.range_owners if (getattr(o, "xshift", 6) != 6 or any(x != 6 for x in
+                                                                                  getattr(o, "shifts", [6])))]
+    assert 0 < len(wide) < len(eng.range_owners) // 2       # only the flagged layers moved
     assert rel_rms(out, d["enh_out"]) < 1e-3 and si_sdr(out, d["enh_out"]) > 60
-    with torch.no_grad():   # the model stays on f32 operands: no second rerun
+    w0 = m.range_widenings
+    with torch.no_grad():   # the widened exponents stay: no second rerun, same bits
         out2 = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
-    assert m.range_fallbacks == 1 and torch.equal(out2, out)
+    assert m.range_widenings == w0 and m.range_fallbacks == 0 and torch.equal(out2, out)
 
 
 def test_full_width_pp24_damped_split_f16_vs_reference():

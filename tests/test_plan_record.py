@@ -62,23 +62,59 @@ def test_enhance_plan_records_onto_an_arena():
         assert lo <= t.data_ptr() < hi
 
 
-@pytest.mark.parametrize("env", [{}, {"OUHIP_MEL_LANE": "2"}, {"OUHIP_MEL_LANE": "0"},
-                                 {"OUHIP_SCORE_AFTER_CENC": "1"},
-                                 {"OUHIP_MEL_LANE": "2", "OUHIP_SCORE_AFTER_CENC": "1"}])
-def test_lane_schedule_variants_validate(monkeypatch, env):
-    """Every lane schedule of the first step (mel branch in line, on the st
-    lane or a lane of its own; the score pass started after the
-    conditioner's encoder) records a program whose lane structure
+@pytest.mark.parametrize("rates", [None, [4]])
+@pytest.mark.parametrize("env", [{}, {"OUHIP_OVERLAP": "0"}])
+def test_lane_schedules_validate(monkeypatch, env, rates):
+    """The first step's lane schedules (conditioner beside the first score
+    pass, mel branch on a lane of its own, st_convs on the score lane; or
+    everything in line) record a program whose lane structure
     ou_program_validate accepts (host-only: joins, signal-before-wait, no
-    side-lane wait cycles), with the same ops as the default schedule."""
+    side-lane wait cycles), with the same ops either way.  With one rate
+    factor there are no st_convs: the mel branch then stays in line (the
+    last st_conv is what joins its lane)."""
+    from open_universe_amd.networks.universe import UniverseGAN
+    from open_universe_amd.utils.synthetic import synth_state_dict
+
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    d = load_golden("pp16_c4")
-    eng = Engine(get_config("pp16", 4), golden_state_dict(d), "cpu", _record_only=True)
+    cfg = get_config("pp16", 4)
+    if rates is None:
+        sd = golden_state_dict(load_golden("pp16_c4"))
+    else:
+        cfg["score_model"]["rate_factors"] = cfg["condition_model"]["rate_factors"] = rates
+        m = UniverseGAN(**{k: v for k, v in cfg.items() if k != "_target_"})
+        sd = synth_state_dict([(k, v.shape) for k, v in m.state_dict().items() if not k.startswith("loss_")])
+    eng = Engine(cfg, sd, "cpu", _record_only=True)
     plan = EnhancePlan(eng, 1, 3000, 8, 1.3)
     plan.prog.validate()
     kinds = [k for k in plan.prog.op_kinds() if k not in (L.OP_LANE, L.OP_SIGNAL, L.OP_WAIT)]
     for k in env:
         monkeypatch.delenv(k)
     ref = EnhancePlan(eng, 1, 3000, 8, 1.3)
-    assert kinds == [k for k in ref.prog.op_kinds() if k not in (L.OP_LANE, L.OP_SIGNAL, L.OP_WAIT)]
+    ref.prog.validate()
+    # the same ops (in line, the conditioner's ops come in another order)
+    assert sorted(kinds) == sorted(k for k in ref.prog.op_kinds() if k not in (L.OP_LANE, L.OP_SIGNAL, L.OP_WAIT))
+
+
+def test_split_images_link_the_deep_level_convs():
+    """Full-width PP16 (256 / 512-channel levels): every conv whose input the
+    conv just before it on the same lane produced reads that producer's split
+    image (ou_conv_desc.xs), the producer's descriptor is patched to store it
+    (sy), and one image per activation buffer serves all diffusion steps."""
+    d = load_golden("pp16")
+    eng = Engine(get_config("pp16"), golden_state_dict(d), "cpu", _record_only=True)
+    plan = EnhancePlan(eng, 1, 16000, 8, 1.3)
+    links = plan.prog.split_links
+    steps = len(links) // 8
+    assert steps >= 12, len(links)            # per score step: the 256 / 512-channel chains
+    assert len(plan.prog.split_bufs) <= 40    # images shared across the steps
+    for prod, cons in links:
+        assert plan.prog.lanes[prod] == plan.prog.lanes[cons] and prod < cons
+
+
+def test_split_images_off_records_plain_convs(monkeypatch):
+    monkeypatch.setenv("OUHIP_SPLIT_IMAGES", "0")
+    d = load_golden("pp16")
+    eng = Engine(get_config("pp16"), golden_state_dict(d), "cpu", _record_only=True)
+    plan = EnhancePlan(eng, 1, 16000, 8, 1.3)
+    assert not getattr(plan.prog, "split_links", [])

@@ -201,22 +201,6 @@ def test_numpy_block_packing_matches_c():
         assert ua == ub and np.array_equal(a, b)
 
 
-def test_gru_cu16_packing_matches_restatement():
-    """ou_gru_pack_cu16 (the single-CU f16 recurrence's weight order) against
-    a numpy restatement of the order include/ouhip.h documents."""
-    from open_universe_amd import engine as E
-
-    H = 256
-    w = np.random.default_rng(3).standard_normal((2, 3 * H, H)).astype(np.float32) * 0.06
-    got = E.pack_gru_cu16(w, H)
-    # [dir][wave 16][lane 64: p = l >> 3, q = l & 7][u 2][g 3][k 32]
-    d, wv, p, q, u, g, k = np.meshgrid(np.arange(2), np.arange(16), np.arange(8), np.arange(8), np.arange(2),
-                                        np.arange(3), np.arange(32), indexing="ij")
-    want = w[d, g * H + wv * 16 + 2 * p + u, 32 * q + k].astype(np.float16).reshape(-1)
-    assert got.dtype == np.float16 and got.shape == want.shape
-    np.testing.assert_array_equal(got, want)
-
-
 @pytest.mark.parametrize("C,kt", [(32, 5), (48, 3), (64, 3), (96, 5), (192, 3)])
 def test_numpy_block_f32_packing_matches_c(C, kt):
     """ou_block's f32-operand layout (prec 0): the numpy restatement the
@@ -230,3 +214,21 @@ def test_numpy_block_f32_packing_matches_c(C, kt):
     n, un = L.block_pack_f32_np(wp)
     assert uc == un == 64.0
     assert c.shape == n.shape and np.array_equal(c, n)
+
+
+@pytest.mark.parametrize("m,cin,kt", [(32, 32, 5), (64, 160, 3), (1536, 512, 1), (50, 96, 3)])
+def test_numpy_natural_split_packing_matches_c(m, cin, kt):
+    """conv_pack_split_nat_np (what the engine packs for the split-image
+    kernel) is byte-identical to ou_conv_pack_split_nat, and holds the same
+    hi / lo halves as the pair-ordered packing, only permuted."""
+    import numpy as np
+
+    from open_universe_amd import _lib as L
+
+    g = np.random.default_rng(m * cin + kt)
+    w = (g.standard_normal((m, cin, kt)) * 0.05).astype(np.float32)
+    a, ua = L.conv_pack_split(w, natural=True)
+    b, ub = L.conv_pack_split_nat_np(w)
+    assert ua == ub and a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    c, uc = L.conv_pack_split_np(w)
+    assert uc == ua and np.array_equal(np.sort(a.view(np.uint16)), np.sort(c.view(np.uint16)))

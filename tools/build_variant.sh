@@ -3,14 +3,16 @@
 # link it with the other objects of the last full build (csrc/build/) into
 # open_universe_amd/variants/libouhip_NAME.so (gitignored; travels to the GPU
 # box with the tree).  Select one at run time with OUHIP_LIB=<path>.
-#   tools/build_variant.sh NAME SOURCE "FLAGS"     e.g. ring10 ou_block.hip "-DOU_BLOCK_RING1=10"
+#   tools/build_variant.sh NAME SOURCE "FLAGS" [OBJECT]   e.g. ring10 ou_block.hip "-DOU_BLOCK_RING1=10"
+# OBJECT: the build/ object the variant replaces (default SOURCE's), e.g. one
+# tap-count unit of ou_conv.hip:  nb ou_conv.hip "-DOU_CONV_SPLIT_KT=3 -DX=0" ou_conv_k3.o
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 CS="$ROOT/open_universe_amd/csrc"
-NAME="$1"; SRC="$2"; FLAGS="${3:-}"
+NAME="$1"; SRC="$2"; FLAGS="${3:-}"; OBJNAME="${4:-${SRC%.hip}.o}"
 OUT="$ROOT/open_universe_amd/variants"
 mkdir -p "$OUT" "$OUT/obj_$NAME"
-OBJ="$OUT/obj_$NAME/${SRC%.hip}.o"
+OBJ="$OUT/obj_$NAME/$OBJNAME"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function $FLAGS -c "$CS/$SRC" -o "$OBJ"
 objs=()
 for o in "$CS"/build/*.o; do

@@ -67,6 +67,32 @@ def make(name, dev, seed=0):
 GRAPH_COPIES = 20
 
 
+def split_image(x, slope, shift, rows=None):
+    """Host-side (torch) split image of prelu(x) * 2^-shift, include/ouhip.h
+    layout [B][C / 32][rows][hi | lo][32] as int16 (tools and tests only)."""
+    B, C, T = x.shape
+    rows = T if rows is None else rows
+    p = x.float() * 2.0 ** -shift
+    p = torch.where(p >= 0, p, p * slope)
+    hi = p.half()
+    lo = ((p - hi.float()) * 2048.0).half()
+    img = torch.zeros(B, C // 32, rows, 2, 32, dtype=torch.float16, device=x.device)
+    img[:, :, :T, 0, :] = hi.reshape(B, C // 32, 32, T).transpose(2, 3)
+    img[:, :, :T, 1, :] = lo.reshape(B, C // 32, 32, T).transpose(2, 3)
+    return img.view(torch.int16).reshape(-1)
+
+
+def split_variant(d, keep, shift=6):
+    """The same layer reading a split image of its input (tile bit 15)."""
+    cw, x = keep[0], keep[1]
+    img = split_image(x.t, cw.slope, shift)
+    ds = L.ConvDesc.from_buffer_copy(d)
+    ds._flops = d._flops
+    ds.xs, ds.xs_bstride, ds.xs_rows, ds.xs_shift = img.data_ptr(), img.numel() * 2 // x.B, x.T, shift
+    ds.w, ds.w_unscale = cw.w_nat.data_ptr(), cw.w_unscale_nat
+    return ds, img
+
+
 def time_tile_graph(d, tile, reps, stream):
     """Device time per launch: GRAPH_COPIES copies of the op captured in one
     hipGraph (no host launch cost in the figure; K-slice tiles pay their
@@ -123,8 +149,12 @@ def main():
                     help="register-streamed tiles: also time without input loads (bit 8) / without the K loop (bit 9)")
     ap.add_argument("--stamps", action="store_true", help="diag library: per-phase cycles")
     ap.add_argument("--wstamps", action="store_true", help="diag library: warp-specialised kernel phases")
-    ap.add_argument("--amax", action="store_true",
-                    help="split-f16: re-time the best tile with amax_out, then amax_in + amax_out")
+    ap.add_argument("--sstamps", action="store_true",
+                    help="with --split, a library built with -DOU_SK_STAMPS: per-wave phase cycles of the best "
+                         "split-image tile")
+    ap.add_argument("--split", action="store_true",
+                    help="also time the split-image kernel (tile bit 15) on a split image of the input, check its "
+                         "output against the best tile's, and re-time the best tile storing a split image (sy)")
     a = ap.parse_args()
     dev = "cuda:0"
     stream = torch.cuda.current_stream().cuda_stream
@@ -159,16 +189,57 @@ def main():
         line = "  ".join(f"{nm(t)}:{ms * 1e3:.1f}us" for ms, t in res[:40 if a.rdiag else 12])
         print(f"{name:5s} {fl / 1e9:6.2f} GFLOP  best {nm(res[0][1])} {res[0][0] * 1e3:.1f} us "
               f"{fl / res[0][0] / 1e9:.1f} TF/s | {line}", flush=True)
-        if a.amax:
-            slots = torch.zeros(2, 64, device=dev)
-            slots[0] = 1.0
-            d.amax_out = slots[1].data_ptr()
-            t_out = time_tile(d, res[0][1], a.reps, stream)
-            d.amax_in = slots[0].data_ptr()
-            t_both = time_tile(d, res[0][1], a.reps, stream)
-            d.amax_out = d.amax_in = None
-            print(f"      amax: none {res[0][0] * 1e3:.1f} us, out {t_out * 1e3:.1f} us, in+out {t_both * 1e3:.1f} us",
-                  flush=True)
+        if a.split and keep[0].w_nat is not None:
+            import ctypes
+
+            y = keep[2].t
+            d.tile = res[0][1]
+            lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream))
+            torch.cuda.synchronize()
+            yref = y.clone()
+            ds, img = split_variant(d, keep)
+            sres = []
+            for t in range(3):
+                for mj in (0, 1 << 16):
+                    ms = time_tile(ds, L.SS_BIT | t | mj, a.reps, stream)
+                    if ms is not None:
+                        sres.append((ms, L.SS_BIT | t | mj))
+            sres.sort()
+            ds.tile = sres[0][1]
+            y.fill_(float("nan"))
+            assert lib.ou_conv(ctypes.byref(ds), ctypes.c_void_p(stream)) == 0
+            torch.cuda.synchronize()
+            err = ((y - yref).norm() / yref.norm()).item()
+            # the producer side: the best tile storing a split image of its output
+            m_out = keep[0].cout
+            sy = torch.zeros(m_out // 32 * y.shape[-1] * 64 * y.shape[0], dtype=torch.int16, device=dev) \
+                if keep[0].rout == 1 and m_out % 32 == 0 else None
+            t_sy = None
+            if sy is not None:
+                d.sy, d.sy_bstride, d.sy_rows, d.sy_shift, d.sy_slope = sy.data_ptr(), m_out // 32 * y.shape[-1] * 128, \
+                    y.shape[-1], 6, 0.25
+                t_sy = time_tile(d, res[0][1], a.reps, stream)
+                d.sy = None
+            if a.sstamps:
+                st_buf = torch.zeros(1024 * 4 * 8, dtype=torch.int64, device=dev)
+                ds.ks_ws = st_buf.data_ptr()
+                assert lib.ou_conv(ctypes.byref(ds), ctypes.c_void_p(stream)) == 0
+                torch.cuda.synchronize()
+                ds.ks_ws = None
+                st = st_buf.view(1024, 4, 8).cpu().numpy().astype(np.float64)
+                st = st[st[:, :, :4].sum(axis=(1, 2)) > 0]
+                if len(st):
+                    ph = st[:, :, :4].mean(axis=(0, 1))
+                    life = (st[:, :, 7] - st[:, :, 6]).mean() / 100.0
+                    t0 = st[:, :, 6].min()
+                    print(f"      stamps ({len(st)} WGs, cycles per wave): prologue={ph[0]:.0f} main={ph[1]:.0f} "
+                          f"reduce={ph[2]:.0f} epilogue={ph[3]:.0f}; wave lifetime {life:.2f} us; starts "
+                          f"0..{(st[:, :, 6].max() - t0) / 100:.2f} us, last end {(st[:, :, 7].max() - t0) / 100:.2f} us",
+                          flush=True)
+            sl = "  ".join(f"s{t & 0xff}{'m' if t & (1 << 16) else ''}:{ms * 1e3:.1f}us" for ms, t in sres)
+            print(f"      split image: best {sres[0][0] * 1e3:.1f} us {fl / sres[0][0] / 1e9:.1f} TF/s "
+                  f"(rel diff vs best tile {err:.2e}) | {sl}" +
+                  (f" | best tile storing sy: {t_sy * 1e3:.1f} us" if t_sy else ""), flush=True)
         if a.wstamps:
             import ctypes
 

@@ -14,6 +14,8 @@
 #   ab:VAR=[A,]B     C2 bench with VAR=A / B / A / B (A defaults to 0; same box, alternating)
 #   ablib:NAME       C2 bench, in-tree libouhip.so vs variants/libouhip_NAME.so (3 pairs)
 #   convlib:NAME     tools/conv_bench.py deep-level layers, in-tree library vs the variant
+#   convsplit[:L,..] tools/conv_bench.py --split: the split-image kernel on the deep-level layers
+#   convsplitlib:A,B the same on the k3 layers, in-tree library then variants A, B (stamps: --sstamps)
 #
 #   e.g. tools/gpu_run.sh r04k profile:c2 critical bench:c1 bench:c3 bench:c5
 set -o pipefail
@@ -76,6 +78,18 @@ for step in "$@"; do
                   bench "$O/ab_${TAG}_${lib}_$i" 200 --steps 20 --warmup 3 --no-cpu-baseline --no-f32-pass \
                       --no-queued --traffic-json "" ) || exit 1
             done
+        done ;;
+    convsplit)   # tools/conv_bench.py --split on the deep-level layers (split-image kernel vs the best tile)
+        timeout -k 10 300 python3 tools/conv_bench.py --layer ${arg:-L4k3,L4k5,L3k3,L3k5,GI,U3,U2,D3,D2} --reps 20 \
+            --split > "$O/cbs_$TAG.txt" 2>&1 || { tail -20 "$O/cbs_$TAG.txt"; exit 1; }
+        grep -v amdgpu "$O/cbs_$TAG.txt" | cut -c1-200 ;;
+    convsplitlib)   # convsplit (k3 layers) with the in-tree library, then each variant of ARG (comma list)
+        for lib in main ${arg//,/ }; do
+            ( [ "$lib" = main ] || export OUHIP_LIB="$ROOT/open_universe_amd/variants/libouhip_$lib.so"
+              st=""; [ "$lib" = stamps ] && st="--sstamps"
+              timeout -k 10 300 python3 tools/conv_bench.py --layer L4k3,L3k3,U3,U2,D3,D2 --reps 20 --split $st \
+                  > "$O/cbs_${TAG}_$lib.txt" 2>&1 ) || { tail -20 "$O/cbs_${TAG}_$lib.txt"; exit 1; }
+            echo "## $lib"; grep -v amdgpu "$O/cbs_${TAG}_$lib.txt" | grep -v "^L\|^U\|^D\|^G" | cut -c1-200
         done ;;
     convlib)   # tools/conv_bench.py on the deep-level layers: in-tree library vs variant ARG
         for lib in main "$arg"; do

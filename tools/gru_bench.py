@@ -23,14 +23,6 @@ def main():
     T = int(os.environ.get("GRU_T", "801"))
     stream = torch.cuda.current_stream().cuda_stream
     gw = eng.s_gru
-    if os.environ.get("GRU_CU16") == "1":   # the single-CU f16 recurrence (f16 operand mode)
-        sd = {k: v.cpu() for k, v in m.state_dict().items()}
-        saved, E._PREP_PREC = E._PREP_PREC, 2
-        os.environ["OUHIP_GRU_CU16"] = "1"
-        try:
-            gw = E.prep_gru(sd, "_edm_model.encoder.gru", 1, dev)
-        finally:
-            E._PREP_PREC = saved
     for B in (1, 4, 8):
         x = E.Act(torch.randn(B, 512, T, device=dev) * 0.5)
         gi, y = E.new_act(B, 1536, T, dev), E.new_act(B, 512, T, dev)

@@ -90,15 +90,11 @@ def main():
             xm = float(x.abs().max()) if x is not None else -1
             ym = float(y.abs().max()) if y is not None else -1
             fin = y is None or bool(torch.isfinite(y).all())
-            ain = -1.0
-            if desc.amax_in:
-                row = (desc.amax_in - plan.amax.data_ptr()) // 256
-                ain = float(plan.amax[row].max())
-            st = eng.status.tolist()
+            st = eng.status[:4 + len(eng.range_owners)].tolist()
             print(f"{i} conv m={desc.m} cin={desc.cin} fr={desc.frame} kt={desc.kt} n={desc.n_frames} "
-                  f"rout={desc.rout} tile={desc.tile} prec={desc.prec} |x|max={xm:.4g} amax_in={ain:.4g} "
+                  f"rout={desc.rout} tile={desc.tile} prec={desc.prec} xs_shift={desc.xs_shift} |x|max={xm:.4g} "
                   f"|y|max={ym:.4g} finite={fin} status={st}", flush=True)
-            if st[1]:
+            if any(st[1:]):
                 print("RANGE FLAG at op", i)
                 return
             if not fin:
