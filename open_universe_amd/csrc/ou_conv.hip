@@ -1362,9 +1362,6 @@ __global__ __launch_bounds__(256) void conv_rreduce(ou_conv_desc d, int S, int W
 // One workgroup = one 32-row m-tile x 32 NR frames.  Waves whose chunk
 // count falls short of the unrolled body run zero chunks (their B rows read
 // 0, their A steps are clamped to real ones: +0 exactly).
-#ifndef OU_SK_SETS
-#define OU_SK_SETS 1
-#endif
 #ifndef OU_SK_BPREF   // B fragments read one step ahead of their MFMAs
 #define OU_SK_BPREF 1
 #endif
@@ -1392,7 +1389,7 @@ __global__ __launch_bounds__(256) void conv_rreduce(ou_conv_desc d, int S, int W
 #define OU_SSTAMP_SAVE do { } while (0)
 #endif
 
-template <int KT, int NR>
+template <int KT, int NR, int DEEP = 0>
 struct SCfg {
     static constexpr int W = 32 * NR + KT - 1;      // window frames (LDS rows) of a chunk
     static constexpr int NL = (W * 8 + 63) / 64;   // 16-B loads per lane per chunk (8 lanes per row)
@@ -1401,10 +1398,10 @@ struct SCfg {
     static constexpr int STEPS = 2 * KT;           // K steps per chunk: 2 groups of 16 channels x taps
     static constexpr int U = KT == 1 ? 4 : 2;      // chunks per unrolled body
     // register sets for rows in flight: 1 = the next chunk's rows loaded at a
-    // chunk's start and stored halfway through it; U = loaded SETS - 0.5
-    // chunks ahead (more VGPRs: at 64-frame tiles two waves per SIMD no
-    // longer fit, measured slower on the 4005-frame levels)
-    static constexpr int SETS = OU_SK_SETS == 1 ? 1 : U;
+    // chunk's start and stored halfway through it; DEEP: U sets, loaded
+    // SETS - 0.5 chunks ahead (more VGPRs: at 64-frame tiles two waves per
+    // SIMD no longer fit, slower on the 4005-frame levels, faster at 801)
+    static constexpr int SETS = DEEP ? U : 1;
     static constexpr int DR = KT == 5 ? 10 : U * STEPS;   // weight ring depth (divides U * STEPS)
     static constexpr int RED = 4 * NR * 16 * 64 * 4;       // the reduction image (bytes)
     static constexpr int LDS = 8 * SLOT > RED ? 8 * SLOT : RED;
@@ -1500,10 +1497,10 @@ __device__ __forceinline__ void conv_epi_q_store(const ou_conv_desc& d, const Ep
     }
 }
 
-template <int KT, int NR>
+template <int KT, int NR, int DEEP>
 __global__ __launch_bounds__(256) void conv_skernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride)
 {
-    using S = SCfg<KT, NR>;
+    using S = SCfg<KT, NR, DEEP>;
     ou_kernarg_prefetch8();
     OU_DYNAMIC_LDS(float4, lds4);
     char* lds = (char*)lds4;
@@ -1607,11 +1604,12 @@ __global__ __launch_bounds__(256) void conv_skernel(ou_conv_desc d, int mtiles, 
     //   OU_SK_BPREF the B fragments of step s + 1 are read before step s's
     //   MFMAs (the next chunk's first ones from the other slot).
     OU_SSTAMP_INIT
+    stage_load(0, 0);   // the first rows first: chunk 0 waits for them, not for the ring
 #pragma unroll
     for (int i = 0; i < S::DR - 1; ++i) load_a(i, ra[i]);
-#pragma unroll
-    for (int q = 0; q < S::SETS; ++q) stage_load(q, q);
     stage_store(0, 0);
+#pragma unroll
+    for (int q = 1; q < S::SETS; ++q) stage_load(q, q);
     if (OU_SK_BPREF) read_b(0, 0, 0, bq[0], bl[0]);
     OU_SSTAMP(0);
     for (int jb = 0; jb < njb; ++jb) {
@@ -2740,15 +2738,17 @@ int launch_rs(const ou_conv_desc& d, int shape, hipStream_t s)
     }
 }
 
-// split-image shapes (tile bit 15): bits 0-7 = NR - 1 (32 NR frames per workgroup)
+// split-image shapes (tile bit 15): bits 0-7 = NR - 1 (32 NR frames per
+// workgroup), + 3: rows prefetched U - 0.5 chunks ahead instead of half a
+// chunk (more VGPRs: one wave per SIMD at NR 2 / 3)
 constexpr int kSsBit = 1 << 15;
-[[maybe_unused]] constexpr int kNumSTiles = 3;
+[[maybe_unused]] constexpr int kNumSTiles = 6;
 
-template <int KT, int NR>
+template <int KT, int NR, int DEEP>
 int launch_s1(const ou_conv_desc& d, hipStream_t s)
 {
-    using S = SCfg<KT, NR>;
-    auto kern = conv_skernel<KT, NR>;
+    using S = SCfg<KT, NR, DEEP>;
+    auto kern = conv_skernel<KT, NR, DEEP>;
     static bool attr = false;
     if (!attr && S::LDS > 64 * 1024) {
         OU_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS),
@@ -2769,9 +2769,12 @@ int launch_ss(const ou_conv_desc& d, int shape, hipStream_t s)
 {
     if constexpr (KT == 1 || KT == 3 || KT == 5) {
         switch (shape) {
-        case 0: return launch_s1<KT, 1>(d, s);
-        case 1: return launch_s1<KT, 2>(d, s);
-        case 2: return launch_s1<KT, 3>(d, s);
+        case 0: return launch_s1<KT, 1, 0>(d, s);
+        case 1: return launch_s1<KT, 2, 0>(d, s);
+        case 2: return launch_s1<KT, 3, 0>(d, s);
+        case 3: return launch_s1<KT, 1, 1>(d, s);
+        case 4: return launch_s1<KT, 2, 1>(d, s);
+        case 5: return launch_s1<KT, 3, 1>(d, s);
         }
         return ou_fail(-2, "conv: bad split-image tile %d", shape);
     } else {

@@ -258,6 +258,8 @@ class EnhancePlan(_PlanBase):
             # the chunked score pass (Engine.chunk_plan): GRU segments on lane
             # 0, conv chunks on side lanes 2 / 3 (rec_score_chunked)
             self.chunks = eng.chunk_plan(B, Tp, force=chunk is True) if chunk is not False else None
+            if self.chunks is not None:   # chunks keep the whole ops' tiles: no split-image links
+                L.ADD_HOOK = None
             self.sb = eng.alloc_score(B, Tp, chunked=self.chunks is not None)
             E.rec_gru_ws_zero(p, self.sb["gran"])   # lane 0, ahead of the first score GRU
             # initial sample (universe.py:322-331)

@@ -119,7 +119,7 @@ int main(int argc, char** argv)
             }
         double rn = 0;
         for (double v : ref) rn += v * v;
-        for (int shape = 0; shape < 3; ++shape) {
+        for (int shape = 0; shape < 6; ++shape) {
             std::vector<float> y(ref.size(), 1e30f);
             ou_conv_desc d{};
             d.x = x.data(); d.x_bstride = (int64_t)g.cin * g.T; d.x_cstride = g.T;   // unused by the kernel

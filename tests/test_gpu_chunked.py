@@ -33,10 +33,23 @@ def model(request):
 
 
 def _pair(eng, B, T, split=None, monkeypatch=None, **kw):
+    """A chunked plan and the unchunked one it must equal bit for bit.  The
+    chunked pass records no split-image links (its chunks keep the whole ops'
+    tiles), so the unchunked plan is recorded without them too."""
+    import os
+
     if split is not None:
         monkeypatch.setenv("OUHIP_CHUNK_SPLIT", split)
     p1 = EnhancePlan(eng, B, T, 8, 1.3, chunk=True, **kw)
-    p0 = EnhancePlan(eng, B, T, 8, 1.3, chunk=False, **kw)
+    saved = os.environ.get("OUHIP_SPLIT_IMAGES")
+    os.environ["OUHIP_SPLIT_IMAGES"] = "0"
+    try:
+        p0 = EnhancePlan(eng, B, T, 8, 1.3, chunk=False, **kw)
+    finally:
+        if saved is None:
+            del os.environ["OUHIP_SPLIT_IMAGES"]
+        else:
+            os.environ["OUHIP_SPLIT_IMAGES"] = saved
     return p0, p1
 
 
@@ -83,6 +96,7 @@ def test_chunked_keep_rms_and_model_enhance(model, monkeypatch):
         out = model.enhance(mix, rng=torch.Generator(device=DEV).manual_seed(4), keep_rms=True)
     plan = next(p for k, p in model._plans.items() if k[1] == T)
     assert plan.chunks is not None
+    monkeypatch.setenv("OUHIP_SPLIT_IMAGES", "0")   # as the chunked plan: no split-image links
     p0 = EnhancePlan(model._get_engine(), 1, T, 8, 1.3, keep_rms=True, chunk=False)
     ref = p0(mix[None, None], torch.Generator(device=DEV).manual_seed(4)).clone()
     assert torch.equal(out, ref[0])

@@ -87,7 +87,7 @@ def test_split_image_kernel_every_shape(geom):
     img = split_image(xa.t, 0.25, 6, rows=T + 2)
     lib = L.load()
     stream = torch.cuda.current_stream().cuda_stream
-    for shape in range(3):
+    for shape in range(6):
         for mj in (0, 1 << 16):
             y = E.new_act(B, cout, U * rout, DEV)
             y.t.fill_(float("nan"))

@@ -199,7 +199,7 @@ def main():
             yref = y.clone()
             ds, img = split_variant(d, keep)
             sres = []
-            for t in range(3):
+            for t in range(6):
                 for mj in (0, 1 << 16):
                     ms = time_tile(ds, L.SS_BIT | t | mj, a.reps, stream)
                     if ms is not None:
@@ -230,10 +230,12 @@ def main():
                 st = st[st[:, :, :4].sum(axis=(1, 2)) > 0]
                 if len(st):
                     ph = st[:, :, :4].mean(axis=(0, 1))
+                    skew = (st[:, :, 1].max(1) - st[:, :, 1].min(1)).mean()   # main-loop spread within a WG
                     life = (st[:, :, 7] - st[:, :, 6]).mean() / 100.0
                     t0 = st[:, :, 6].min()
                     print(f"      stamps ({len(st)} WGs, cycles per wave): prologue={ph[0]:.0f} main={ph[1]:.0f} "
-                          f"reduce={ph[2]:.0f} epilogue={ph[3]:.0f}; wave lifetime {life:.2f} us; starts "
+                          f"reduce={ph[2]:.0f} epilogue={ph[3]:.0f} (main-loop skew in a WG {skew:.0f}); "
+                          f"wave lifetime {life:.2f} us; starts "
                           f"0..{(st[:, :, 6].max() - t0) / 100:.2f} us, last end {(st[:, :, 7].max() - t0) / 100:.2f} us",
                           flush=True)
             sl = "  ".join(f"s{t & 0xff}{'m' if t & (1 << 16) else ''}:{ms * 1e3:.1f}us" for ms, t in sres)
