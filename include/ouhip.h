@@ -444,6 +444,21 @@ typedef struct ou_block_desc {
      * a larger value sets range code 1 / 2 / 8 / 16 in *status, an infinite
      * one 4).  The engine uses 6 unless a range flag widened a stage. */
     int32_t shift[4];
+    /* Split images (prec 1; layout and values as ou_conv_desc.sy / xs).  sy:
+     * also store the block output's image for the next conv (y is stored
+     * too; not with a head; range code 32 when a value leaves the range).
+     * xs: stage 0 copies the conv1 operand from this image (stored by the
+     * producing conv with slope[0] and shift[0]) instead of staging h, which
+     * is then read only as the residual (whole signal: f0 = f1 = h0 = h1 = 0,
+     * no input conv). */
+    uint16_t* sy;
+    int64_t sy_bstride;        /* bytes between batch items                      */
+    int32_t sy_rows, sy_shift; /* samples per 32-channel block; exponent        */
+    float sy_slope;            /* the consumer's PReLU slope                     */
+    int32_t sy_pad_;
+    const uint16_t* xs;
+    int64_t xs_bstride;        /* bytes between batch items                      */
+    int32_t xs_rows, xs_pad_;  /* samples per 32-channel block (>= length)       */
 } ou_block_desc;
 
 /* 1 when ou_block handles this channel count and operand precision. */

@@ -146,6 +146,9 @@ class BlockDesc(ctypes.Structure):
         ("rate", c_int32), ("down_kt", c_int32), ("e", fp), ("e_bstride", c_int64), ("e_cstride", c_int64),
         ("f0", c_int32), ("f1", c_int32), ("h0", c_int32), ("h1", c_int32),
         ("shift", c_int32 * 4),
+        ("sy", fp), ("sy_bstride", c_int64), ("sy_rows", c_int32), ("sy_shift", c_int32),
+        ("sy_slope", c_float), ("sy_pad_", c_int32),
+        ("xs", fp), ("xs_bstride", c_int64), ("xs_rows", c_int32), ("xs_pad_", c_int32),
     ]
 
 
@@ -431,7 +434,7 @@ def mmajor_order(desc):
 TUNER = None
 
 
-ADD_HOOK = None   # engine.split_hook while a plan records: links a conv to its producer's split image
+ADD_HOOK = None   # engine.split_hook while a plan records: links an op to its producer's split image
 SS_BIT = 1 << 15  # ConvDesc.tile bit: the split-image kernel (conv_skernel), bits 0-7 = NR - 1
 
 
@@ -450,24 +453,24 @@ class Program:
         self.lanes = []         # lane of each op
         self.label = ""         # phase label recorded with each op (engine sets it; reports only)
         self.labels = []
-        self.prev_conv = {}     # lane -> (op index, ConvDesc): the lane's last op, when it is a conv
+        self.prev_op = {}       # lane -> (op index, op, desc): the lane's last op, when a conv or block
 
     def add(self, op, desc):
         assert isinstance(desc, OP_STRUCT[op])
         if op == OP_LANE:
             self.cur_lane = desc.id
-        if op == OP_CONV and ADD_HOOK is not None:
-            ADD_HOOK(self, desc)   # may link it to the lane's previous conv (split image)
+        if op in (OP_CONV, OP_BLOCK) and ADD_HOOK is not None:
+            ADD_HOOK(self, op, desc)   # may link it to the lane's previous op (split image)
         if op == OP_CONV and desc.tile < 0 and TUNER is not None:
             desc.tile = TUNER(desc)
         if op == OP_CONV and desc.tile >= 0 and mmajor_order(desc):
             desc.tile |= MAJ_BIT
         check(self.lib.ou_program_add(self.h, op, ctypes.byref(desc), ctypes.sizeof(desc)),
               f"program_add(op={op})")
-        if op == OP_CONV:
-            self.prev_conv[self.cur_lane] = (len(self.flops), desc)
+        if op in (OP_CONV, OP_BLOCK):
+            self.prev_op[self.cur_lane] = (len(self.flops), op, desc)
         elif op not in (OP_LANE, OP_SIGNAL):   # a wait may hand over data another lane wrote
-            self.prev_conv.pop(self.cur_lane, None)
+            self.prev_op.pop(self.cur_lane, None)
         self.flops.append(float(getattr(desc, "_flops", 0.0)))
         self.bytes.append(float(getattr(desc, "_bytes", 0.0)))
         self.lanes.append(self.cur_lane)

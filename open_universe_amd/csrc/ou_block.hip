@@ -58,10 +58,7 @@ namespace {
 
 constexpr int kStageShift = 6;   // the exponent ou_block_pack's w_unscale assumes (ou_conv's kSplitShift)
 
-__device__ __forceinline__ float ou_bexp2i(int e)   // 2^e, |e| <= 126 (exact)
-{
-    return __uint_as_float((unsigned)(127 + e) << 23);
-}
+
 #ifndef OU_BLOCK_NT32
 #define OU_BLOCK_NT32 4
 #endif
@@ -380,7 +377,7 @@ __device__ __forceinline__ void down_stage(const ou_block_desc& d, const _Float1
     const half8_t* wp = (const half8_t*)d.w_down;
     const int TE = (TS + R - 1) / R;   // e stored for output frames < ceil(TS / R)
     const int e0 = t0 / R;
-    const float un = d.w_down_unscale * ou_bexp2i(d.shift[3] - kStageShift);
+    const float un = d.w_down_unscale * ou_exp2i(d.shift[3] - kStageShift);
     for (int tile = wave; tile < M4 * N4; tile += 4) {
         const int m4 = tile % M4, n4 = tile / M4;
         const int u = n4 * 32 + l32;
@@ -449,8 +446,8 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     constexpr int OFF = block_off<EPI, R, KF>();   // conv3 starts OFF frames before t0
     constexpr int F = block_f<C, NT, P, EPI, R, KF>();
     // per-stage staging exponents (the host widens one whose range flag trips)
-    const float kIn0 = ou_bexp2i(-d.shift[0]), kIn1 = ou_bexp2i(-d.shift[1]), kIn2 = ou_bexp2i(-d.shift[2]),
-                kInD = ou_bexp2i(-d.shift[3]);
+    const float kIn0 = ou_exp2i(-d.shift[0]), kIn1 = ou_exp2i(-d.shift[1]), kIn2 = ou_exp2i(-d.shift[2]),
+                kInD = ou_exp2i(-d.shift[3]);
     OU_DYNAMIC_LDS(half8_t, lds8);
     using E = typename K::E;
     E* lds = (E*)lds8;
@@ -466,6 +463,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     const int hlo = d.h0, hhi = d.h1 > 0 ? min(d.h1, T) : T;   // h frames the caller produced
     const float* __restrict__ hb = d.h + (int64_t)b * d.h_bstride;
     float om0 = 0.f, om1 = 0.f, om2 = 0.f, omd = 0.f;   // max |staged value| of the conv1 / 2 / 3 / down inputs
+    float oms = 0.f;                                     // max |split-image value| (d.sy)
     // weight-fragment ring shared by the three split-f16 / f16 stages; conv1's
     // first fragments are requested before the input staging
     constexpr bool early = OU_BLOCK_RING_EARLY && P != 0;
@@ -481,11 +479,38 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                               __builtin_fmaf(d.w_in[3 * c + 1], xm, __builtin_fmaf(d.w_in[3 * c], xl, d.b_in[c])));
     };
 
-    // ---- stage 0: PReLU1(h) * 2^-6 over frames [t0 - 4 - OFF, ...) -> region A.
+    // ---- stage 0: PReLU1(h) * 2^-shift over frames [t0 - 4 - OFF, ...) -> region A.
     // A work item is (8-channel group, frame): 8 coalesced loads (consecutive
     // lanes = consecutive frames), then one 16-B LDS write per plane.  All
-    // loads of a thread are issued before any arithmetic.
-    {
+    // loads of a thread are issued before any arithmetic.  With a split image
+    // of the operand (d.xs, stored by the producing conv) an item is two 16-B
+    // loads (hi, lo) copied to LDS as they are.
+    if (P == 1 && !(EPI & kEpiIn) && d.xs) {
+        constexpr int NI = (C / 8) * K::R1;
+        constexpr int NIT = (NI + K::NTH - 1) / K::NTH;
+        const __amdgpu_buffer_rsrc_t xrs =
+            ou_rsrc((const char*)d.xs + (int64_t)b * d.xs_bstride, (int64_t)(C / 32) * d.xs_rows * 128);
+        ou_u4_t vh[NIT], vl[NIT];
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int item = min(tid + K::NTH * it, NI - 1);
+            const int g = item / K::R1, r = item - g * K::R1;
+            const int t = t0 - 4 - OFF + r;
+            const bool ok = t >= 0 && t < T && !(d.dbg & 1);
+            const int vo = ok ? ((g >> 2) * d.xs_rows + t) * 128 + (g & 3) * 16 : kBlkSentinel;
+            vh[it] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0);
+            vl[it] = __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 64, 0);
+        }
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int item = tid + K::NTH * it;
+            if (NIT * K::NTH > NI && item >= NI) break;
+            const int g = item / K::R1, r = item - g * K::R1;
+            E* dst = xa + r * SX + 8 * g;
+            *(ou_u4_t*)dst = vh[it];
+            *(ou_u4_t*)(dst + K::PA) = vl[it];
+        }
+    } else {
         constexpr int NI = (C / 8) * K::R1;
         constexpr int NIT = (NI + K::NTH - 1) / K::NTH;
         const float a1 = d.slope[0];
@@ -600,7 +625,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                     }
                 }
             }
-        const float un = d.w_unscale[0] * ou_bexp2i(d.shift[0] - kStageShift);
+        const float un = d.w_unscale[0] * ou_exp2i(d.shift[0] - kStageShift);
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
@@ -646,7 +671,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     run_stage<3, C, NT, P>(d.w[1], xbuf, K::PB, wm, wn, lane, d.dbg, acc, accx, ring, early);
     if (early) ring_pro<3, C, NT, P>(d.w[2], wm, lane, ring);   // conv3's first fragments
     {
-        const float a3 = d.slope[2], un = d.w_unscale[1] * ou_bexp2i(d.shift[1] - kStageShift);
+        const float a3 = d.slope[2], un = d.w_unscale[1] * ou_exp2i(d.shift[1] - kStageShift);
         float bia[MR][16];
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
@@ -720,7 +745,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     run_stage<3, C, NT, P>(d.w[2], xa, K::PA, wm, wn, lane, d.dbg, acc, accx, ring, early);
     if constexpr (!(OU_BLOCK_HV_EARLY && !(EPI & kEpiIn))) load_res();
     {
-        const float un = d.w_unscale[2] * ou_bexp2i(d.shift[2] - kStageShift);
+        const float un = d.w_unscale[2] * ou_exp2i(d.shift[2] - kStageShift);
         float bia[MR][16];
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr)
@@ -777,6 +802,10 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
             }
         } else {
             float* yb = d.y + (int64_t)b * d.y_bstride;
+            const __amdgpu_buffer_rsrc_t srs =
+                ou_rsrc(d.sy ? (const char*)d.sy + (int64_t)b * d.sy_bstride : (const char*)yb,
+                        d.sy ? (int64_t)(C / 32) * d.sy_rows * 128 : 0);
+            const float sscale = ou_exp2i(-d.sy_shift);
             // kEpiDown: PReLU_down(y) 2^-6 also goes to region A (split), rows
             // w <-> frames t0 - OFF + w, zero outside [0, T) and past the rows
             // the strided conv reads
@@ -798,6 +827,15 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                         if constexpr (EPI & kEpiRes2) v = (v + rv[mr][nr][r]) * d.s2;
                         vv[r] = v;
                         if (own && rok(mr, r)) yb[(int64_t)row(mr, r) * d.y_cstride + t] = v;
+                    }
+                    if (P == 1 && d.sy) {   // the next conv's split image (host-checked: C % 32 == 0)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int c0 = (wm * MR + mr) * 32 + 8 * j + 4 * h;
+                            const int off = own ? ((c0 >> 5) * d.sy_rows + t) * 128 + (c0 & 31) * 2 : kBlkSentinel;
+                            ou_split_store4(srs, off, own, vv[4 * j], vv[4 * j + 1], vv[4 * j + 2], vv[4 * j + 3],
+                                            sscale, d.sy_slope, oms);
+                        }
                     }
                     if constexpr (EPI & kEpiDown) {
                         constexpr int RH = R * (KF - 1 - (KF - 1) / 2);
@@ -826,12 +864,14 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
         }
     }
     // range codes: 1 / 2 / 8 / 16 the conv1 / conv2 / conv3 / down input's
-    // exponent is too small, 4 an infinite input (ou_range_flag)
+    // exponent is too small, 32 the split image's (d.sy), 4 an infinite
+    // input (ou_range_flag)
     if constexpr (P != 0) {
         ou_range_flag(d.status, om0, 1, lane);
         ou_range_flag(d.status, om1, 2, lane);
         ou_range_flag(d.status, om2, 8, lane);
         if constexpr ((EPI & kEpiDown) != 0) ou_range_flag(d.status, omd, 16, lane);
+        if (d.sy) ou_range_flag(d.status, oms, 32, lane);
     }
 }
 
@@ -1054,6 +1094,21 @@ extern "C" int ou_block(const ou_block_desc* dp, void* stream)
         return ou_fail(-1, "block: invalid descriptor");
     if (!ou_block_supported(d.channels, d.prec))
         return ou_fail(-1, "block: channels %d / prec %d not supported", d.channels, d.prec);
+    // buffer resources take 32-bit offsets with a sentinel for "outside":
+    // every per-item tensor must stay below it
+    const int64_t lim = kBlkSentinel;
+    if ((int64_t)d.channels * d.h_cstride * 4 >= lim || (int64_t)d.channels * d.y_cstride * 4 >= lim ||
+        (d.res2 && (int64_t)d.channels * d.r2_cstride * 4 >= lim) ||
+        (d.e && (int64_t)2 * d.channels * d.e_cstride * 4 >= lim))
+        return ou_fail(-1, "block: a per-item tensor of %d x %lld floats exceeds the 32-bit buffer range", d.channels,
+                       (long long)d.h_cstride);
+    if (d.sy && (d.prec != 1 || d.channels % 32 || d.head.w || d.sy_rows < d.length || d.sy_shift < -100 ||
+                 d.sy_shift > 100 || (int64_t)(d.channels / 32) * d.sy_rows * 128 >= lim))
+        return ou_fail(-1, "block: a split-image output needs prec 1, channels %% 32 == 0, no head, sy_rows >= length");
+    if (d.xs && (d.prec != 1 || d.channels % 32 || d.x || d.f0 || d.f1 || d.h0 || d.h1 || d.xs_rows < d.length ||
+                 (int64_t)(d.channels / 32) * d.xs_rows * 128 >= lim))
+        return ou_fail(-1, "block: a split-image input needs prec 1, channels %% 32 == 0, the whole signal, no input "
+                           "conv, xs_rows >= length");
     hipStream_t s = (hipStream_t)stream;
     return d.prec == 1 ? launch_p<1>(d, s) : d.prec == 2 ? launch_p<2>(d, s) : launch_p<0>(d, s);
 }

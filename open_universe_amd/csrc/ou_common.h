@@ -138,6 +138,34 @@ __device__ __forceinline__ void ou_range_flag(int* status, float omax, int big, 
     }
 }
 
+// 2^e for |e| <= 126 (exact: the exponent field)
+__device__ __forceinline__ float ou_exp2i(int e)
+{
+    return __uint_as_float((unsigned)(127 + e) << 23);
+}
+
+// Split-image store (include/ouhip.h, ou_conv_desc.sy): 4 consecutive
+// channels of one sample, p = prelu_slope(v) * scale split into f16 hi (8 B at
+// byte `off` of `rs`) and lo (8 B at off + 64).  `off` is the sentinel for
+// elements that are not stored; omax tracks max |p| of the stored ones.
+typedef _Float16 ou_h4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t ou_u2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t ou_u4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ou_split_store4(__amdgpu_buffer_rsrc_t rs, int off, bool ok, float v0, float v1,
+                                                float v2, float v3, float scale, float slope, float& omax)
+{
+    float p[4] = {v0 * scale, v1 * scale, v2 * scale, v3 * scale};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = p[j] >= 0.f ? p[j] : p[j] * slope;
+    const ou_h4_t hi = {(_Float16)p[0], (_Float16)p[1], (_Float16)p[2], (_Float16)p[3]};
+    const ou_h4_t lo = {(_Float16)((p[0] - (float)hi[0]) * 2048.f), (_Float16)((p[1] - (float)hi[1]) * 2048.f),
+                        (_Float16)((p[2] - (float)hi[2]) * 2048.f), (_Float16)((p[3] - (float)hi[3]) * 2048.f)};
+    const float m = fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fmaxf(fabsf(p[2]), fabsf(p[3])));
+    omax = fmaxf(omax, ok ? m : 0.f);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(ou_u2_t, hi), rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(ou_u2_t, lo), rs, off, 64, 0);
+}
+
 // XCD-aware workgroup order (speed only, never correctness).  Workgroups
 // are dealt round-robin over the 8 XCDs, so the neighbouring workgroups that
 // share a weight panel (the N tiles of one m-group) land on 8 different L2s

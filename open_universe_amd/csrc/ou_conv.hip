@@ -194,11 +194,6 @@ struct SplitOut {
     float scale, slope;
 };
 
-__device__ __forceinline__ float ou_exp2i(int e)   // 2^e, |e| <= 126 (exact)
-{
-    return __uint_as_float((unsigned)(127 + e) << 23);
-}
-
 __device__ __forceinline__ SplitOut split_ctx(const ou_conv_desc& d, int b, int cout)
 {
     SplitOut s;
@@ -217,17 +212,8 @@ __device__ __forceinline__ SplitOut split_ctx(const ou_conv_desc& d, int b, int 
 __device__ __forceinline__ void split_store4(const SplitOut& s, int co0, int t, bool ok, float v0, float v1,
                                              float v2, float v3, float& omax)
 {
-    float p[4] = {v0 * s.scale, v1 * s.scale, v2 * s.scale, v3 * s.scale};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) p[j] = p[j] >= 0.f ? p[j] : p[j] * s.slope;
-    const half4_t hi = {(_Float16)p[0], (_Float16)p[1], (_Float16)p[2], (_Float16)p[3]};
-    const half4_t lo = {(_Float16)((p[0] - (float)hi[0]) * 2048.f), (_Float16)((p[1] - (float)hi[1]) * 2048.f),
-                        (_Float16)((p[2] - (float)hi[2]) * 2048.f), (_Float16)((p[3] - (float)hi[3]) * 2048.f)};
-    const float m = fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fmaxf(fabsf(p[2]), fabsf(p[3])));
-    omax = fmaxf(omax, ok ? m : 0.f);
     const int off = ok ? ((co0 >> 5) * s.rows + t) * 128 + (co0 & 31) * 2 : kSentinel;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(ou_u32x2, hi), s.rs, off, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(ou_u32x2, lo), s.rs, off, 64, 0);
+    ou_split_store4(s.rs, off, ok, v0, v1, v2, v3, s.scale, s.slope, omax);
 }
 
 struct EpiCtx {
@@ -3024,6 +3010,15 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
     if (!d.x || !d.w || !d.y || d.m <= 0 || d.batch <= 0 || d.n_frames <= 0 || d.cin <= 0 ||
         d.frame <= 0 || d.rout == 0 || d.m % d.rout != 0 || d.in_len <= 0 || d.out_len <= 0 || d.f0 < 0)
         return ou_fail(-1, "conv: invalid descriptor (m=%d rout=%d frame=%d f0=%d)", d.m, d.rout, d.frame, d.f0);
+    {   // buffer resources take 32-bit offsets with a sentinel for "outside":
+        // every per-item tensor must stay below it
+        const int64_t lim = kSentinel, cout = d.m / (d.rout < 0 ? -d.rout : d.rout);
+        if ((int64_t)d.cin * d.x_cstride * 4 >= lim || cout * d.y_cstride * 4 >= lim ||
+            (d.res1 && cout * d.r1_cstride * 4 >= lim) || (d.res2 && cout * d.r2_cstride * 4 >= lim))
+            return ou_fail(-1, "conv: a per-item tensor (cin %d x %lld, cout %lld x %lld floats) exceeds the 32-bit "
+                               "buffer range", d.cin, (long long)d.x_cstride, (long long)cout,
+                           (long long)d.y_cstride);
+    }
     if (d.sy) {   // split-image output (any split-f16 kernel's epilogue)
         if (d.prec != 1 || d.rout != 1 || d.m % 32 || d.sy_rows < d.out_len || d.sy_shift < -100 ||
             d.sy_shift > 100 || (int64_t)(d.m / 32) * d.sy_rows * 128 >= kSentinel)

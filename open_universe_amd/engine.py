@@ -111,41 +111,68 @@ def end_record():
 SPLIT_SHIFT = 6
 
 
-def split_hook(prog, d):
-    """Program.add hook (split-f16 plans): link conv ``d`` to the split image
-    of the lane's previous op when that op is the conv that produced d's input."""
-    wn = getattr(d, "_w_nat", None)
-    if (wn is None or d.prec != 1 or d.xs or d.in_scale or d.f0 or d.cin % 32
-            or getattr(d, "_full", None) is not None):
+def _split_consumer(op, d):
+    """(x ptr, bstride, cstride, in_len, channels, slope, shift, owner) of an
+    op that can read its operand from a split image, or None."""
+    if op == L.OP_CONV:
+        wn = getattr(d, "_w_nat", None)
+        if (wn is None or d.prec != 1 or d.xs or d.in_scale or d.f0 or d.cin % 32
+                or getattr(d, "_full", None) is not None):
+            return None
+        return (d.x, d.x_bstride, d.x_cstride, d.in_len, d.cin, d.slope, d.xs_shift, ("c", getattr(d, "_cw", None), 0))
+    fw = getattr(d, "_fw", None)
+    if (fw is None or d.prec != 1 or d.xs or d.x or d.f0 or d.f1 or d.h0 or d.h1 or d.channels % 32):
+        return None
+    return (d.h, d.h_bstride, d.h_cstride, d.length, d.channels, d.slope[0], d.shift[0], ("f", fw, 0))
+
+
+def _split_producer(op, p):
+    """(y ptr, bstride, cstride, out_len, channels, batch) of an op whose
+    epilogue can store a split image, or None."""
+    if op == L.OP_CONV:
+        if (p.prec != 1 or p.rout != 1 or p.m % 32 or p.sy or p.f0 or getattr(p, "_full", None) is not None):
+            return None
+        return (p.y, p.y_bstride, p.y_cstride, p.out_len, p.m, p.batch)
+    if (p.prec != 1 or p.head.w or p.sy or p.channels % 32 or p.f0 or p.f1):
+        return None
+    return (p.y, p.y_bstride, p.y_cstride, p.length, p.channels, p.batch)
+
+
+def split_hook(prog, op, d):
+    """Program.add hook (split-f16 plans): link op ``d`` (a conv, or a fused
+    block's conv1) to the split image of the lane's previous op when that op
+    -- a conv or a fused block -- produced d's input."""
+    cons = _split_consumer(op, d)
+    pv = prog.prev_op.get(prog.cur_lane)
+    if cons is None or pv is None:
         return
-    pv = prog.prev_conv.get(prog.cur_lane)
-    if pv is None:
+    idx, pop, p = pv
+    prod = _split_producer(pop, p)
+    x, xb, xc, in_len, C, slope, shift, owner = cons
+    if (p is d or prod is None or prod[0] != x or prod[1] != xb or prod[2] != xc or prod[3] < in_len
+            or prod[4] != C or prod[5] < d.batch):
         return
-    idx, p = pv
-    if (p is d or p.prec != 1 or p.rout != 1 or p.m % 32 or p.sy or p.f0
-            or getattr(p, "_full", None) is not None or p.y != d.x or p.y_bstride != d.x_bstride
-            or p.y_cstride != d.x_cstride or p.out_len < d.in_len or p.batch < d.batch or p.m != d.cin):
-        return
-    rows = p.out_len
-    per_item = (p.m // 32) * rows * 128
+    rows, batch = prod[3], prod[5]
+    per_item = (C // 32) * rows * 128
     # one image per (activation buffer, lane): every step of the score loop
     # rewrites the same activations in order on one lane, so their images too
-    key = (p.y, p.y_bstride, p.y_cstride, rows, p.m, p.batch, prog.cur_lane)
+    key = (x, xb, xc, rows, C, batch, prog.cur_lane)
     cache = prog.__dict__.setdefault("split_bufs", {})
     buf = cache.get(key)
     if buf is None:
-        buf = cache[key] = empty((p.batch * per_item // 2,), dtype=torch.int16, device=_REC_DEVICE)
+        buf = cache[key] = empty((batch * per_item // 2,), dtype=torch.int16, device=_REC_DEVICE)
         prog.keep.append(buf)
     prog.__dict__.setdefault("split_links", []).append((idx, len(prog.flops)))
-    shift = d.xs_shift   # the consumer's exponent
-    if p.status and getattr(d, "_cw", None) is not None:
-        _SPLIT_CONSUMERS[p.status] = d._cw   # a split-image range code 2 of p widens d's layer
-    p.sy, p.sy_bstride, p.sy_rows, p.sy_shift, p.sy_slope = buf.data_ptr(), per_item, rows, shift, d.slope
-    prog.patch(idx, L.OP_CONV, p)
-    d.xs, d.xs_bstride, d.xs_rows, d.xs_shift = p.sy, per_item, rows, shift
-    d.w, d.w_unscale = wn
-    if d.tile >= 0 and not d.tile & L.SS_BIT:
-        d.tile = -1
+    if p.status and owner[1] is not None:
+        _SPLIT_CONSUMERS[p.status] = owner   # a split-image range code (2 / 32) of p widens d's operand
+    p.sy, p.sy_bstride, p.sy_rows, p.sy_shift, p.sy_slope = buf.data_ptr(), per_item, rows, shift, slope
+    prog.patch(idx, pop, p)
+    d.xs, d.xs_bstride, d.xs_rows = p.sy, per_item, rows
+    if op == L.OP_CONV:
+        d.xs_shift = shift
+        d.w, d.w_unscale = d._w_nat
+        if d.tile >= 0 and not d.tile & L.SS_BIT:
+            d.tile = -1
 
 
 # ---------------------------------------------------------------------------
@@ -752,6 +779,7 @@ def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film
     d.status = fw.status or bw.conv1.status or 0
     for i in range(4):
         d.shift[i] = fw.shifts[i]
+    d._fw = fw   # split-image linking (split_hook)
     if x_in is not None:
         xa, scale, w_in, b_in = x_in
         assert bw.C == 32 and xa.C == 1 and xa.T == h.T and xa.B >= h.B
@@ -1065,9 +1093,9 @@ class Engine:
     def widen_ranges(self, flags, step=8):
         """A range error's per-layer codes [(slot, code)] (plan.check): widen
         the staging exponent of every operand whose finite values left the
-        split-f16 range by 2^step -- the conv's own input (code 1), the input
-        of the conv it stores a split image for (2), a fused block's conv1 /
-        conv2 / conv3 / down input (1 / 2 / 8 / 16).  Codes 4 alone (an
+        split-f16 range by 2^step -- the conv's own input (code 1), a fused
+        block's conv1 / conv2 / conv3 / down input (1 / 2 / 8 / 16), the
+        operand of the op a conv (2) or block (32) stores a split image for.  Codes 4 alone (an
         infinite value: an overflow upstream) widen nothing.  Returns the
         number of exponents widened; 0 (nothing to widen, or an exponent past
         MAX_SHIFT) means the caller falls back to f32 operands.  Plans must
@@ -1080,14 +1108,13 @@ class Engine:
             targets = []
             if isinstance(own, FusedW):
                 targets = [("f", own, i) for i, bit in enumerate((1, 2, 8, 16)) if code & bit]
-            else:
-                if code & 1:
-                    targets.append(("c", own, 0))
-                if code & 2:
-                    cons = _SPLIT_CONSUMERS.get(own.status)
-                    if cons is None:
-                        return 0
-                    targets.append(("c", cons, 0))
+            elif code & 1:
+                targets.append(("c", own, 0))
+            if code & (32 if isinstance(own, FusedW) else 2):   # its split image: the consumer's operand
+                cons = _SPLIT_CONSUMERS.get(own.status)
+                if cons is None:
+                    return 0
+                targets.append(cons)
             for kind, o, i in targets:
                 if kind == "f":
                     o.shifts[i] += step

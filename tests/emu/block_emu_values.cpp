@@ -4,7 +4,9 @@
 // (include/ouhip.h, blocks.py:393-416), whole-signal and on a frame range
 // (f0, f1, h0, h1: only the range is stored and compared).  Channel counts
 // 32 / 48 / 64 / 96 / 128 / 192 (48: MFMA rows padded to 64), f32,
-// split-f16 and f16 operands, the epilogues FiLM, input_cond + FiLM, cond_out and res2.
+// split-f16 and f16 operands, the epilogues FiLM, input_cond + FiLM, cond_out and res2,
+// and split images (ou_block_desc.xs: stage 0 copies the producer's image of
+// the operand; .sy: the epilogue stores prelu(y) 2^-s for the next conv).
 // Prints one line per failing case and exits 1.
 #include "../../open_universe_amd/csrc/ou_block.hip"
 
@@ -20,7 +22,24 @@ static float rnd()
 struct Case {
     int C, T, prec;
     bool film, sc, cond, res2, chunk;
+    bool xs = false, sy = false;
 };
+
+// prelu_slope(v) 2^-shift as a split image [C / 32][rows][hi | lo][32] f16
+static std::vector<_Float16> split_image(const std::vector<float>& v, int C, int T, int rows, float slope, int shift)
+{
+    std::vector<_Float16> img((size_t)C / 32 * rows * 64, (_Float16)0.f);
+    for (int c = 0; c < C; ++c)
+        for (int t = 0; t < T; ++t) {
+            float p = std::ldexp(v[(size_t)c * T + t], -shift);
+            if (p < 0) p *= slope;
+            const _Float16 hi = (_Float16)p;
+            const size_t o = ((size_t)(c / 32) * rows + t) * 64 + c % 32;
+            img[o] = hi;
+            img[o + 32] = (_Float16)((p - (float)hi) * 2048.f);
+        }
+    return img;
+}
 
 // conv over [0, T) with zero padding: out[m][t] = b[m] + sum w[m][c][k] prelu(in[c][t + k - pad])
 static void conv_ref(const std::vector<double>& in, const std::vector<float>& w, const std::vector<float>& b, int C,
@@ -83,6 +102,18 @@ static int run(const Case& cs)
     d.y = y.data(); d.y_bstride = (int64_t)C * T; d.y_cstride = T; d.s_res = 0.7f; d.s2 = 0.5f;
     if (cs.res2) { d.res2 = res2.data(); d.r2_bstride = (int64_t)C * T; d.r2_cstride = T; }
     d.status = &status;
+    d.shift[0] = 7; d.shift[1] = 5; d.shift[2] = 6; d.shift[3] = 6;
+    const int rows = T + 3, sshift = 9;
+    const float sslope = 0.125f;
+    std::vector<_Float16> ximg, yimg((size_t)C / 32 * rows * 64, (_Float16)1e4f);
+    if (cs.xs) {
+        ximg = split_image(h, C, T, rows, slopes[0], d.shift[0]);
+        d.xs = (const uint16_t*)ximg.data(); d.xs_bstride = (int64_t)ximg.size() * 2; d.xs_rows = rows;
+    }
+    if (cs.sy) {
+        d.sy = (uint16_t*)yimg.data(); d.sy_bstride = (int64_t)yimg.size() * 2; d.sy_rows = rows;
+        d.sy_shift = sshift; d.sy_slope = sslope;
+    }
     int f0 = 0, f1 = T;
     if (cs.chunk) {
         f0 = T / 3;
@@ -128,11 +159,27 @@ static int run(const Case& cs)
                 rc2 += c1[o] * c1[o];
             }
         }
+    bool img_bad = false;   // the stored split image: prelu(y) 2^-s element by element, rows >= T untouched
+    if (cs.sy)
+        for (int c = 0; c < C; ++c)
+            for (int t = 0; t < rows; ++t) {
+                const size_t o = ((size_t)(c / 32) * rows + t) * 64 + c % 32;
+                if (t >= T) {
+                    img_bad |= (float)yimg[o] != 1e4f || (float)yimg[o + 32] != 1e4f;
+                    continue;
+                }
+                double p = std::ldexp((double)y[(size_t)c * T + t], -sshift);
+                if (p < 0) p *= sslope;
+                const double got = (double)yimg[o] + (double)yimg[o + 32] / 2048.0;
+                img_bad |= !(std::fabs(got - p) <= std::fabs(p) * std::ldexp(1.0, -21) + std::ldexp(1.0, -35));
+            }
     const double rel = std::sqrt(en / rn), relc = cs.cond ? std::sqrt(ec / rc2) : 0.0;
     const double tol = cs.prec == 2 ? 3e-3 : 2e-5;
-    if (!(rel < tol) || !(relc < tol) || outside || status) {
-        std::printf("C %d T %d prec %d film %d sc %d cond %d res2 %d chunk %d: rel %.3g cond %.3g outside %d status %d\n",
-                    C, T, cs.prec, cs.film, cs.sc, cs.cond, cs.res2, cs.chunk, rel, relc, outside, status);
+    if (!(rel < tol) || !(relc < tol) || outside || status || img_bad) {
+        std::printf("C %d T %d prec %d film %d sc %d cond %d res2 %d chunk %d xs %d sy %d: rel %.3g cond %.3g "
+                    "outside %d status %d image %d\n",
+                    C, T, cs.prec, cs.film, cs.sc, cs.cond, cs.res2, cs.chunk, cs.xs, cs.sy, rel, relc, outside,
+                    status, img_bad);
         return 1;
     }
     return 0;
@@ -148,11 +195,14 @@ int main(int argc, char** argv)
             cases.push_back({C, T, prec, true, true, false, false, false});
             cases.push_back({C, T, prec, false, false, true, false, true});
             cases.push_back({C, T, prec, false, false, false, true, true});
+            const bool img = prec == 1 && C % 32 == 0;   // split images: both ends, then input only
+            cases.push_back({C, T, prec, true, true, false, false, false, img, img});
+            cases.push_back({C, T, prec, false, false, true, false, false, img, false});
         }
     const int only = argc > 1 ? std::atoi(argv[1]) : -1;
     int bad = 0, n = 0;
     for (int i = 0; i < (int)cases.size(); ++i) {
-        if (only >= 0 && i / 12 != only) continue;   // argv: channel-count group (12 cases each)
+        if (only >= 0 && i / 18 != only) continue;   // argv: channel-count group (18 cases each)
         bad += run(cases[i]);
         ++n;
     }

@@ -170,3 +170,51 @@ def test_staging_exponent_and_range_codes():
     assert lib.ou_conv(ctypes.byref(d), ctypes.c_void_p(stream)) == 0
     torch.cuda.synchronize()
     assert st[0].item() == 2, st.tolist()
+
+
+def test_fused_block_split_image_links():
+    """Split images through a fused block (ou_block_desc.xs / sy): conv ->
+    block -> conv recorded with the split-image hook links the block to both
+    neighbours (it reads the first conv's image at stage 0 and stores the
+    last conv's operand), and the result equals the unlinked program's and a
+    float64 evaluation."""
+    from test_gpu_block import _ref as block_ref, _specs
+
+    C, T, B = 128, 1003, 2
+    g = torch.Generator().manual_seed(11)
+    specs = _specs(C, g)
+    cws = [E.make_conv(sp, DEV, prec=1) for sp in specs]
+    bw = E.BlockW(C, "none", None, *cws, None, E.prep_fused(specs, C, 1, DEV))
+    wa, wb = (torch.randn(C, C, 3, generator=g) * 0.05 for _ in range(2))
+    ca, cb = (E.make_conv(E.ConvSpec(w.numpy(), C, 1, 1, 1, 0.2, np.zeros(C, np.float32)), DEV, prec=1)
+              for w in (wa, wb))
+    x = torch.randn(B, C, T, generator=g)
+    h_ref = _ref(wa, torch.zeros(C), x, 1, 3, 0.2, None, 1.0)
+    y_ref, _ = block_ref(specs, h_ref)
+    z_ref = _ref(wb, torch.zeros(C), y_ref, 1, 3, 0.2, None, 1.0)
+    xa = E.Act(x.to(DEV))
+    outs = {}
+    saved = L.ADD_HOOK
+    try:
+        for linked in (False, True):
+            E.begin_record(1 if linked else 0, DEV)
+            prog = L.Program()
+            h, y, z = (E.new_act(B, C, T, DEV) for _ in range(3))
+            tA, tB = E.new_act(B, C, T, DEV), E.new_act(B, C, T, DEV)
+            prog.add(L.OP_CONV, E.conv_desc(ca, xa, h))
+            E.rec_block(prog, bw, h, y, tA, tB)
+            prog.add(L.OP_CONV, E.conv_desc(cb, y, z))
+            E.end_record()
+            links = getattr(prog, "split_links", [])
+            assert len(links) == (2 if linked else 0), links
+            prog.run(torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            outs[linked] = (y.t.cpu().double(), z.t.cpu().double())
+    finally:
+        E.end_record()
+        L.ADD_HOOK = saved
+    for k in (0, 1):
+        a, b = outs[True][k], outs[False][k]
+        assert ((a - b).norm() / b.norm()).item() < 1e-6
+    assert ((outs[True][0] - y_ref).norm() / y_ref.norm()).item() < 1e-5
+    assert ((outs[True][1] - z_ref).norm() / z_ref.norm()).item() < 1e-5
