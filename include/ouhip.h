@@ -218,9 +218,10 @@ typedef struct ou_gru_desc {
     int32_t ws_zeroed;         /* nonzero: the caller zeroed the workspace before */
                                /* the first launch on it (per replay); launches   */
                                /* leave it reusable, so no per-launch memset --   */
-                               /* launches of steps < 5 still clear it (the tags  */
-                               /* T-1, T-2 a launch leaves must not match a new   */
-                               /* launch's first two polls, tags 1 and 2)         */
+                               /* launches of steps < 5 clear it before and after */
+                               /* they run (the tags T-1, T-2 a launch leaves     */
+                               /* must not match a new launch's first two polls,  */
+                               /* tags 1 and 2): launches of any T may share it   */
     int32_t _pad;
 } ou_gru_desc;
 

@@ -1099,6 +1099,8 @@ extern "C" int ou_block(const ou_block_desc* dp, void* stream)
     const int64_t lim = kBlkSentinel;
     if ((int64_t)d.channels * d.h_cstride * 4 >= lim || (int64_t)d.channels * d.y_cstride * 4 >= lim ||
         (d.res2 && (int64_t)d.channels * d.r2_cstride * 4 >= lim) ||
+        (d.sc && (int64_t)d.channels * d.sc_cstride * 4 >= lim) ||
+        (d.cond_out && (int64_t)d.channels * d.co_cstride * 4 >= lim) ||
         (d.e && (int64_t)2 * d.channels * d.e_cstride * 4 >= lim))
         return ou_fail(-1, "block: a per-item tensor of %d x %lld floats exceeds the 32-bit buffer range", d.channels,
                        (long long)d.h_cstride);

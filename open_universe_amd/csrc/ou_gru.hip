@@ -697,6 +697,16 @@ extern "C" int64_t ou_gru_workspace_bytes(int hidden, int batch)
            (int64_t)sizeof(uint64_t);
 }
 
+// after a launch: a short one (steps < 5) on a ws_zeroed workspace leaves it
+// zeroed for the next launch on it, whatever that one's T
+static int gru_after(const ou_gru_desc& d, hipStream_t s)
+{
+    const int rc = ou_check_launch("gru");
+    if (rc == 0 && d.ws_zeroed && d.steps < 5)
+        OU_HIP_CHECK(hipMemsetAsync(d.granules, 0, ou_gru_workspace_bytes(d.hidden, d.batch), s), "gru: memset");
+    return rc;
+}
+
 extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
 {
     if (!dp) return ou_fail(-1, "gru: null descriptor");
@@ -721,7 +731,8 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
     // tags 1 and 2, and every later poll of a slot follows one that already
     // saw this launch's tag there.  So with T - 2 >= 3 (T >= 5) a workspace
     // zeroed once per replay serves every launch of it (ws_zeroed); shorter
-    // launches clear it themselves.
+    // launches clear it themselves, before they run and again after (their
+    // tags T - 1, T - 2 are < 3: a following launch could match them).
     // a launch continuing a split recurrence (t_begin > 0) starts from hstate:
     // the tags the previous launches left are all older than the ones it polls
     if ((!d.ws_zeroed && d.t_begin == 0) || d.steps < 5)
@@ -738,7 +749,7 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
         case 512: launch_ks_all<512>(d, kflags, s); break;
         default: return ou_fail(-1, "gru: unsupported hidden size %d", d.hidden);
         }
-        return ou_check_launch("gru");
+        return gru_after(d, s);
     }
     const int nb = d.batch >= kMaxBatchPerWG ? kMaxBatchPerWG : (d.batch >= 2 ? 2 : 1);
     const int nchains = 2 * ((d.batch + nb - 1) / nb);
@@ -757,5 +768,5 @@ extern "C" int ou_gru(const ou_gru_desc* dp, void* stream)
     case 384: launch_h<384>(d, nb, nchains, flags, s); break;
     default: return ou_fail(-1, "gru: unsupported hidden size %d", d.hidden);
     }
-    return ou_check_launch("gru");
+    return gru_after(d, s);
 }

@@ -510,26 +510,31 @@ int ou_program_trace(ou_program* p, void* stream, float* t0, float* t1)
             if ((rc = shared_stream(&g_side[dev][l - 1], &side[l - 1]))) return rc;
     }
     const size_t n = p->ops.size();
+    // every failure below sets rc and falls through: whatever was enqueued is
+    // drained and the timing events destroyed on every path
     std::vector<hipEvent_t> ev(2 * n + 1, nullptr);
-    for (auto& e : ev) OU_HIP_CHECK(hipEventCreate(&e), "event create");
-    (void)hipEventRecord(ev[2 * n], s0);
+    for (auto& e : ev)
+        if (rc == 0 && hipEventCreate(&e) != hipSuccess) rc = ou_fail(-100, "program_trace: event create");
+    if (rc == 0) (void)hipEventRecord(ev[2 * n], s0);
     hipStream_t cur = s0;
     for (size_t i = 0; i < n && rc == 0; ++i) {
         const auto& o = p->ops[i];
         if (is_sync(o.kind)) {
             const int v = ((const ou_sync_args*)o.desc.data())->id;
+            hipError_t e = hipSuccess;
             if (o.kind == OU_OP_LANE) cur = v == 0 ? s0 : side[v - 1];
-            else if (o.kind == OU_OP_SIGNAL) OU_HIP_CHECK(hipEventRecord(p->events[v], cur), "program signal");
-            else OU_HIP_CHECK(hipStreamWaitEvent(cur, p->events[v], 0), "program wait");
+            else if (o.kind == OU_OP_SIGNAL) e = hipEventRecord(p->events[v], cur);
+            else e = hipStreamWaitEvent(cur, p->events[v], 0);
+            if (e != hipSuccess) rc = ou_fail(-100, "program_trace: lane sync: %s", hipGetErrorString(e));
             continue;
         }
         (void)hipEventRecord(ev[2 * i], cur);
         rc = run_op(o.kind, o.desc.data(), cur);
         (void)hipEventRecord(ev[2 * i + 1], cur);
     }
-    if (rc == 0) {
-        hipError_t e = hipDeviceSynchronize();
-        if (e != hipSuccess) rc = ou_fail(-100, "trace sync: %s", hipGetErrorString(e));
+    {
+        hipError_t e = hipDeviceSynchronize();   // also after a failure: the side lanes may still run
+        if (rc == 0 && e != hipSuccess) rc = ou_fail(-100, "trace sync: %s", hipGetErrorString(e));
     }
     for (size_t i = 0; i < n && rc == 0; ++i) {
         float a = -1.f, b = -1.f;
@@ -539,7 +544,8 @@ int ou_program_trace(ou_program* p, void* stream, float* t0, float* t1)
         }
         t0[i] = a, t1[i] = b;
     }
-    for (auto& e : ev) (void)hipEventDestroy(e);
+    for (auto& e : ev)
+        if (e) (void)hipEventDestroy(e);
     return rc;
 }
 
@@ -548,25 +554,27 @@ int ou_program_profile(ou_program* p, void* stream, float* ms)
     if (!p || !ms) return ou_fail(-1, "program_profile: null");
     hipStream_t s = (hipStream_t)stream;
     const size_t n = p->ops.size();
-    std::vector<hipEvent_t> ev(n + 1);
-    for (auto& e : ev) OU_HIP_CHECK(hipEventCreate(&e), "event create");
+    std::vector<hipEvent_t> ev(n + 1, nullptr);
     int rc = 0;
-    (void)hipEventRecord(ev[0], s);
+    for (auto& e : ev)
+        if (rc == 0 && hipEventCreate(&e) != hipSuccess) rc = ou_fail(-100, "program_profile: event create");
+    if (rc == 0) (void)hipEventRecord(ev[0], s);
     // lanes are ignored here: the op list in order is a valid serial schedule
     for (size_t i = 0; i < n && rc == 0; ++i) {
         if (!is_sync(p->ops[i].kind)) rc = run_op(p->ops[i].kind, p->ops[i].desc.data(), s);
         (void)hipEventRecord(ev[i + 1], s);
     }
-    if (rc == 0) {
-        hipError_t e = hipEventSynchronize(ev[n]);
-        if (e != hipSuccess) rc = ou_fail(-100, "profile sync: %s", hipGetErrorString(e));
+    {
+        hipError_t e = hipStreamSynchronize(s);   // also after a failure
+        if (rc == 0 && e != hipSuccess) rc = ou_fail(-100, "profile sync: %s", hipGetErrorString(e));
     }
     for (size_t i = 0; i < n && rc == 0; ++i) {
         float t = 0.f;
         (void)hipEventElapsedTime(&t, ev[i], ev[i + 1]);
         ms[i] = t;
     }
-    for (auto& e : ev) (void)hipEventDestroy(e);
+    for (auto& e : ev)
+        if (e) (void)hipEventDestroy(e);
     return rc;
 }
 

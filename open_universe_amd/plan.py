@@ -198,6 +198,11 @@ class EnhancePlan(_PlanBase):
         # lane 0 waits for them right before the first decoder.  Not with the
         # aux / warm-start paths, whose initial sample needs the conditioner.
         self.overlap = E.overlap_enabled() and not use_aux_signal and warm_start is None
+        # the chunked score pass (Engine.chunk_plan): its chunks keep the whole
+        # ops' tiles, so a chunked plan records no split-image links at all
+        chunks = eng.chunk_plan(B, Tp, force=chunk is True) if chunk is not False and not use_aux_signal else None
+        if chunks is not None:
+            L.ADD_HOOK = None
         ev_cond = {}
         after_level = None
         if self.overlap:
@@ -257,9 +262,7 @@ class EnhancePlan(_PlanBase):
             self.WIN = torch.from_numpy(win).to(dev)
             # the chunked score pass (Engine.chunk_plan): GRU segments on lane
             # 0, conv chunks on side lanes 2 / 3 (rec_score_chunked)
-            self.chunks = eng.chunk_plan(B, Tp, force=chunk is True) if chunk is not False else None
-            if self.chunks is not None:   # chunks keep the whole ops' tiles: no split-image links
-                L.ADD_HOOK = None
+            self.chunks = chunks
             self.sb = eng.alloc_score(B, Tp, chunked=self.chunks is not None)
             E.rec_gru_ws_zero(p, self.sb["gran"])   # lane 0, ahead of the first score GRU
             # initial sample (universe.py:322-331)

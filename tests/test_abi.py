@@ -111,3 +111,38 @@ def test_conv_pack_split_layout():
                             ref[mt, g, k, lane, j] = float(w[row, c, k]) * 2.0**e
     assert np.abs(a - ref).max() <= 2.0**-21 * np.abs(ref).max()
     assert np.count_nonzero(ref) == np.count_nonzero(h[:, :, 0])
+
+
+@pytest.mark.parametrize("field", ["x", "y", "res1"])
+def test_conv_rejects_per_item_tensors_past_the_buffer_range(field):
+    """Kernels address a batch item through a 32-bit buffer resource with a
+    sentinel offset for "outside": ou_conv refuses a per-item tensor that
+    reaches the sentinel (host-side validation, refused before any HIP call)."""
+    lib = L.load()
+    d = L.ConvDesc()
+    d.x = d.w = d.y = 256
+    d.m, d.cin, d.kt, d.frame, d.rout, d.batch = 64, 64, 3, 1, 1, 1
+    d.n_frames = d.in_len = d.out_len = 1000
+    d.x_cstride = d.y_cstride = d.r1_cstride = 1000
+    big = (1 << 31) // (4 * 64)   # 64 channels x big floats = 2 GiB
+    if field == "res1":
+        d.res1 = 256
+    setattr(d, f"{'r1' if field == 'res1' else field}_cstride", big)
+    assert lib.ou_conv(ctypes.byref(d), None) == -1
+    assert b"32-bit buffer range" in lib.ou_last_error()
+
+
+@pytest.mark.parametrize("field", ["h", "y", "sc", "co"])
+def test_block_rejects_per_item_tensors_past_the_buffer_range(field):
+    lib = L.load()
+    d = L.BlockDesc()
+    d.h = d.y = d.w[0] = d.w[1] = d.w[2] = 256
+    d.channels, d.length, d.batch, d.prec = 64, 1000, 1, 1
+    d.h_cstride = d.y_cstride = d.sc_cstride = d.co_cstride = 1000
+    if field == "sc":
+        d.sc = 256
+    if field == "co":
+        d.cond_out = 256
+    setattr(d, f"{field}_cstride", (1 << 31) // (4 * 64))
+    assert lib.ou_block(ctypes.byref(d), None) == -1
+    assert b"32-bit buffer range" in lib.ou_last_error()

@@ -123,17 +123,18 @@ def test_gru_layer(pp16):
     assert rel_rms(y.t.cpu(), ref) < 1e-5
 
 
-@pytest.mark.parametrize("T", [2, 3, 4, 5, 6])
-def test_gru_ws_zeroed_short_launches_back_to_back(pp16, T):
+@pytest.mark.parametrize("Ts", [(2, 2, 2), (3, 3, 3), (4, 4, 4), (5, 5, 5), (6, 6, 6), (4, 6, 9), (3, 7, 2)])
+def test_gru_ws_zeroed_short_launches_back_to_back(pp16, Ts):
     """Launches that skip the per-launch memset (ou_gru_desc.ws_zeroed) on one
     workspace zeroed once: a short launch's leftover step tags (T-1, T-2) must
     not satisfy the next launch's first polls (tags 1, 2) -- launches of fewer
-    than 5 steps clear the workspace themselves.  Each of three back-to-back
+    than 5 steps clear the workspace before and after they run, so launches
+    of different T (4 then 6) share it too.  Each of three back-to-back
     launches must equal the same layer run alone with a per-launch memset."""
     d, cfg, m = pp16
     eng = m._get_engine()
     B = 2
-    xs = [torch.randn(B, 512, T, generator=torch.Generator().manual_seed(20 + i)) * 0.5 for i in range(3)]
+    xs = [torch.randn(B, 512, T, generator=torch.Generator().manual_seed(20 + i)) * 0.5 for i, T in enumerate(Ts)]
     gran = torch.zeros(L.load().ou_gru_workspace_bytes(256, B) // 8, dtype=torch.int64, device=DEV)
 
     def run(ws_zeroed, inputs):
@@ -144,6 +145,7 @@ def test_gru_ws_zeroed_short_launches_back_to_back(pp16, T):
                 E.rec_gru_ws_zero(prog, gran)
             outs = []
             for x in inputs:
+                T = x.shape[2]
                 xa, gi, y = E.Act(x.to(DEV)), E.new_act(B, 1536, T, DEV), E.new_act(B, 512, T, DEV)
                 E.rec_gru(prog, eng.s_gru, 0, xa, gi, y, gran, eng.status)
                 outs.append((xa, gi, y))
