@@ -59,6 +59,32 @@ int shared_stream(hipStream_t* slot, hipStream_t* out)
     return 0;
 }
 
+// Side lanes given the device's highest stream priority (OUHIP_LANE_PRIO,
+// a digit string of side-lane ids, default "12": the conditioner lane and the
+// mel front end's).  The first diffusion step waits on the conditioner, the
+// score lane beside it has slack: the dispatcher serves the conditioner's
+// workgroups first.  Captured graphs carry the priority per node
+// (hipGraphInstantiateFlagUseNodePriority).
+bool lane_prio(int lane)
+{
+    static const char* env = getenv("OUHIP_LANE_PRIO");
+    const char* v = env ? env : "12";
+    for (; *v; ++v)
+        if (*v - '0' == lane) return true;
+    return false;
+}
+
+int side_stream(int dev, int lane, hipStream_t* out)
+{
+    hipStream_t* slot = &g_side[dev][lane - 1];
+    if (!*slot && lane_prio(lane)) {
+        int least = 0, greatest = 0;
+        OU_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priority range");
+        OU_HIP_CHECK(hipStreamCreateWithPriority(slot, hipStreamNonBlocking, greatest), "program stream");
+    }
+    return shared_stream(slot, out);
+}
+
 int current_device(int* dev)
 {
     OU_HIP_CHECK(hipGetDevice(dev), "program: device");
@@ -180,7 +206,7 @@ static int run_lanes(ou_program* p, hipStream_t s0)
         int dev = 0;
         if ((rc = current_device(&dev))) return rc;
         for (int l = 1; l < nl; ++l)
-            if ((rc = shared_stream(&g_side[dev][l - 1], &side[l - 1]))) return rc;
+            if ((rc = side_stream(dev, l, &side[l - 1]))) return rc;
     }
     hipStream_t cur = s0;
     static const bool trace = std::getenv("OUHIP_PROG_TRACE") != nullptr;   // diagnostics
@@ -379,7 +405,7 @@ int ou_program_capture(ou_program* p)
     }
     if (e != hipSuccess) return ou_fail(-100, "end capture: %s", hipGetErrorString(e));
     p->graph = g;
-    e = hipGraphInstantiate(&p->exec, g, nullptr, nullptr, 0);
+    e = hipGraphInstantiateWithFlags(&p->exec, g, hipGraphInstantiateFlagUseNodePriority);
     if (e != hipSuccess) {
         drop_graph(p);
         return ou_fail(-100, "graph instantiate: %s", hipGetErrorString(e));
@@ -452,7 +478,7 @@ static int launch_segments(ou_program* p, hipStream_t s0)
         int dev = 0;
         if ((rc = current_device(&dev))) return rc;
         for (int l = 1; l < nl; ++l)
-            if ((rc = shared_stream(&g_side[dev][l - 1], &side[l - 1]))) return rc;
+            if ((rc = side_stream(dev, l, &side[l - 1]))) return rc;
     }
     hipStream_t cur = s0;
     size_t si = 0;
@@ -507,7 +533,7 @@ int ou_program_trace(ou_program* p, void* stream, float* t0, float* t1)
         int dev = 0;
         if ((rc = current_device(&dev))) return rc;
         for (int l = 1; l < nl; ++l)
-            if ((rc = shared_stream(&g_side[dev][l - 1], &side[l - 1]))) return rc;
+            if ((rc = side_stream(dev, l, &side[l - 1]))) return rc;
     }
     const size_t n = p->ops.size();
     // every failure below sets rc and falls through: whatever was enqueued is

@@ -54,6 +54,7 @@ KSWS_BYTES = 64 << 20
 RS_BIT = 1 << 14      # ConvDesc.tile bit: the register-streamed conv kernel (conv_rkernel)
 
 _REC = None   # set while a plan records (begin_record)
+_TUNE_BATCH = None   # the plan's batch while it records sub-batches (ConvTuner.geometry)
 # lane the recorder is on (plan lanes run concurrently) and the plan slot
 # (plans of one model that may run at the same time on different streams,
 # Universe.enhance_many): convs recorded on (slot, lane) use K-slice workspace
@@ -70,6 +71,24 @@ def set_lane(prog, i):
     assert 0 <= i < MAX_LANES
     prog.lane(i)
     _LANE = i
+
+
+SUB_LANE = 3   # the second score sub-batch's lane (plan.EnhancePlan)
+
+
+def score_sub_batches(B):
+    """[(b0, b1), ...]: the score network's batch split in two halves on two
+    lanes (EnhancePlan), or None.  At small batches the bottleneck GRU's
+    serial step chain leaves most of the chip idle; with two sub-batches one
+    half's GRU runs beside the other half's convolutions.  Default for
+    2 <= B <= 6; OUHIP_SUB_BATCH=0 / 1 forces it off / on (B >= 2)."""
+    import os
+
+    v = os.environ.get("OUHIP_SUB_BATCH", "auto")
+    if B < 2 or v == "0" or (v != "1" and not 2 <= B <= 6):
+        return None
+    h = (B + 1) // 2
+    return [(0, h), (h, B)]
 
 
 def overlap_enabled():
@@ -899,8 +918,11 @@ class ConvTuner:
 
     @staticmethod
     def geometry(d):
-        # bool(ks_ws): K-slice tiles are only valid with a workspace
-        return (d.m, d.cin, d.frame, d.kt, d.pad, d.batch, d.rout, bool(d.res1), bool(d.film), bool(d.res2),
+        # bool(ks_ws): K-slice tiles are only valid with a workspace.  The
+        # batch is the plan's (_TUNE_BATCH while a plan records sub-batches):
+        # a sub-batched plan and the whole-batch one run the same tiles
+        b = _TUNE_BATCH if _TUNE_BATCH is not None else d.batch
+        return (d.m, d.cin, d.frame, d.kt, d.pad, b, d.rout, bool(d.res1), bool(d.film), bool(d.res2),
                 bool(d.in_scale), d.prec, bool(d.ks_ws), bool(d.xs))
 
     @classmethod
@@ -1293,7 +1315,7 @@ class Engine:
         return [n - 1 - l for l in range(n)]
 
     def rec_score(self, prog, bufs, x: Act, film_base, film_bs, in_scale=0, sc_list=None, before_level=None,
-                  head=None):
+                  head=None, after_encoder=None):
         """ScoreNetwork.forward (score.py:278-298).  The encoder and the
         bottleneck GRU do not read the conditions (score.py:284-286), and
         decoder level l reads only condition l: ``before_level(l)`` runs right
@@ -1301,7 +1323,8 @@ class Engine:
         descriptor, h unset) the head is recorded too and None is returned;
         otherwise the decoder output Act is returned.  When the 32-channel end
         blocks are fused, the input conv runs inside the first encoder block and
-        the head inside the last decoder block (ou_block kEpiIn / kEpiHead)."""
+        the head inside the last decoder block (ou_block kEpiIn / kEpiHead).
+        ``after_encoder()`` runs between the encoder and the bottleneck GRU."""
         n_lvl = len(self.s_enc)
         nr = len(self.rates)
         fb = lambda j: film_base + 4 * self.film_off[j]
@@ -1320,6 +1343,8 @@ class Engine:
             rec_block(prog, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
                       film=fb(i), film_bs=film_bs, x_in=x_in,
                       e_out=bufs[f"E{i+1}"] if bw.kind == "down" else None)
+        if after_encoder is not None:
+            after_encoder()
         # bottleneck GRU, fused with the decoder's first residual add
         top = n_lvl - 1
         prog.label = "score gru"

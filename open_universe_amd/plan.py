@@ -263,8 +263,19 @@ class EnhancePlan(_PlanBase):
             # the chunked score pass (Engine.chunk_plan): GRU segments on lane
             # 0, conv chunks on side lanes 2 / 3 (rec_score_chunked)
             self.chunks = chunks
-            self.sb = eng.alloc_score(B, Tp, chunked=self.chunks is not None)
-            E.rec_gru_ws_zero(p, self.sb["gran"])   # lane 0, ahead of the first score GRU
+            # small batches: the score network as two sub-batches on lanes 0
+            # and E.SUB_LANE (E.score_sub_batches), the second half's first
+            # step starting behind the first half's encoder, so one half's
+            # GRU chain runs beside the other half's convolutions
+            subs = E.score_sub_batches(B) if chunks is None else None
+            self.subs = subs
+            if subs is None:
+                sbs = [eng.alloc_score(B, Tp, chunked=self.chunks is not None)]
+            else:
+                sbs = [eng.alloc_score(b1 - b0, Tp) for b0, b1 in subs]
+            self.sb = sbs[0]
+            for sb in sbs:
+                E.rec_gru_ws_zero(p, sb["gran"])   # lane 0, ahead of the first score GRU
             # initial sample (universe.py:322-331)
             if warm_start is None:
                 p.add(L.OP_SCALE, L.ScaleArgs(z=self.NZ.data_ptr(), y=self.X.ptr, n=B * Tp,
@@ -274,20 +285,47 @@ class EnhancePlan(_PlanBase):
                                               scale=float(sig[n_start]), add=self.SIG.ptr))
             film_base = self.FILM.data_ptr()
             zi = 1
-            for n in steps:
-                in_scale = self.WIN[n].data_ptr() if edm is not None else 0
-                join = (lambda l: p.wait(ev_cond[l])) if (ev_cond and n == steps[0]) else None
-                last = n == n_steps - 1
-                z_ptr = 0 if last else self.NZ[zi].data_ptr()
-                zi += 0 if last else 1
-                head = eng.head_desc(None, self.X.ptr, B, Tp, mode=2 if last else 1,
-                                     x_ptr=self.X.ptr, z_ptr=z_ptr, coef=coefs[n])
-                if self.chunks is not None:
-                    eng.rec_score_chunked(p, self.sb, self.X, film_base + 4 * n * eng.film_rows, 0, self.chunks,
-                                          in_scale=in_scale, sc_list=self.SC, before_level=join, head=head)
-                else:
-                    eng.rec_score(p, self.sb, self.X, film_base + 4 * n * eng.film_rows, 0,
-                                  in_scale=in_scale, sc_list=self.SC, before_level=join, head=head)
+            ev_sub = []
+            saved_tb = E._TUNE_BATCH
+            if subs is not None:
+                E._TUNE_BATCH = B   # the sub-batches run the whole batch's tiles
+            try:
+                for n in steps:
+                    join = (lambda l: p.wait(ev_cond[l])) if (ev_cond and n == steps[0]) else None
+                    last = n == n_steps - 1
+                    film = film_base + 4 * n * eng.film_rows
+                    if self.chunks is not None:
+                        in_scale = self.WIN[n].data_ptr() if edm is not None else 0
+                        head = eng.head_desc(None, self.X.ptr, B, Tp, mode=2 if last else 1, x_ptr=self.X.ptr,
+                                             z_ptr=0 if last else self.NZ[zi].data_ptr(), coef=coefs[n])
+                        eng.rec_score_chunked(p, self.sb, self.X, film, 0, self.chunks,
+                                              in_scale=in_scale, sc_list=self.SC, before_level=join, head=head)
+                    for k, (b0, b1) in enumerate(subs or [(0, B)] if self.chunks is None else []):
+                        whole = subs is None
+                        xk = self.X if whole else Act(self.X.t[b0:b1])
+                        in_scale = self.WIN[n, b0:].data_ptr() if edm is not None else 0
+                        head = eng.head_desc(None, xk.ptr, b1 - b0, Tp, mode=2 if last else 1, x_ptr=xk.ptr,
+                                             z_ptr=0 if last else self.NZ[zi, b0].data_ptr(), coef=coefs[n])
+                        sc = self.SC if whole else [Act(a.t[b0:b1]) for a in self.SC]
+                        after = None
+                        if k == 1:
+                            E.set_lane(p, E.SUB_LANE)
+                            if n == steps[0]:
+                                p.wait(ev_sub[0])   # behind the first half's first encoder
+                        elif not whole and n == steps[0]:
+                            after = lambda: ev_sub.append(p.signal())
+                        eng.rec_score(p, sbs[k], xk, film, 0, in_scale=in_scale, sc_list=sc, before_level=join,
+                                      head=head, after_encoder=after)
+                        if k == 1:
+                            E.set_lane(p, 0)
+                    zi += 0 if last else 1
+            finally:
+                E._TUNE_BATCH = saved_tb
+            if subs is not None:   # lane 0 joins the second half
+                E.set_lane(p, E.SUB_LANE)
+                ev_end = p.signal()
+                E.set_lane(p, 0)
+                p.wait(ev_end)
             x_final = self.X
             if self.chunks is not None and ev_cond:
                 # the side lanes waited on the conditions; lane 0 joins lane 1

@@ -9,6 +9,7 @@
 #   levels:CFG       tools/gpu_level_pmc.sh (per-op conv-stack table)
 #   bench:CFG        bench.py --config CFG, default arguments (the driver's line)
 #   shards           C4 at the per-rank batches of 2/4/8 GPUs (B = 16, 8, 4)
+#   subbatch[:B]     C4 at per-rank batch B (default 4), score sub-batches off / on, alternating
 #   critical         tools/critical_path.py --config c2 (lane timeline, first step)
 #   chunk:CFG        whole pass vs chunked pass (OUHIP_CHUNK=0/1) at CFG
 #   ab:VAR=[A,]B     C2 bench with VAR=A / B / A / B (A defaults to 0; same box, alternating)
@@ -50,6 +51,14 @@ for step in "$@"; do
         for b in 16 8 4; do
             OUHIP_TUNE_CACHE="$O/tune_${TAG}_c4.json" bench "$O/bench_${TAG}_c4_b$b" 300 --config c4 --batch $b \
                 --steps 4 --warmup 1 --no-f32-pass --no-cpu-baseline --traffic-json "" || exit 1
+        done ;;
+    subbatch)
+        for i in 1 2; do
+            for v in 0 1; do
+                OUHIP_SUB_BATCH=$v OUHIP_TUNE_CACHE="$O/tune_${TAG}_c4.json" bench "$O/bench_${TAG}_c4_b${arg:-4}_sub${v}_$i" \
+                    300 --config c4 --batch "${arg:-4}" --steps 3 --warmup 1 --no-f32-pass --no-cpu-baseline \
+                    --traffic-json "" || exit 1
+            done
         done ;;
     critical)
         OUHIP_TUNE_CACHE="$O/tune_${TAG}_c2.json" timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 \
