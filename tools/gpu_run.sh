@@ -8,6 +8,7 @@
 #   profile:CFG      tools/gpu_profile.sh (bench line, kernel trace, FETCH/WRITE PMC passes)
 #   levels:CFG       tools/gpu_level_pmc.sh (per-op conv-stack table)
 #   bench:CFG        bench.py --config CFG, default arguments (the driver's line)
+#   benchpmc:CFG     profile:CFG, then bench:CFG quoting `traffic` from that PMC summary
 #   shards           C4 at the per-rank batches of 2/4/8 GPUs (B = 16, 8, 4)
 #   subbatch[:B]     C4 at per-rank batch B (default 4), score sub-batches off / on, alternating
 #   critical         tools/critical_path.py --config c2 (lane timeline, first step)
@@ -47,6 +48,13 @@ for step in "$@"; do
         head -24 "$O/levels_${arg}_$TAG.txt" ;;
     bench)
         OUHIP_TUNE_CACHE="$O/tune_${TAG}_$arg.json" bench "$O/bench_${TAG}_config_$arg" 600 --config "$arg" || exit 1 ;;
+    benchpmc)   # the PMC passes first, so the bench line carries its own library's traffic
+        if [ "$arg" = c2 ]; then bash tools/gpu_profile.sh "${TAG}_pmc" c2 > /dev/null || exit 1
+        else bash tools/gpu_profile.sh "${TAG}_pmc_$arg" "$arg" --steps 4 --warmup 1 --no-f32-pass --no-queued \
+            > /dev/null || exit 1; fi
+        pt="${TAG}_pmc$([ "$arg" = c2 ] || echo "_$arg")"   # the profile's tag: same tiles (its tuning cache)
+        OUHIP_TUNE_CACHE="$O/tune_$pt.json" bench "$O/bench_${TAG}_config_$arg" 600 --config "$arg" \
+            --traffic-json "$O/pmc_$pt.json" || exit 1 ;;
     shards)
         for b in 16 8 4; do
             OUHIP_TUNE_CACHE="$O/tune_${TAG}_c4.json" bench "$O/bench_${TAG}_c4_b$b" 300 --config c4 --batch $b \
