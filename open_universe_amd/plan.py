@@ -273,7 +273,7 @@ class EnhancePlan(_PlanBase):
                 sbs = [eng.alloc_score(B, Tp, chunked=self.chunks is not None)]
             else:
                 sbs = [eng.alloc_score(b1 - b0, Tp) for b0, b1 in subs]
-            self.sb = sbs[0]
+            self.sb, self._sbs = sbs[0], sbs
             for sb in sbs:
                 E.rec_gru_ws_zero(p, sb["gran"])   # lane 0, ahead of the first score GRU
             # initial sample (universe.py:322-331)
