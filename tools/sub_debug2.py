@@ -37,7 +37,8 @@ def snap():
                 out[f"{name}.{k}"] = t.clone()
             elif isinstance(v, list):
                 for i, a in enumerate(v):
-                    out[f"{name}.{k}{i}"] = a.t.clone()
+                    if hasattr(a, "t"):
+                        out[f"{name}.{k}{i}"] = a.t.clone()
     for i, a in enumerate(p.SC):
         out[f"SC{i}"] = a.t.clone()
     out["X"], out["OUT"] = p.X.t.clone(), p.OUT.clone()
