@@ -45,14 +45,33 @@ def snap():
     return out
 
 
-for graph in (False, False):
-    # poison every buffer first: a read before its write in this replay shows
-    pass
+def poison():
+    """NaN into every activation and split-image buffer of the plan (not the
+    GRU workspaces, which a replay zeroes itself): a read of a value this
+    replay did not write shows as a NaN output."""
+    for name, bufs in [("cb", p.cb)] + [(f"sb{k}", sb) for k, sb in enumerate(getattr(p, "_sbs", [p.sb]))]:
+        for k, v in bufs.items():
+            if k == "gran":
+                continue
+            for a in (v if isinstance(v, list) else [v]):
+                t = getattr(a, "t", a)
+                if isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32:
+                    t.fill_(float("nan"))
+    for a in p.SC:
+        a.t.fill_(float("nan"))
+    for buf in getattr(p.prog, "split_bufs", {}).values():
+        buf.fill_(0x7E00)
+    torch.cuda.synchronize()
+
+
 y1 = p(mix, torch.Generator(device=DEV).manual_seed(5), use_graph=False).clone()
 s1 = snap()
-y2 = p(mix, torch.Generator(device=DEV).manual_seed(5), use_graph=False).clone()
+for i, graph in enumerate((False, False, True, True)):
+    poison()
+    y2 = p(mix, torch.Generator(device=DEV).manual_seed(5), use_graph=graph).clone()
+    print(f"poisoned replay {i} graph {int(graph)}: finite {bool(torch.isfinite(y2).all())} "
+          f"diff vs first {(y1 - y2).abs().nan_to_num(1e9).max().item():.3g}", flush=True)
 s2 = snap()
-print("out diff", (y1 - y2).abs().max().item())
 for k in s1:
     a, b = s1[k], s2[k]
     if not torch.equal(a, b):
