@@ -64,14 +64,25 @@ def poison():
     torch.cuda.synchronize()
 
 
+def nan_bufs(s):
+    return {k for k, v in s.items() if torch.isnan(v).any()}
+
+
+if os.environ.get("DBG_POISON_FIRST", "1") == "1":
+    poison()
 y1 = p(mix, torch.Generator(device=DEV).manual_seed(5), use_graph=False).clone()
 s1 = snap()
+print(f"first replay: finite {bool(torch.isfinite(y1).all())}", flush=True)
+unused = None
 for i, graph in enumerate((False, False, True, True)):
     poison()
     y2 = p(mix, torch.Generator(device=DEV).manual_seed(5), use_graph=graph).clone()
     print(f"poisoned replay {i} graph {int(graph)}: finite {bool(torch.isfinite(y2).all())} "
           f"diff vs first {(y1 - y2).abs().nan_to_num(1e9).max().item():.3g}", flush=True)
+    nb = nan_bufs(snap())
+    unused = nb if unused is None else unused & nb
 s2 = snap()
+print("NaN after the first replay only:", sorted(nan_bufs(s1) - unused))
 for k in s1:
     a, b = s1[k], s2[k]
     if not torch.equal(a, b):
