@@ -454,6 +454,7 @@ class Program:
         self.label = ""         # phase label recorded with each op (engine sets it; reports only)
         self.labels = []
         self.prev_op = {}       # lane -> (op index, op, desc): the lane's last op, when a conv or block
+        self.descs = []         # each op's descriptor (patched in place by the split-image hook; hazards.py)
 
     def add(self, op, desc):
         assert isinstance(desc, OP_STRUCT[op])
@@ -471,6 +472,7 @@ class Program:
             self.prev_op[self.cur_lane] = (len(self.flops), op, desc)
         elif op not in (OP_LANE, OP_SIGNAL):   # a wait may hand over data another lane wrote
             self.prev_op.pop(self.cur_lane, None)
+        self.descs.append(desc)
         self.flops.append(float(getattr(desc, "_flops", 0.0)))
         self.bytes.append(float(getattr(desc, "_bytes", 0.0)))
         self.lanes.append(self.cur_lane)

@@ -273,7 +273,10 @@ class EnhancePlan(_PlanBase):
                 sbs = [eng.alloc_score(B, Tp, chunked=self.chunks is not None)]
             else:
                 sbs = [eng.alloc_score(b1 - b0, Tp) for b0, b1 in subs]
-            self.sb, self._sbs = sbs[0], sbs
+            # the plan owns every buffer its program points at: the second
+            # sub-batch's buffers too (freed, the caching allocator would hand
+            # their memory to the next tensor while the program still used it)
+            self.sb, self.score_bufs = sbs[0], sbs
             for sb in sbs:
                 E.rec_gru_ws_zero(p, sb["gran"])   # lane 0, ahead of the first score GRU
             # initial sample (universe.py:322-331)

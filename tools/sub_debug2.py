@@ -30,7 +30,7 @@ p = EnhancePlan(eng, B, T, n_steps, 1.3)
 
 def snap():
     out = {}
-    for name, bufs in [("cb", p.cb)] + [(f"sb{k}", sb) for k, sb in enumerate(getattr(p, "_sbs", [p.sb]))]:
+    for name, bufs in [("cb", p.cb)] + [(f"sb{k}", sb) for k, sb in enumerate(getattr(p, "score_bufs", [p.sb]))]:
         for k, v in bufs.items():
             t = getattr(v, "t", v)
             if isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32:
@@ -49,7 +49,7 @@ def poison():
     """NaN into every activation and split-image buffer of the plan (not the
     GRU workspaces, which a replay zeroes itself): a read of a value this
     replay did not write shows as a NaN output."""
-    for name, bufs in [("cb", p.cb)] + [(f"sb{k}", sb) for k, sb in enumerate(getattr(p, "_sbs", [p.sb]))]:
+    for name, bufs in [("cb", p.cb)] + [(f"sb{k}", sb) for k, sb in enumerate(getattr(p, "score_bufs", [p.sb]))]:
         for k, v in bufs.items():
             if k == "gran":
                 continue
