@@ -134,7 +134,9 @@ typedef struct ou_conv_desc {
                                /* larger staged value sets range code 1 in       */
                                /* *status, a larger split-image value (sy) 2, an */
                                /* infinite one 4; the engine then widens that    */
-                               /* layer's exponent (default 6)                   */
+                               /* layer's exponent (default 6).  Bits 8 / 9 / 10 */
+                               /* (with 1 / 2, ou_block's codes too): a finite   */
+                               /* staged value reached 2^23 / 2^31 / 2^39        */
 } ou_conv_desc;
 
 /* Default channel chunk of the kernel for a tap count (informational: the

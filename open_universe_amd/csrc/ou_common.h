@@ -129,11 +129,17 @@ __device__ __forceinline__ void ou_kernarg_prefetch8()
 // value reached 2^15 (this operand's exponent is too small: the host widens
 // it) and bit 4 when a value was infinite (an overflow upstream propagating).
 #define OU_RANGE_FINITE_MAX 3.4028235e38f
+// Bits 8-10 say how far: set when a finite value reached 2^23 / 2^31 / 2^39,
+// i.e. the exponent needs 2 / 3 / 4 steps of 8 (a thermometer code, so the
+// OR over waves keeps the largest).
 __device__ __forceinline__ void ou_range_flag(int* status, float omax, int big, int lane)
 {
     if (__any(omax >= 32768.f) && status) {
-        const int code = (__any(omax >= 32768.f && omax <= OU_RANGE_FINITE_MAX) ? big : 0) |
-                         (__any(omax > OU_RANGE_FINITE_MAX) ? 4 : 0);
+        const bool fin = omax >= 32768.f && omax <= OU_RANGE_FINITE_MAX;
+        const int code = (__any(fin) ? big : 0) | (__any(omax > OU_RANGE_FINITE_MAX) ? 4 : 0) |
+                         (__any(fin && omax >= 8388608.f) ? 256 : 0) |          // 2^23
+                         (__any(fin && omax >= 2147483648.f) ? 512 : 0) |       // 2^31
+                         (__any(fin && omax >= 549755813888.f) ? 1024 : 0);     // 2^39
         if (lane == 0) atomicOr(status, code);
     }
 }

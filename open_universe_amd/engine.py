@@ -1118,7 +1118,9 @@ class Engine:
         split-f16 range by 2^step -- the conv's own input (code 1), a fused
         block's conv1 / conv2 / conv3 / down input (1 / 2 / 8 / 16), the
         operand of the op a conv (2) or block (32) stores a split image for.  Codes 4 alone (an
-        infinite value: an overflow upstream) widen nothing.  Returns the
+        infinite value: an overflow upstream) widen nothing.  Bits 8-10 (a
+        thermometer of how far the values went: 2^23 / 2^31 / 2^39) widen by
+        2 / 3 / 4 steps at once, so one rerun fixes what one replay saw.  Returns the
         number of exponents widened; 0 (nothing to widen, or an exponent past
         MAX_SHIFT) means the caller falls back to f32 operands.  Plans must
         be recorded again: the exponents are read at record time."""
@@ -1127,6 +1129,7 @@ class Engine:
             if slot < 0 or slot >= len(self.range_owners):
                 return 0
             own = self.range_owners[slot]
+            w = step * (1 + bin((code >> 8) & 7).count("1"))
             targets = []
             if isinstance(own, FusedW):
                 targets = [("f", own, i) for i, bit in enumerate((1, 2, 8, 16)) if code & bit]
@@ -1139,11 +1142,11 @@ class Engine:
                 targets.append(cons)
             for kind, o, i in targets:
                 if kind == "f":
-                    o.shifts[i] += step
+                    o.shifts[i] += w
                     if o.shifts[i] > MAX_SHIFT:
                         return 0
                 else:
-                    o.xshift += step
+                    o.xshift += w
                     if o.xshift > MAX_SHIFT:
                         return 0
                 n += 1
