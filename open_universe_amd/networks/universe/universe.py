@@ -415,8 +415,15 @@ class Universe(nn.Module):
         again -- until a replay is clean.  An error that names no layer, an
         exponent past its limit, or ``rounds`` failed reruns switch the model
         to f32 operands instead (one counted fallback)."""
+        log = os.environ.get("OUHIP_RANGE_LOG") == "1"   # diagnostics: each round's per-layer codes
         for _ in range(rounds):
             eng = self._engine
+            if log:
+                import sys
+
+                print(f"[ou range] round {self.range_widenings + 1}: "
+                      + " ".join(f"{type(eng.range_owners[s]).__name__}#{s}:{c:#x}" for s, c in err.flags),
+                      file=sys.stderr, flush=True)
             if eng is None or not getattr(err, "flags", ()) or not eng.widen_ranges(err.flags):
                 break
             self.range_widenings += 1
