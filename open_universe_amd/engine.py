@@ -74,6 +74,7 @@ def set_lane(prog, i):
 
 
 SUB_LANE = 3   # the second score sub-batch's lane (plan.EnhancePlan)
+SC_LANE = 2    # the conditions' signal_cond_proj convs (after the mel front end on the same lane)
 
 
 def score_sub_batches(B):

@@ -215,9 +215,15 @@ class EnhancePlan(_PlanBase):
             self.SC = eng.alloc_sc(B, Tp)
 
             def after_level(l, cond):
+                # the projection runs on its own lane (E.SC_LANE), so the
+                # conditioner's next decoder level does not queue behind it
+                ev = p.signal()
+                E.set_lane(p, E.SC_LANE)
+                p.wait(ev)
                 p.label = f"cond sc{l}"
                 p.add(L.OP_CONV, E.conv_desc(eng.s_sc[l], cond, self.SC[l]))
                 ev_cond[l] = p.signal()
+                E.set_lane(p, 1)
         conds, yaux = eng.rec_cond(p, cb, self.XN, need_aux=use_aux_signal or warm_start is not None,
                                    after_level=after_level, st_lane=0 if (self.overlap and st_lane) else None)
         if use_aux_signal or warm_start is not None:
@@ -227,6 +233,7 @@ class EnhancePlan(_PlanBase):
                 eng.rec_aux(p, yaux, self.AUXT, self.SIG.ptr, B, Tp)
             else:
                 raise NotImplementedError("aux signal without a signal-decoupling layer")
+        ev_c1 = p.signal() if self.overlap else None   # lane 1's last signal: lane 0 joins it before finish
         if use_aux_signal:
             x_final = self.SIG
         else:
@@ -336,6 +343,8 @@ class EnhancePlan(_PlanBase):
                 # before its next node adds an edge to that node, and a capture
                 # whose node took 9 crashed in the HIP runtime)
                 p.wait(max(ev_cond.values()))
+        if ev_c1 is not None:
+            p.wait(ev_c1)   # long done: the conditions were waited on in the first step
         p.label = "finish"
         p.add(L.OP_FINISH, L.FinishArgs(x=x_final.ptr, x_bstride=Tp, left=self.pad // 2,
                                         batch=B, len=mix_len, y=self.OUT.data_ptr(),
