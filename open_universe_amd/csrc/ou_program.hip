@@ -59,30 +59,9 @@ int shared_stream(hipStream_t* slot, hipStream_t* out)
     return 0;
 }
 
-// Side lanes given the device's highest stream priority (OUHIP_LANE_PRIO,
-// a digit string of side-lane ids, default "12": the conditioner lane and the
-// mel front end's).  The first diffusion step waits on the conditioner, the
-// score lane beside it has slack: the dispatcher serves the conditioner's
-// workgroups first.  Captured graphs carry the priority per node
-// (hipGraphInstantiateFlagUseNodePriority).
-bool lane_prio(int lane)
-{
-    static const char* env = getenv("OUHIP_LANE_PRIO");
-    const char* v = env ? env : "12";
-    for (; *v; ++v)
-        if (*v - '0' == lane) return true;
-    return false;
-}
-
 int side_stream(int dev, int lane, hipStream_t* out)
 {
-    hipStream_t* slot = &g_side[dev][lane - 1];
-    if (!*slot && lane_prio(lane)) {
-        int least = 0, greatest = 0;
-        OU_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priority range");
-        OU_HIP_CHECK(hipStreamCreateWithPriority(slot, hipStreamNonBlocking, greatest), "program stream");
-    }
-    return shared_stream(slot, out);
+    return shared_stream(&g_side[dev][lane - 1], out);
 }
 
 int current_device(int* dev)
@@ -405,7 +384,7 @@ int ou_program_capture(ou_program* p)
     }
     if (e != hipSuccess) return ou_fail(-100, "end capture: %s", hipGetErrorString(e));
     p->graph = g;
-    e = hipGraphInstantiateWithFlags(&p->exec, g, hipGraphInstantiateFlagUseNodePriority);
+    e = hipGraphInstantiate(&p->exec, g, nullptr, nullptr, 0);
     if (e != hipSuccess) {
         drop_graph(p);
         return ou_fail(-100, "graph instantiate: %s", hipGetErrorString(e));

@@ -165,6 +165,29 @@ def _split_producer(op, p):
     return (p.y, p.y_bstride, p.y_cstride, p.length, p.channels, p.batch)
 
 
+SPLIT_STORE_BPMS = 4e9   # bytes per ms a producer's epilogue adds for its image (~4 TB/s)
+
+
+def _split_pays(d, buf, per_item, rows, shift, batch):
+    """A conv consumer takes the split image only where the split-image
+    kernel's best tile, plus the producer's extra image store, beats its best
+    plain tile (both timed by the tuner; without one, always)."""
+    tuner = L.TUNER
+    if not hasattr(tuner, "timed"):
+        return True
+    plain = L.ConvDesc.from_buffer_copy(d)
+    plain.tile = -1
+    _, ms_p = tuner.timed(plain)
+    trial = L.ConvDesc.from_buffer_copy(d)
+    trial.xs, trial.xs_bstride, trial.xs_rows, trial.xs_shift = buf.data_ptr(), per_item, rows, shift
+    trial.w, trial.w_unscale = d._w_nat
+    trial.tile = -1
+    _, ms_s = tuner.timed(trial)
+    if ms_p is None or ms_s is None:
+        return True
+    return ms_s + batch * per_item / SPLIT_STORE_BPMS < ms_p
+
+
 def split_hook(prog, op, d):
     """Program.add hook (split-f16 plans): link op ``d`` (a conv, or a fused
     block's conv1) to the split image of the lane's previous op when that op
@@ -187,7 +210,11 @@ def split_hook(prog, op, d):
     cache = prog.__dict__.setdefault("split_bufs", {})
     buf = cache.get(key)
     if buf is None:
-        buf = cache[key] = empty((batch * per_item // 2,), dtype=torch.int16, device=_REC_DEVICE)
+        buf = empty((batch * per_item // 2,), dtype=torch.int16, device=_REC_DEVICE)
+    if op == L.OP_CONV and not _split_pays(d, buf, per_item, rows, shift, batch):
+        return
+    if key not in cache:
+        cache[key] = buf
         prog.keep.append(buf)
     prog.__dict__.setdefault("split_links", []).append((idx, len(prog.flops)))
     if p.status and owner[1] is not None:
@@ -897,6 +924,7 @@ class ConvTuner:
         import os
 
         self.cache = {}
+        self.times = {}   # key -> the chosen tile's ms per launch (split_hook weighs a split-image link by it)
         self.reps = reps
         self.graph = os.environ.get("OUHIP_TUNE_GRAPH", "1") != "0"   # time candidates inside a hipGraph
         if self.graph:
@@ -906,7 +934,10 @@ class ConvTuner:
         self.by_geom = {}   # geometry -> frame-count buckets cached
         if path and os.path.exists(path):
             with open(path) as fh:
-                self.cache = {tuple(json.loads(k)): v for k, v in json.load(fh).items()}
+                raw = json.load(fh)
+            times = raw.pop("__ms__", {})
+            self.cache = {tuple(json.loads(k)): v for k, v in raw.items()}
+            self.times = {tuple(json.loads(k)): v for k, v in times.items()}
         # persisted geometries seed the nearest-length reuse too
         for kk in self.cache:
             self.by_geom.setdefault(kk[:-1], set()).add(kk[-1])
@@ -915,8 +946,10 @@ class ConvTuner:
         import json
 
         if self.path:
+            out = {json.dumps(list(k)): v for k, v in self.cache.items()}
+            out["__ms__"] = {json.dumps(list(k)): v for k, v in self.times.items()}
             with open(self.path, "w") as fh:
-                json.dump({json.dumps(list(k)): v for k, v in self.cache.items()}, fh)
+                json.dump(out, fh)
 
     @staticmethod
     def bucket(n):
@@ -960,6 +993,8 @@ class ConvTuner:
         if near and os.environ.get("OUHIP_TUNE_EVERY_LENGTH", "0") != "1":
             bb = min(near, key=lambda x: (abs(x - b), x))
             self.cache[k] = self.cache[g + (bb,)]
+            if g + (bb,) in self.times:   # another length's time: a rough figure, scaled by the frames
+                self.times[k] = self.times[g + (bb,)] * 2.0 ** (b - bb)
             near.add(b)
             return self.fit_workspace(d, self.cache[k])
         lib = L.load()
@@ -1043,6 +1078,7 @@ class ConvTuner:
         d.status = status
         L.ADD_HOOK = hook
         self.cache[k] = best
+        self.times[k] = best_ms
         self.by_geom.setdefault(k[:-1], set()).add(k[-1])
         if os.environ.get("OUHIP_TUNE_VERBOSE", "1") != "0":   # progress (long plan builds)
             import sys
@@ -1052,6 +1088,12 @@ class ConvTuner:
                   file=sys.stderr, flush=True)
         self._save()
         return best
+
+
+    def timed(self, d):
+        """(tile, ms per launch or None) for a descriptor, tuning it if new."""
+        tile = self(d)
+        return tile, self.times.get(self.key(d))
 
 
 _TUNER = None
