@@ -174,7 +174,10 @@ def test_full_width_pp24_enhance():
         out = m.enhance(mix[:, 0], rng=torch.Generator().manual_seed(1028282)).cpu()
     eng = m._get_engine()
     assert eng.conv_prec == 1 and m.range_fallbacks == 0   # still split-f16
-    assert 1 <= m.range_widenings <= 2                      # reported (bench.py "widenings")
+    # reported (bench.py "widenings").  One replay names only the first
+    # layers to overflow: their inf / NaN hides the layers behind them, which
+    # the next rerun names (OUHIP_RANGE_LOG=1: 2 + 7 + 4 layers over 3 reruns)
+    assert 1 <= m.range_widenings <= 3
     wide = [o for o in eng.range_owners if (getattr(o, "xshift", 6) != 6 or any(x != 6 for x in
                                                                                   getattr(o, "shifts", [6])))]
     assert 0 < len(wide) < len(eng.range_owners) // 2       # only the flagged layers moved
