@@ -173,16 +173,16 @@ def _split_pays(d, buf, per_item, rows, shift, batch):
     kernel's best tile, plus the producer's extra image store, beats its best
     plain tile (both timed by the tuner; without one, always)."""
     tuner = L.TUNER
-    if not hasattr(tuner, "timed"):
+    if not hasattr(tuner, "pick"):
         return True
     plain = L.ConvDesc.from_buffer_copy(d)
     plain.tile = -1
-    _, ms_p = tuner.timed(plain)
+    _, ms_p = tuner.pick(plain)
     trial = L.ConvDesc.from_buffer_copy(d)
     trial.xs, trial.xs_bstride, trial.xs_rows, trial.xs_shift = buf.data_ptr(), per_item, rows, shift
     trial.w, trial.w_unscale = d._w_nat
     trial.tile = -1
-    _, ms_s = tuner.timed(trial)
+    _, ms_s = tuner.pick(trial)
     if ms_p is None or ms_s is None:
         return True
     return ms_s + batch * per_item / SPLIT_STORE_BPMS < ms_p
@@ -1090,7 +1090,7 @@ class ConvTuner:
         return best
 
 
-    def timed(self, d):
+    def pick(self, d):
         """(tile, ms per launch or None) for a descriptor, tuning it if new."""
         tile = self(d)
         return tile, self.times.get(self.key(d))
