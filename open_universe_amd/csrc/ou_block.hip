@@ -341,6 +341,8 @@ constexpr int block_f()
 }
 
 typedef float float2_t __attribute__((ext_vector_type(2)));
+// per-element fma on a pair: one v_pk_fma_f32, the same bits as two fmaf
+__device__ __forceinline__ float2_t fma2(float2_t a, float2_t b, float2_t c) { return __builtin_elementwise_fma(a, b, c); }
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 
 // x (already scaled by the stage's 2^-shift) -> hi (+ lo) halves of 4
@@ -574,6 +576,11 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
     // real row (the value is never stored), stores skip them
     constexpr bool PADM = C % 32 != 0;
     auto rowc = [&](int mr, int r) { return PADM ? min(row(mr, r), C - 1) : row(mr, r); };
+    // row(mr, r) - 4 h: wave-uniform, so an f32 plane [C][cs] is read and
+    // written through a buffer resource with the row in the scalar soffset and
+    // the lane's frame (plus its half's 4 rows) in the voffset -- no per-element
+    // 64-bit address arithmetic (channel counts without padded rows)
+    auto rbase = [&](int mr, int r) { return (wm * MR + mr) * 32 + (r & 3) + 8 * (r >> 2); };
     auto rok = [&](int mr, int r) { return !PADM || row(mr, r) < C; };
     auto gok = [&](int mr, int j) { return !PADM || (wm * MR + mr) * 32 + 8 * j + 4 * h < C; };
     // a stage output: channels c0 .. c0 + 3 (c0 % 4 == 0) of one LDS row, as
@@ -621,7 +628,14 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
 #pragma unroll
                     for (int nr = 0; nr < NR; ++nr) {   // frames outside [0, T) are zeroed below
                         const int t = min(max(t0 - 2 - OFF + (wn * NR + nr) * 32 + l32, 0), T - 1);
-                        scv[mr][nr][r] = d.sc[(int64_t)b * d.sc_bstride + (int64_t)m * d.sc_cstride + t];
+                        if constexpr (PADM) {
+                            scv[mr][nr][r] = d.sc[(int64_t)b * d.sc_bstride + (int64_t)m * d.sc_cstride + t];
+                        } else {
+                            const int cs4 = (int)d.sc_cstride * 4;
+                            scv[mr][nr][r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                ou_rsrc(d.sc + (int64_t)b * d.sc_bstride, (int64_t)C * cs4), t * 4 + 4 * h * cs4,
+                                rbase(mr, r) * cs4, 0));
+                        }
                     }
                 }
             }
@@ -635,19 +649,32 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                 const bool inside = t >= 0 && t < T;
                 float o[16];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    float v = __builtin_fmaf(__builtin_fmaf(accx[mr][nr][r], 1.f / 2048.f, acc[mr][nr][r]), un,
-                                             bia[mr][r]);
-                    if constexpr (EPI & kEpiSc) v = (v + scv[mr][nr][r]) * d.s_sc;
-                    if constexpr (EPI & kEpiFilm) v = __builtin_fmaf(gam[mr][r], v, bet[mr][r]);
-                    o[r] = inside ? v : 0.f;
+                for (int r = 0; r < 16; r += 2) {   // pairs: packed fma / add / mul, bit-identical to scalar
+                    float2_t v = fma2(fma2(float2_t{accx[mr][nr][r], accx[mr][nr][r + 1]}, 1.f / 2048.f,
+                                           float2_t{acc[mr][nr][r], acc[mr][nr][r + 1]}),
+                                      un, float2_t{bia[mr][r], bia[mr][r + 1]});
+                    if constexpr (EPI & kEpiSc) v = (v + float2_t{scv[mr][nr][r], scv[mr][nr][r + 1]}) * d.s_sc;
+                    if constexpr (EPI & kEpiFilm)
+                        v = fma2(float2_t{gam[mr][r], gam[mr][r + 1]}, v, float2_t{bet[mr][r], bet[mr][r + 1]});
+                    o[r] = inside ? v.x : 0.f, o[r + 1] = inside ? v.y : 0.f;
                 }
                 if constexpr (EPI & kEpiCond) {
-                    if (inside && t >= t0 && t < t0 + F && t < TS) {
-                        float* co = d.cond_out + (int64_t)b * d.co_bstride + t;
+                    const bool st = inside && t >= t0 && t < t0 + F && t < TS;
+                    if constexpr (PADM) {
+                        if (st) {
+                            float* co = d.cond_out + (int64_t)b * d.co_bstride + t;
+#pragma unroll
+                            for (int r = 0; r < 16; ++r)
+                                if (rok(mr, r)) co[(int64_t)row(mr, r) * d.co_cstride] = o[r];
+                        }
+                    } else {
+                        const int cs4 = (int)d.co_cstride * 4;
+                        const __amdgpu_buffer_rsrc_t crs =
+                            ou_rsrc(d.cond_out + (int64_t)b * d.co_bstride, (int64_t)C * cs4);
+                        const int vo = st ? t * 4 + 4 * h * cs4 : kBlkSentinel;
 #pragma unroll
                         for (int r = 0; r < 16; ++r)
-                            if (rok(mr, r)) co[(int64_t)row(mr, r) * d.co_cstride] = o[r];
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o[r]), crs, vo, rbase(mr, r) * cs4, 0);
                     }
                 }
 #pragma unroll
@@ -655,9 +682,10 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                     if (!gok(mr, j)) continue;
                     float x[4];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const float q = o[4 * j + i];
-                        x[i] = (q >= 0.f ? kIn1 : a2 * kIn1) * q;
+                    for (int i = 0; i < 4; i += 2) {
+                        const float2_t q = {o[4 * j + i], o[4 * j + i + 1]};
+                        const float2_t xx = q * float2_t{q.x >= 0.f ? kIn1 : a2 * kIn1, q.y >= 0.f ? kIn1 : a2 * kIn1};
+                        x[i] = xx.x, x[i + 1] = xx.y;
                     }
                     put4(xbuf + u * SX, (wm * MR + mr) * 32 + 8 * j + 4 * h, x, K::PB, om1);
                 }
@@ -683,17 +711,19 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
             for (int nr = 0; nr < NR; ++nr) {
                 const int v_ = (wn * NR + nr) * 32 + l32;
                 const int t = t0 - 1 - OFF + v_;
-                const float keep = (t >= 0 && t < T) ? kIn2 : 0.f;
+                const float keep = (t >= 0 && t < T) ? kIn2 : 0.f, akeep = a3 * keep;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if (!gok(mr, j)) continue;
                     float x[4];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
+                    for (int i = 0; i < 4; i += 2) {   // pairs: packed fma / mul, bit-identical to the scalar chain
                         const int r = 4 * j + i;
-                        const float q = __builtin_fmaf(__builtin_fmaf(accx[mr][nr][r], 1.f / 2048.f, acc[mr][nr][r]),
-                                                       un, bia[mr][r]);
-                        x[i] = (q >= 0.f ? keep : a3 * keep) * q;
+                        const float2_t q = fma2(fma2(float2_t{accx[mr][nr][r], accx[mr][nr][r + 1]}, 1.f / 2048.f,
+                                                     float2_t{acc[mr][nr][r], acc[mr][nr][r + 1]}),
+                                                un, float2_t{bia[mr][r], bia[mr][r + 1]});
+                        const float2_t xx = q * float2_t{q.x >= 0.f ? keep : akeep, q.y >= 0.f ? keep : akeep};
+                        x[i] = xx.x, x[i + 1] = xx.y;
                     }
                     put4(xa + v_ * SX, (wm * MR + mr) * 32 + 8 * j + 4 * h, x, K::PA, om2);
                 }
@@ -724,20 +754,45 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                 // them) feed no stored output; zero, so that kEpiDown's
                 // re-split of those frames cannot trip the range flag
                 const bool hk = t >= hlo && t < hhi;
+                if constexpr (PADM) {
 #pragma unroll
-                for (int mr = 0; mr < MR; ++mr)
+                    for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const float v = hb[(int64_t)rowc(mr, r) * d.h_cstride + tc];
-                        hv[mr][nr][r] = hk ? v : 0.f;
-                    }
+                        for (int r = 0; r < 16; ++r) {
+                            const float v = hb[(int64_t)rowc(mr, r) * d.h_cstride + tc];
+                            hv[mr][nr][r] = hk ? v : 0.f;
+                        }
+                } else {   // frames outside [h0, h1) at the sentinel: they load 0
+                    const int cs4 = (int)d.h_cstride * 4;
+                    const __amdgpu_buffer_rsrc_t rs = ou_rsrc(hb, (int64_t)C * cs4);
+                    const int vo = hk ? tc * 4 + 4 * h * cs4 : kBlkSentinel;
+#pragma unroll
+                    for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            hv[mr][nr][r] =
+                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, rbase(mr, r) * cs4, 0));
+                }
             }
             if constexpr (EPI & kEpiRes2) {
+                if constexpr (PADM) {
 #pragma unroll
-                for (int mr = 0; mr < MR; ++mr)
+                    for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        rv[mr][nr][r] = d.res2[(int64_t)b * d.r2_bstride + (int64_t)rowc(mr, r) * d.r2_cstride + tc];
+                        for (int r = 0; r < 16; ++r)
+                            rv[mr][nr][r] =
+                                d.res2[(int64_t)b * d.r2_bstride + (int64_t)rowc(mr, r) * d.r2_cstride + tc];
+                } else {
+                    const int cs4 = (int)d.r2_cstride * 4;
+                    const __amdgpu_buffer_rsrc_t rs = ou_rsrc(d.res2 + (int64_t)b * d.r2_bstride, (int64_t)C * cs4);
+                    const int vo = tc * 4 + 4 * h * cs4;
+#pragma unroll
+                    for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            rv[mr][nr][r] =
+                                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, rbase(mr, r) * cs4, 0));
+                }
             }
         }
     };
@@ -806,6 +861,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                 ou_rsrc(d.sy ? (const char*)d.sy + (int64_t)b * d.sy_bstride : (const char*)yb,
                         d.sy ? (int64_t)(C / 32) * d.sy_rows * 128 : 0);
             const float sscale = ou_exp2i(-d.sy_shift);
+            const __amdgpu_buffer_rsrc_t yrs = ou_rsrc(yb, (int64_t)C * d.y_cstride * 4);
             // kEpiDown: PReLU_down(y) 2^-6 also goes to region A (split), rows
             // w <-> frames t0 - OFF + w, zero outside [0, T) and past the rows
             // the strided conv reads
@@ -819,14 +875,25 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                     const int t = t0 - OFF + w;
                     const bool own = w >= OFF && w < OFF + F && t < TS && !((d.dbg & 4) && !(d.dbg & 1024));
                     float vv[16];
+                    const int ycs4 = (int)d.y_cstride * 4;
+                    const int yvo = own ? t * 4 + 4 * h * ycs4 : kBlkSentinel;
+#pragma unroll
+                    for (int r = 0; r < 16; r += 2) {   // pairs: packed arithmetic, bit-identical to scalar
+                        float2_t v2 = fma2(fma2(float2_t{accx[mr][nr][r], accx[mr][nr][r + 1]}, 1.f / 2048.f,
+                                                float2_t{acc[mr][nr][r], acc[mr][nr][r + 1]}),
+                                           un, float2_t{bia[mr][r], bia[mr][r + 1]});
+                        v2 = (v2 + float2_t{hv[mr][nr][r], hv[mr][nr][r + 1]}) * d.s_res;
+                        if constexpr (EPI & kEpiRes2) v2 = (v2 + float2_t{rv[mr][nr][r], rv[mr][nr][r + 1]}) * d.s2;
+                        vv[r] = v2.x, vv[r + 1] = v2.y;
+                    }
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
-                        float v = __builtin_fmaf(__builtin_fmaf(accx[mr][nr][r], 1.f / 2048.f, acc[mr][nr][r]), un,
-                                                 bia[mr][r]);
-                        v = (v + hv[mr][nr][r]) * d.s_res;
-                        if constexpr (EPI & kEpiRes2) v = (v + rv[mr][nr][r]) * d.s2;
-                        vv[r] = v;
-                        if (own && rok(mr, r)) yb[(int64_t)row(mr, r) * d.y_cstride + t] = v;
+                        const float v = vv[r];
+                        if constexpr (PADM) {
+                            if (own && rok(mr, r)) yb[(int64_t)row(mr, r) * d.y_cstride + t] = v;
+                        } else {
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), yrs, yvo, rbase(mr, r) * ycs4, 0);
+                        }
                     }
                     if (P == 1 && d.sy) {   // the next conv's split image (host-checked: C % 32 == 0)
 #pragma unroll
