@@ -217,13 +217,18 @@ class EnhancePlan(_PlanBase):
             def after_level(l, cond):
                 # the projection runs on its own lane (E.SC_LANE), so the
                 # conditioner's next decoder level does not queue behind it
-                ev = p.signal()
-                E.set_lane(p, E.SC_LANE)
-                p.wait(ev)
+                # (not in a chunked plan, whose conv chunks use that lane:
+                # the HIP runtime's capture crashed on the extra side-lane
+                # edges)
+                if chunks is None:
+                    ev = p.signal()
+                    E.set_lane(p, E.SC_LANE)
+                    p.wait(ev)
                 p.label = f"cond sc{l}"
                 p.add(L.OP_CONV, E.conv_desc(eng.s_sc[l], cond, self.SC[l]))
                 ev_cond[l] = p.signal()
-                E.set_lane(p, 1)
+                if chunks is None:
+                    E.set_lane(p, 1)
         conds, yaux = eng.rec_cond(p, cb, self.XN, need_aux=use_aux_signal or warm_start is not None,
                                    after_level=after_level, st_lane=0 if (self.overlap and st_lane) else None)
         if use_aux_signal or warm_start is not None:
@@ -233,7 +238,8 @@ class EnhancePlan(_PlanBase):
                 eng.rec_aux(p, yaux, self.AUXT, self.SIG.ptr, B, Tp)
             else:
                 raise NotImplementedError("aux signal without a signal-decoupling layer")
-        ev_c1 = p.signal() if self.overlap else None   # lane 1's last signal: lane 0 joins it before finish
+        # lane 1's last signal (the sc lane took the conditions'): lane 0 joins it before finish
+        ev_c1 = p.signal() if self.overlap and chunks is None else None
         if use_aux_signal:
             x_final = self.SIG
         else:
