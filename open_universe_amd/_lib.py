@@ -435,6 +435,7 @@ TUNER = None
 
 
 ADD_HOOK = None   # engine.split_hook while a plan records: links an op to its producer's split image
+                 # (ADD_HOOK.note(prog, index, op, desc) then sees every op added)
 SS_BIT = 1 << 15  # ConvDesc.tile bit: the split-image kernel (conv_skernel), bits 0-7 = NR - 1
 
 
@@ -453,7 +454,6 @@ class Program:
         self.lanes = []         # lane of each op
         self.label = ""         # phase label recorded with each op (engine sets it; reports only)
         self.labels = []
-        self.prev_op = {}       # lane -> (op index, op, desc): the lane's last op, when a conv or block
         self.descs = []         # each op's descriptor (patched in place by the split-image hook; hazards.py)
 
     def add(self, op, desc):
@@ -468,10 +468,8 @@ class Program:
             desc.tile |= MAJ_BIT
         check(self.lib.ou_program_add(self.h, op, ctypes.byref(desc), ctypes.sizeof(desc)),
               f"program_add(op={op})")
-        if op in (OP_CONV, OP_BLOCK):
-            self.prev_op[self.cur_lane] = (len(self.flops), op, desc)
-        elif op not in (OP_LANE, OP_SIGNAL):   # a wait may hand over data another lane wrote
-            self.prev_op.pop(self.cur_lane, None)
+        if ADD_HOOK is not None and hasattr(ADD_HOOK, "note"):
+            ADD_HOOK.note(self, len(self.flops), op, desc)   # the split-image producers' bookkeeping
         self.descs.append(desc)
         self.flops.append(float(getattr(desc, "_flops", 0.0)))
         self.bytes.append(float(getattr(desc, "_bytes", 0.0)))

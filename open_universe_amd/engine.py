@@ -121,6 +121,7 @@ def begin_record(prec, device=None):
     L.ADD_HOOK = split_hook if prec == 1 and split_images_enabled() else None
 
 
+
 def end_record():
     global _REC
     _REC = None
@@ -142,7 +143,7 @@ def _split_consumer(op, d):
     op that can read its operand from a split image, or None."""
     if op == L.OP_CONV:
         wn = getattr(d, "_w_nat", None)
-        if (wn is None or d.prec != 1 or d.xs or d.in_scale or d.f0 or d.cin % 32
+        if (wn is None or getattr(d, "_no_split", False) or d.prec != 1 or d.xs or d.in_scale or d.f0 or d.cin % 32
                 or getattr(d, "_full", None) is not None):
             return None
         return (d.x, d.x_bstride, d.x_cstride, d.in_len, d.cin, d.slope, d.xs_shift, ("c", getattr(d, "_cw", None), 0))
@@ -188,15 +189,36 @@ def _split_pays(d, buf, per_item, rows, shift, batch):
     return ms_s + batch * per_item / SPLIT_STORE_BPMS < ms_p
 
 
+def _split_note(prog, idx, op, d):
+    """Every op added while a split-f16 plan records: forget the producers
+    whose output it overwrites, then record it if it is a producer (a conv or
+    fused block whose epilogue can store a split image)."""
+    from .hazards import footprint, overlap
+
+    writers = prog.__dict__.setdefault("split_writers", {})
+    if op in (L.OP_LANE, L.OP_SIGNAL, L.OP_WAIT):
+        return
+    W = footprint(op, d)[1]
+    for k in [k for k, (_, _, _, box) in writers.items() if any(overlap(w, box) for w in W)]:
+        del writers[k]
+    if op in (L.OP_CONV, L.OP_BLOCK) and _split_producer(op, d) is not None:
+        y = [w for w in W if w.base == d.y]
+        if y:
+            writers[d.y] = (idx, op, d, y[0])
+
+
 def split_hook(prog, op, d):
     """Program.add hook (split-f16 plans): link op ``d`` (a conv, or a fused
-    block's conv1) to the split image of the lane's previous op when that op
-    -- a conv or a fused block -- produced d's input."""
+    block's conv1) to the split image of the op that last wrote d's input,
+    when that op is a conv or a fused block (any lane: d reads that output,
+    so the program already orders d after it).  The pairing follows the data,
+    not the lanes, so plans that place unrelated ops differently (enhance and
+    enhance_many's) link the same pairs and compute the same bits."""
     cons = _split_consumer(op, d)
-    pv = prog.prev_op.get(prog.cur_lane)
+    pv = prog.__dict__.get("split_writers", {}).get(d.x if op == L.OP_CONV else d.h)
     if cons is None or pv is None:
         return
-    idx, pop, p = pv
+    idx, pop, p, _ = pv
     prod = _split_producer(pop, p)
     x, xb, xc, in_len, C, slope, shift, owner = cons
     if (p is d or prod is None or prod[0] != x or prod[1] != xb or prod[2] != xc or prod[3] < in_len
@@ -204,9 +226,9 @@ def split_hook(prog, op, d):
         return
     rows, batch = prod[3], prod[5]
     per_item = (C // 32) * rows * 128
-    # one image per (activation buffer, lane): every step of the score loop
-    # rewrites the same activations in order on one lane, so their images too
-    key = (x, xb, xc, rows, C, batch, prog.cur_lane)
+    # one image per activation buffer: every step of the score loop rewrites
+    # the same activations in the same order, so their images too
+    key = (x, xb, xc, rows, C, batch)
     cache = prog.__dict__.setdefault("split_bufs", {})
     buf = cache.get(key)
     if buf is None:
@@ -227,6 +249,9 @@ def split_hook(prog, op, d):
         d.w, d.w_unscale = d._w_nat
         if d.tile >= 0 and not d.tile & L.SS_BIT:
             d.tile = -1
+
+
+split_hook.note = _split_note
 
 
 # ---------------------------------------------------------------------------
@@ -1797,8 +1822,13 @@ class Engine:
                         if ev_mel is not None and (res_a is bufs["XMEL"] or res_b is not None):
                             prog.wait(ev_mel)
                     prog.label = f"cond st{i}"
-                    prog.add(L.OP_CONV, conv_desc(self.c_st[i], bufs[f"V{i}"], bufs["SUM"],
-                                                  n_frames=U, res1=res_a, s1=1.0, res2=res_b, s2=1.0))
+                    dst = conv_desc(self.c_st[i], bufs[f"V{i}"], bufs["SUM"], n_frames=U, res1=res_a, s1=1.0,
+                                    res2=res_b, s2=1.0)
+                    # never a split-image consumer: where it is recorded (in
+                    # line, or on lane 0 behind a wait) must not change its
+                    # bits -- enhance_many's plans keep it in line
+                    dst._no_split = True
+                    prog.add(L.OP_CONV, dst)
                     prog.label = f"cond enc L{i}"
                     if st_lane is not None:
                         set_lane(prog, side)

@@ -97,10 +97,13 @@ def test_lane_schedules_validate(monkeypatch, env, rates):
 
 
 def test_split_images_link_the_deep_level_convs():
-    """Full-width PP16 (256 / 512-channel levels): every conv whose input the
-    conv just before it on the same lane produced reads that producer's split
-    image (ou_conv_desc.xs), the producer's descriptor is patched to store it
-    (sy), and one image per activation buffer serves all diffusion steps."""
+    """Full-width PP16 (256 / 512-channel levels): every conv whose input a
+    conv or fused block wrote last reads that producer's split image
+    (ou_conv_desc.xs; on any lane: the program orders the consumer after its
+    producer), the producer's descriptor is patched to store it (sy), and one
+    image per activation buffer serves all diffusion steps."""
+    from open_universe_amd.hazards import happens_before
+
     d = load_golden("pp16")
     eng = Engine(get_config("pp16"), golden_state_dict(d), "cpu", _record_only=True)
     plan = EnhancePlan(eng, 1, 16000, 8, 1.3)
@@ -108,8 +111,10 @@ def test_split_images_link_the_deep_level_convs():
     steps = len(links) // 8
     assert steps >= 12, len(links)            # per score step: the 256 / 512-channel chains
     assert len(plan.prog.split_bufs) <= 40    # images shared across the steps
+    hb = happens_before(plan.prog)
     for prod, cons in links:
-        assert plan.prog.lanes[prod] == plan.prog.lanes[cons] and prod < cons
+        lane, k, _ = hb[prod]
+        assert prod < cons and hb[cons][2].get(lane, 0) >= k   # the consumer runs after its producer
 
 
 def test_split_images_off_records_plain_convs(monkeypatch):
