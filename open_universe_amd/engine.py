@@ -1393,7 +1393,7 @@ class Engine:
         return [n - 1 - l for l in range(n)]
 
     def rec_score(self, prog, bufs, x: Act, film_base, film_bs, in_scale=0, sc_list=None, before_level=None,
-                  head=None, after_encoder=None):
+                  head=None, after_encoder=None, gru_xcd=0):
         """ScoreNetwork.forward (score.py:278-298).  The encoder and the
         bottleneck GRU do not read the conditions (score.py:284-286), and
         decoder level l reads only condition l: ``before_level(l)`` runs right
@@ -1402,7 +1402,9 @@ class Engine:
         otherwise the decoder output Act is returned.  When the 32-channel end
         blocks are fused, the input conv runs inside the first encoder block and
         the head inside the last decoder block (ou_block kEpiIn / kEpiHead).
-        ``after_encoder()`` runs between the encoder and the bottleneck GRU."""
+        ``after_encoder()`` runs between the encoder and the bottleneck GRU;
+        ``gru_xcd`` rotates the GRU chains' XCDs (ou_gru_desc.flags bits 12-14:
+        the same bits, other L2s than a GRU running beside it)."""
         n_lvl = len(self.s_enc)
         nr = len(self.rates)
         fb = lambda j: film_base + 4 * self.film_off[j]
@@ -1427,7 +1429,7 @@ class Engine:
         top = n_lvl - 1
         prog.label = "score gru"
         rec_gru(prog, self.s_gru, 0, bufs[f"V{top}"], bufs["GI"], bufs[f"V{top}"],
-                bufs["gran"], self.status, res=bufs[f"V{top}"], res_scale=NF2)
+                bufs["gran"], self.status, res=bufs[f"V{top}"], res_scale=NF2, xcd=gru_xcd)
         # decoder (score.py:197-211)
         h = None
         for l in range(n_lvl):

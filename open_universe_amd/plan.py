@@ -331,7 +331,7 @@ class EnhancePlan(_PlanBase):
                         elif not whole and n == steps[0]:
                             after = lambda: ev_sub.append(p.signal())
                         eng.rec_score(p, sbs[k], xk, film, 0, in_scale=in_scale, sc_list=sc, before_level=join,
-                                      head=head, after_encoder=after)
+                                      head=head, after_encoder=after, gru_xcd=4 * k)
                         if k == 1:
                             E.set_lane(p, 0)
                     zi += 0 if last else 1
