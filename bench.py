@@ -485,7 +485,8 @@ def main():
             if args.traffic_json and os.path.exists(args.traffic_json):
                 with open(args.traffic_json) as fh:
                     pmc = json.load(fh)
-                rows = [r for k, r in pmc.get("kernels", {}).items() if k in ("conv_kernel", "conv_rkernel", "block_kernel")]
+                rows = [r for k, r in pmc.get("kernels", {}).items()
+                        if k in ("conv_kernel", "conv_rkernel", "conv_skernel", "conv_rreduce", "block_kernel")]
                 lib_now = lib_sha16()
                 if pmc.get("lib_sha16") != lib_now:
                     # counters of another build of the kernels: not quoted
@@ -516,8 +517,8 @@ def main():
             out["roofline"] = {
                 **rl, "traffic": traffic,
                 "traffic_source": tsrc,
-                "kernel": "conv stack: ou_conv (conv_kernel, conv_rkernel) + fused ConvBlock ou_block (block_kernel), "
-                          "all launches of one enhance",
+                "kernel": "conv stack: ou_conv (conv_kernel, conv_rkernel + conv_rreduce, conv_skernel) + fused "
+                          "ConvBlock ou_block (block_kernel), all launches of one enhance",
                 "launches": prof["n_conv"],
                 "fused_block_launches": prof["n_block"],
                 "avg_launch_ms": round(prof["conv_ms"] / prof["n_conv"], 5),
