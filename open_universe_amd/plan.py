@@ -214,20 +214,23 @@ class EnhancePlan(_PlanBase):
             p.wait(ev_in)
             self.SC = eng.alloc_sc(B, Tp)
 
+            # the projections run on their own lane (E.SC_LANE), so the
+            # conditioner's next decoder level does not queue behind them --
+            # not in a chunked plan, whose conv chunks use that lane (the HIP
+            # runtime's capture crashed on the extra side-lane edges), nor in
+            # enhance_many's (st_lane=False): the side-lane streams are
+            # process-wide, and two plans in flight would serialise on it
+            sc_lane = chunks is None and st_lane
+
             def after_level(l, cond):
-                # the projection runs on its own lane (E.SC_LANE), so the
-                # conditioner's next decoder level does not queue behind it
-                # (not in a chunked plan, whose conv chunks use that lane:
-                # the HIP runtime's capture crashed on the extra side-lane
-                # edges)
-                if chunks is None:
+                if sc_lane:
                     ev = p.signal()
                     E.set_lane(p, E.SC_LANE)
                     p.wait(ev)
                 p.label = f"cond sc{l}"
                 p.add(L.OP_CONV, E.conv_desc(eng.s_sc[l], cond, self.SC[l]))
                 ev_cond[l] = p.signal()
-                if chunks is None:
+                if sc_lane:
                     E.set_lane(p, 1)
         conds, yaux = eng.rec_cond(p, cb, self.XN, need_aux=use_aux_signal or warm_start is not None,
                                    after_level=after_level, st_lane=0 if (self.overlap and st_lane) else None)
@@ -239,7 +242,7 @@ class EnhancePlan(_PlanBase):
             else:
                 raise NotImplementedError("aux signal without a signal-decoupling layer")
         # lane 1's last signal (the sc lane took the conditions'): lane 0 joins it before finish
-        ev_c1 = p.signal() if self.overlap and chunks is None else None
+        ev_c1 = p.signal() if self.overlap and chunks is None and st_lane else None
         if use_aux_signal:
             x_final = self.SIG
         else:
