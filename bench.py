@@ -303,6 +303,9 @@ def main():
     ap.add_argument("--batch", type=int, default=None,
                     help="clips per rank, overriding the config's (c4 at 16/8/4 on one GPU = the per-rank "
                          "shard at 2/4/8 GPUs)")
+    ap.add_argument("--undamped", action="store_true",
+                    help="c4: the undamped synthetic weights (activations past the default split-f16 range; "
+                         "the warm-up widens the named layers' exponents, the line reports `widenings`)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-queued", action="store_true",
@@ -364,7 +367,8 @@ def main():
     dev = torch.device("cuda", gpu)
     if C.get("conv_prec") and "OUHIP_CONV_PREC" not in os.environ:
         os.environ["OUHIP_CONV_PREC"] = C["conv_prec"]
-    cfg, model = build_model(dev, arch=C["arch"], damped=C.get("damped", False))
+    damped = C.get("damped", False) and not args.undamped
+    cfg, model = build_model(dev, arch=C["arch"], damped=damped)
     fs = int(cfg["fs"])
     T = int(args.seconds * fs)
     n_clips = args.warmup + args.steps
@@ -391,7 +395,7 @@ def main():
     # the strictly-f32 figure: a second timed pass with f32 conv operands
     f32 = None
     if prec != 0 and not args.no_f32_pass and args.config in ("c2", "c4"):
-        _, m32 = build_model(dev, arch=C["arch"], damped=C.get("damped", False))
+        _, m32 = build_model(dev, arch=C["arch"], damped=damped)
         m32._conv_prec = 0
         with torch.no_grad():
             e32 = timed_loop(lambda i: m32.enhance(clips[i % len(clips)], rng=rng, **ekw),
@@ -449,7 +453,7 @@ def main():
             "vs_baseline": None,
             "dtype": dtype,
             "data": "synthetic (harmonic+noise clips, seeded synthetic weights%s)"
-                    % (", damped family" if C.get("damped") else ""),
+                    % (", damped family" if damped else (", undamped family" if C.get("damped") else "")),
             "config": {"workload": C["workload"],
                        "model": {"pp16": "UniverseGAN PP16 (42.85 M params)", "orig16": "Universe ORIG16 (43.0 M params)",
                                  "pp24": "UniverseGAN PP24 (107.5 M params)"}[C["arch"]],

@@ -11,6 +11,7 @@
 #   benchpmc:CFG     profile:CFG, then bench:CFG quoting `traffic` from that PMC summary
 #   shards           C4 at the per-rank batches of 2/4/8 GPUs (B = 16, 8, 4)
 #   subbatch[:B]     C4 at per-rank batch B (default 4), score sub-batches off / on, alternating
+#   c4u              C4 on the undamped synthetic weights (exponents widen in the warm-up)
 #   critical         tools/critical_path.py --config c2 (lane timeline, first step)
 #   chunk:CFG        whole pass vs chunked pass (OUHIP_CHUNK=0/1) at CFG
 #   ab:VAR=[A,]B     C2 bench with VAR=A / B / A / B (A defaults to 0; same box, alternating)
@@ -60,6 +61,9 @@ for step in "$@"; do
             OUHIP_TUNE_CACHE="$O/tune_${TAG}_c4.json" bench "$O/bench_${TAG}_c4_b$b" 300 --config c4 --batch $b \
                 --steps 4 --warmup 1 --no-f32-pass --no-cpu-baseline --traffic-json "" || exit 1
         done ;;
+    c4u)
+        OUHIP_TUNE_CACHE="$O/tune_${TAG}_c4.json" bench "$O/bench_${TAG}_config_c4_undamped" 900 --config c4 \
+            --undamped --steps 3 --warmup 2 --no-f32-pass --no-cpu-baseline || exit 1 ;;
     subbatch)
         for i in 1 2; do
             for v in 0 1; do
