@@ -394,7 +394,9 @@ def main():
     fallbacks = model.range_fallbacks   # timed-loop enhances rerun with f32 operands (OuRangeError)
     # the strictly-f32 figure: a second timed pass with f32 conv operands
     f32 = None
-    if prec != 0 and not args.no_f32_pass and args.config in ("c2", "c4"):
+    # (c2 only: at c4 the split-f16 model's arena, split images included, and
+    # an f32 model's no longer fit one GPU's 288 GB together)
+    if prec != 0 and not args.no_f32_pass and args.config == "c2":
         _, m32 = build_model(dev, arch=C["arch"], damped=damped)
         m32._conv_prec = 0
         with torch.no_grad():
