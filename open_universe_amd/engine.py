@@ -79,14 +79,14 @@ SC_LANE = 2    # the conditions' signal_cond_proj convs (after the mel front end
 
 def score_sub_batches(B):
     """[(b0, b1), ...]: the score network's batch split in two halves on two
-    lanes (EnhancePlan), or None.  At small batches the bottleneck GRU's
-    serial step chain leaves most of the chip idle; with two sub-batches one
-    half's GRU runs beside the other half's convolutions.  Default for
-    2 <= B <= 6; OUHIP_SUB_BATCH=0 / 1 forces it off / on (B >= 2)."""
+    lanes (EnhancePlan), or None.  With two sub-batches one half's GRU chain
+    runs beside the other half's convolutions.  Opt-in (OUHIP_SUB_BATCH=1,
+    B >= 2): measured at C4's per-rank batch of 4 it is slower, 522-532
+    against 549-567 audio-s/s (profiles/c4_subbatch_r05s.txt) -- the halves'
+    convolutions lose more than the overlap hides."""
     import os
 
-    v = os.environ.get("OUHIP_SUB_BATCH", "auto")
-    if B < 2 or v == "0" or (v != "1" and not 2 <= B <= 6):
+    if B < 2 or os.environ.get("OUHIP_SUB_BATCH", "0") != "1":
         return None
     h = (B + 1) // 2
     return [(0, h), (h, B)]

@@ -45,8 +45,10 @@ def test_sub_batched_enhance_bit_exact(model, B, T, monkeypatch):
     assert torch.equal(b, c)
 
 
-def test_sub_batched_model_enhance_default(model):
-    """Universe.enhance at B = 4 records the sub-batched plan by default."""
+def test_sub_batched_model_enhance(model, monkeypatch):
+    """Universe.enhance at B = 4 with OUHIP_SUB_BATCH=1 records the sub-batched plan."""
+    monkeypatch.setenv("OUHIP_SUB_BATCH", "1")
+    model._plans.clear()
     mix = 0.1 * torch.randn(4, 32000, generator=torch.Generator().manual_seed(3)).to(DEV)
     y = model.enhance(mix, rng=torch.Generator(device=DEV).manual_seed(1))
     assert y.shape == mix.shape and torch.isfinite(y).all()

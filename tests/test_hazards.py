@@ -85,8 +85,9 @@ def _check(plan):
 
 
 @pytest.mark.parametrize("tag", ["pp16_c4", "orig16_c4", "pp24_c4", "pp16"])
-@pytest.mark.parametrize("B", [1, 2, 3])
-def test_enhance_plans_are_race_free(engines, tag, B):
+@pytest.mark.parametrize("B,sub", [(1, "0"), (2, "0"), (2, "1"), (3, "1")])
+def test_enhance_plans_are_race_free(engines, tag, B, sub, monkeypatch):
+    monkeypatch.setenv("OUHIP_SUB_BATCH", sub)
     T = 16000 if tag == "pp16" else 4000
     _check(EnhancePlan(engines[tag], B, T, 8, 1.3))
 

@@ -126,12 +126,14 @@ def test_split_images_off_records_plain_convs(monkeypatch):
 
 
 @pytest.mark.parametrize("B,subs", [(1, None), (2, [(0, 1), (1, 2)]), (3, [(0, 2), (2, 3)]),
-                                    (4, [(0, 2), (2, 4)]), (8, None)])
-def test_small_batches_record_two_score_sub_batches(B, subs):
-    """2 <= B <= 6: the score network as two sub-batches, the second on its
-    own lane (engine.SUB_LANE) behind the first half's first encoder; the
+                                    (4, [(0, 2), (2, 4)]), (8, [(0, 4), (4, 8)])])
+def test_small_batches_record_two_score_sub_batches(B, subs, monkeypatch):
+    """OUHIP_SUB_BATCH=1: the score network as two sub-batches, the second on
+    its own lane (engine.SUB_LANE) behind the first half's first encoder; the
     lane schedule validates and every score op is recorded once per half."""
     from open_universe_amd import engine as E
+
+    monkeypatch.setenv("OUHIP_SUB_BATCH", "1")
 
     d = load_golden("pp16_c4")
     eng = Engine(get_config("pp16", 4), golden_state_dict(d), "cpu", _record_only=True)
@@ -151,6 +153,8 @@ def test_small_batches_record_two_score_sub_batches(B, subs):
 def test_sub_batch_switch(monkeypatch):
     from open_universe_amd import engine as E
 
+    monkeypatch.delenv("OUHIP_SUB_BATCH", raising=False)
+    assert E.score_sub_batches(4) is None   # opt-in
     monkeypatch.setenv("OUHIP_SUB_BATCH", "0")
     assert E.score_sub_batches(4) is None
     monkeypatch.setenv("OUHIP_SUB_BATCH", "1")
