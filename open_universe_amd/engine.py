@@ -186,7 +186,9 @@ def _split_pays(d, buf, per_item, rows, shift, batch):
     _, ms_s = tuner.pick(trial)
     if ms_p is None or ms_s is None:
         return True
-    return ms_s + batch * per_item / SPLIT_STORE_BPMS < ms_p
+    # the plan's batch (as the tuner's keys): sub-batched and whole plans decide alike
+    b = _TUNE_BATCH if _TUNE_BATCH is not None else batch
+    return ms_s + b * per_item / SPLIT_STORE_BPMS < ms_p
 
 
 def _split_note(prog, idx, op, d):
