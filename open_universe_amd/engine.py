@@ -99,19 +99,15 @@ def overlap_enabled():
 
 
 def split_images_enabled():
-    """OUHIP_SPLIT_IMAGES=0 keeps every conv on its own f32 staging;
-    =convs links conv consumers only (a fused block then always stages h,
-    which it reads anyway for its residual)."""
+    """OUHIP_SPLIT_IMAGES=0 keeps every conv and block on its own f32 staging.
+    (Fused blocks as consumers measured neutral at C2 against conv consumers
+    only, 731-740 vs 735-737x on one box, `ab_r05m`; they stay linked.)"""
     import os
 
-    global _SPLIT_BLOCKS
-    v = os.environ.get("OUHIP_SPLIT_IMAGES", "1")
-    _SPLIT_BLOCKS = v != "convs"
-    return v != "0"
+    return os.environ.get("OUHIP_SPLIT_IMAGES", "1") != "0"
 
 
 _REC_DEVICE = None   # the recording engine's device (split-image buffers outside an arena)
-_SPLIT_BLOCKS = True   # fused blocks may read split images (split_images_enabled)
 
 
 def begin_record(prec, device=None):
@@ -148,8 +144,7 @@ def _split_consumer(op, d):
             return None
         return (d.x, d.x_bstride, d.x_cstride, d.in_len, d.cin, d.slope, d.xs_shift, ("c", getattr(d, "_cw", None), 0))
     fw = getattr(d, "_fw", None)
-    if (fw is None or d.prec != 1 or d.xs or d.x or d.f0 or d.f1 or d.h0 or d.h1 or d.channels % 32
-            or not _SPLIT_BLOCKS):
+    if (fw is None or d.prec != 1 or d.xs or d.x or d.f0 or d.f1 or d.h0 or d.h1 or d.channels % 32):
         return None
     return (d.h, d.h_bstride, d.h_cstride, d.length, d.channels, d.slope[0], d.shift[0], ("f", fw, 0))
 
