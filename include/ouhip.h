@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define OUHIP_ABI_VERSION 6
+#define OUHIP_ABI_VERSION 7
 
 int ou_abi_version(void);
 const char* ou_last_error(void);
@@ -137,6 +137,25 @@ typedef struct ou_conv_desc {
                                /* layer's exponent (default 6).  Bits 8 / 9 / 10 */
                                /* (with 1 / 2, ou_block's codes too): a finite   */
                                /* staged value reached 2^23 / 2^31 / 2^39        */
+    /* Anti-aliased rate-change convs with the binomial FIR applied instead of
+     * folded into the weights (tile bit 17; PReLU_Conv with use_antialiasing,
+     * blocks.py:214-226, BinomialAntiAlias blocks.py:123-134):
+     *   fir 1: f = FIR(prelu(x)) ('same', zero outside [0, in_len)), then the
+     *          strided conv over f's frame view: frame = R, rout 1, K = cin R;
+     *   fir 2: the transposed conv (frame 1, rout = -R, K = cin), then the FIR
+     *          over its R * in_len output samples (zero outside), then bias.
+     * R is 2, 3, 4, 5 or 8; kt 1, pad 0, shift 0, no in_scale, no xs; prec 1
+     * or 2; weights w_logical[m'][k] packed by ou_conv_pack_split_nat(kt 1):
+     *   fir 1: m' = co (m = cout rows),
+     *          k = (cb R + ph) 16 + c  for input channel ci = 16 cb + c
+     *          (cin % 16 == 0) and conv tap ph;
+     *   fir 2: every 32-row m-tile holds P = 32 / R whole channels, row
+     *          m' = 32 (co / P) + (co % P) R + ph (rows past P R zero), so
+     *          ceil(cout / P) * 32 packed rows; k = ci (cin % 32 == 0).
+     * fir 0: the other kernels (FIR folded into the weights). */
+    int32_t fir;
+    int32_t fir_pad_;
+    const float* fir_taps;     /* [2R + 1] FIR taps (device)                     */
 } ou_conv_desc;
 
 /* Default channel chunk of the kernel for a tap count (informational: the

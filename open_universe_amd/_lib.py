@@ -12,7 +12,7 @@ from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OUHIP_LIB", os.path.join(_HERE, "libouhip.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 fp = c_void_p  # device pointers are passed as integers
 
@@ -42,6 +42,7 @@ class ConvDesc(ctypes.Structure):
         ("sy", fp), ("sy_bstride", c_int64), ("sy_rows", c_int32), ("sy_shift", c_int32),
         ("sy_slope", c_float), ("sy_pad_", c_int32),
         ("xs", fp), ("xs_bstride", c_int64), ("xs_rows", c_int32), ("xs_shift", c_int32),
+        ("fir", c_int32), ("fir_pad_", c_int32), ("fir_taps", fp),
     ]
 
 

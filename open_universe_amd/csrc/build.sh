@@ -32,6 +32,9 @@ else
   for k in 1 3 4 5; do
     cc ou_conv.hip "ou_conv_k$k.o" -DOU_CONV_SPLIT_KT=$k
   done
+  for r in 2 3 4 5 8; do   # the FIR-applied rate-change kernels, one unit per rate
+    cc ou_conv.hip "ou_conv_fir$r.o" -DOU_CONV_SPLIT_FIR=$r
+  done
 fi
 rc=0
 for p in "${pids[@]}"; do wait "$p" || rc=1; done

@@ -2391,6 +2391,443 @@ __global__ __launch_bounds__(256 + 64 * kWsLoaders) void conv_wkernel(ou_conv_de
     OU_WSTAMP_SAVE(threadIdx.x == 0, 0);
 }
 
+// ---------------------------------------------------------------------------
+// Anti-aliased rate-change convolutions with the FIR applied (tile bit 17,
+// ou_conv_desc.fir).
+//
+// PReLU_Conv with use_antialiasing runs a (2R+1)-tap binomial FIR
+// (blocks.py:66-72, 123-134) before a strided conv (down, blocks.py:214-218)
+// or after a transposed one (up, blocks.py:221-225).  Folded into the weights
+// (engine.spec_down / spec_up, the kernels above) that is a 3-frame polyphase
+// kernel: three times the reference's dense MACs.  These two kernels keep the
+// reference's factorisation -- the GEMM has one tap and K = cin R (down) or
+// cin (up) -- and run the FIR on the VALU:
+//   conv_fdkernel (down): while a K chunk (16 channels x R phases) is staged,
+//     thread (channel c, frame group g) holds F R + 2 R consecutive PReLU'd
+//     samples of its channel in registers, slides the FIR over them and
+//     writes the F R results, split into f16 hi / lo, into the B image
+//     [frame][phase][16 channels] (row stride 16 R + 8 halves: an odd number
+//     of 16-B slots, so the ds_read_b128 fragment reads are conflict-free);
+//   conv_fukernel (up): the workgroup computes the transposed conv over BN
+//     frames (one frame of halo each side: BN - 2 output frames), keeping
+//     P = 32 / R whole channels per 32-row m-tile (packed rows 32 (co / P) +
+//     (co % P) R + ph), writes the results to LDS as sample rows, and each
+//     thread runs the FIR over 4 consecutive output samples of a channel
+//     before bias, residuals and the store.
+// The weights (ou_conv_pack_split_nat order, include/ouhip.h) stream from L2
+// through a register ring one K chunk deep (the slot a step's MFMAs used is
+// refilled with the next chunk's same step); B is double-buffered in LDS, one
+// barrier per chunk.  Split-f16 (P 1: three MFMAs per k-step) or f16 (P 2).
+// ---------------------------------------------------------------------------
+[[maybe_unused]] constexpr int kFirBit = 1 << 17;
+
+template <int R, int WM, int WN, int MR, int NR>
+struct FCfg {
+    static_assert(WM * WN == 4, "4 waves per workgroup");
+    static constexpr int BM = 32 * WM * MR;
+    static constexpr int BN = 32 * WN * NR;
+    static constexpr int NT = 2 * R + 1;            // FIR taps
+    // down: K chunk = 16 channels x R phases (R k-steps); B row (frame) [ph][16 ch]
+    static constexpr int DRS = 16 * R + 8;          // halves (DRS / 8 = 2 R + 1 slots: odd)
+    static constexpr int DF = BN / 16;              // frames per staging thread (16 per channel)
+    static constexpr int DWIN = (DF + 2) * R;       // window samples per staging thread
+    static constexpr int DPLANE = BN * DRS;         // halves per plane
+    static constexpr int DLDS = 2 * 2 * DPLANE * 2; // bytes: 2 buffers x (hi, lo)
+    // up: K chunk = 32 channels (2 k-steps); B row (frame) [32 ch]
+    static constexpr int URS = 32 + 8;
+    static constexpr int UPLANE = BN * URS;
+    static constexpr int UIT = 4 * BN;              // staging items: 8 channels x 1 frame
+    static constexpr int UIE = (UIT + 255) / 256;
+    static constexpr int CPT = 32 / R;              // up: whole channels per 32-row m-tile
+    static constexpr int UCH = WM * MR * CPT;       // up: channels per workgroup
+    static constexpr int YRS = BN * R + 8;          // up: sample-row stride of the Y image (floats)
+    static constexpr int ULDS_B = 2 * 2 * UPLANE * 2;
+    static constexpr int ULDS_Y = UCH * YRS * 4;
+    static constexpr int ULDS = ULDS_B > ULDS_Y ? ULDS_B : ULDS_Y;
+};
+
+// FIR taps of one launch (uniform addresses: scalar loads)
+template <int NT>
+__device__ __forceinline__ void fir_taps(const ou_conv_desc& d, float (&tap)[NT])
+{
+#pragma unroll
+    for (int j = 0; j < NT; ++j) tap[j] = d.fir_taps[j];
+}
+
+template <int R, int WM, int WN, int MR, int NR, int P>
+__global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride)
+{
+    using F = FCfg<R, WM, WN, MR, NR>;
+    ou_kernarg_prefetch8();
+    OU_DYNAMIC_LDS(float4, lds4);
+    _Float16* ldsh = (_Float16*)lds4;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wave % WN, wm = wave / WN;
+    const int h = lane >> 5, l32 = lane & 31;
+    int bx, by, bz;
+    if (d.tile & kMajBit) ou_xcd_block_m(bx, by, bz); else ou_xcd_block(bx, by, bz);
+    const int b = bz;
+    const int n0 = bx * F::BN + d.f0;     // first output frame (global)
+    const int mt0 = by * (WM * MR);
+    const int in_len = d.in_len;
+    const int nch = d.cin / 16;           // K chunks
+    const float xsc = ou_exp2i(-d.xs_shift), su = d.w_unscale * ou_exp2i(d.xs_shift - kSplitShift);
+    const float slope = d.slope;
+    float tap[F::NT];
+    fir_taps<F::NT>(d, tap);
+
+    // ---- weights: chunk q, step s = phase -> 16-channel group q R + s
+    const __amdgpu_buffer_rsrc_t ars = ou_rsrc(d.w, (int64_t)mtiles * a_mt_stride * 4);
+    half8_t ra[R][MR][2];
+    auto load_a = [&](int q, int s) {   // q uniform, clamped (a reload past the end is never used)
+        q = min(q, nch - 1);
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr) {
+            const int mt = min(mt0 + wm * MR + mr, mtiles - 1);
+            const unsigned so = (unsigned)(mt * a_mt_stride * 4 + (int64_t)(q * R + s) * 2048);
+            ra[s][mr][0] = __builtin_bit_cast(half8_t, __builtin_amdgcn_raw_buffer_load_b128(ars, lane * 16, so, 0));
+            if constexpr (P == 1)
+                ra[s][mr][1] = __builtin_bit_cast(half8_t, __builtin_amdgcn_raw_buffer_load_b128(ars, lane * 16, so + 1024, 0));
+        }
+    };
+
+    // ---- staging: thread (channel sc of the chunk, frame group sg) owns
+    // frames n0 + sg F .. + F - 1; its window is samples [s0, s0 + (F + 2) R)
+    const int sc = tid >> 4, sg = tid & 15;
+    const int64_t xc = d.x_cstride;
+    const __amdgpu_buffer_rsrc_t xrs = ou_rsrc(d.x + (int64_t)b * d.x_bstride, (int64_t)d.cin * xc * 4);
+    const int s0 = (n0 + sg * F::DF - 1) * R;
+    // 16-B (R % 4 == 0) / 8-B (R == 2) loads where every row start is aligned
+    constexpr int V = R % 4 == 0 ? 4 : (R == 2 ? 2 : 1);
+    const bool vec = V > 1 && ((uintptr_t)d.x % (4 * V)) == 0 && d.x_bstride % V == 0 && xc % V == 0;
+    float xw[F::DWIN];
+    auto stage_load = [&](int q) {   // q uniform, clamped (the extra load is never stored)
+        q = min(q, nch - 1);
+        const int row = (q * 16 + sc) * (int)xc;
+        if (vec) {
+#pragma unroll
+            for (int e = 0; e < F::DWIN; e += V) {
+                const int smp = s0 + e;   // a multiple of V: a group lies wholly left of 0 or right of it
+                const int off = (smp >= 0 && smp < in_len) ? (row + smp) * 4 : kSentinel;
+                if constexpr (V == 4) {
+                    const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) xw[e + j] = smp + j < in_len ? __uint_as_float(v4[j]) : 0.f;
+                } else {
+                    const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(xrs, off, 0, 0);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) xw[e + j] = smp + j < in_len ? __uint_as_float(v2[j]) : 0.f;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < F::DWIN; ++e) {
+                const int smp = s0 + e;
+                xw[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    xrs, (smp >= 0 && smp < in_len) ? (row + smp) * 4 : kSentinel, 0, 0));
+            }
+        }
+    };
+    float omax = 0.f;
+    auto stage_store = [&](int buf) {
+        _Float16* bh = ldsh + buf * 2 * F::DPLANE + sg * F::DF * F::DRS + sc;
+#pragma unroll
+        for (int e = 0; e < F::DWIN; ++e) {
+            const float v = xw[e] * xsc;   // 2^-s: exact
+            xw[e] = v >= 0.f ? v : v * slope;
+        }
+#pragma unroll
+        for (int i = 0; i < F::DF * R; ++i) {
+            float f = 0.f;
+#pragma unroll
+            for (int j = 0; j < F::NT; ++j) f = fmaf(tap[j], xw[i + j], f);
+            omax = fmaxf(omax, __builtin_fabsf(f));
+            const _Float16 hi = (_Float16)f;
+            const int o = (i / R) * F::DRS + (i % R) * 16;
+            bh[o] = hi;
+            if constexpr (P == 1) bh[F::DPLANE + o] = (_Float16)((f - (float)hi) * 2048.f);
+        }
+    };
+
+    floatx16 acc[MR][NR];
+    floatx16 accx[P == 1 ? MR : 1][P == 1 ? NR : 1];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    if constexpr (P == 1) {
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) accx[i][j][r] = 0.f;
+    }
+    // B fragments of (buffer, phase s): row wn 32 NR + nr 32 + l32, halves s 16 + 8 h
+    const _Float16* bb = ldsh + (wn * 32 * NR + l32) * F::DRS + 8 * h;
+    auto mfma_step = [&](int buf, int s) {
+        half8_t bq[NR], bl[NR];
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+            const _Float16* p = bb + buf * 2 * F::DPLANE + nr * 32 * F::DRS + s * 16;
+            bq[nr] = *(const half8_t*)p;
+            if constexpr (P == 1) bl[nr] = *(const half8_t*)(p + F::DPLANE);
+        }
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+            for (int nr = 0; nr < NR; ++nr) {
+                acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][mr][0], bq[nr], acc[mr][nr], 0, 0, 0);
+                if constexpr (P == 1) {
+                    accx[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][mr][0], bl[nr], accx[mr][nr], 0, 0, 0);
+                    accx[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][mr][1], bq[nr], accx[mr][nr], 0, 0, 0);
+                }
+            }
+    };
+
+    stage_load(0);
+#pragma unroll
+    for (int s = 0; s < R; ++s) load_a(0, s);
+    stage_store(0);
+    __syncthreads();
+    for (int q = 0; q < nch; ++q) {
+        const int cur = q & 1;
+        stage_load(q + 1);   // the next chunk's window, in flight under this chunk's MFMAs
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+            mfma_step(cur, s);
+            load_a(q + 1, s);   // refill the slot just used
+        }
+        if (q + 1 < nch) stage_store(cur ^ 1);
+        __syncthreads();
+    }
+    if constexpr (P != 0) ou_range_flag(d.status, omax, 1, lane);
+    const float sx = su * (1.f / 2048.f);
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                acc[i][j][r] = P == 1 ? fmaf(accx[i][j][r], sx, acc[i][j][r] * su) : acc[i][j][r] * su;
+    conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane);
+}
+
+template <int R, int WM, int WN, int MR, int NR, int P>
+__global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride)
+{
+    using F = FCfg<R, WM, WN, MR, NR>;
+    constexpr int BNO = F::BN - 2;        // output frames per workgroup (one halo frame each side)
+    ou_kernarg_prefetch8();
+    OU_DYNAMIC_LDS(float4, lds4);
+    _Float16* ldsh = (_Float16*)lds4;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wave % WN, wm = wave / WN;
+    const int h = lane >> 5, l32 = lane & 31;
+    int bx, by, bz;
+    if (d.tile & kMajBit) ou_xcd_block_m(bx, by, bz); else ou_xcd_block(bx, by, bz);
+    const int b = bz;
+    const int u0 = bx * BNO + d.f0;       // first output frame
+    const int fa = u0 - 1;                // frame of B row 0
+    const int mt0 = by * (WM * MR);       // first packed m-tile
+    const int in_len = d.in_len;
+    const int nch = d.cin / 32;
+    const int cout = d.m / R;
+    const float xsc = ou_exp2i(-d.xs_shift), su = d.w_unscale * ou_exp2i(d.xs_shift - kSplitShift);
+    const float slope = d.slope;
+
+    const __amdgpu_buffer_rsrc_t ars = ou_rsrc(d.w, (int64_t)mtiles * a_mt_stride * 4);
+    half8_t ra[2][MR][2];
+    auto load_a = [&](int q, int s) {
+        q = min(q, nch - 1);
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr) {
+            const int mt = min(mt0 + wm * MR + mr, mtiles - 1);
+            const unsigned so = (unsigned)(mt * a_mt_stride * 4 + (int64_t)(q * 2 + s) * 2048);
+            ra[s][mr][0] = __builtin_bit_cast(half8_t, __builtin_amdgcn_raw_buffer_load_b128(ars, lane * 16, so, 0));
+            if constexpr (P == 1)
+                ra[s][mr][1] = __builtin_bit_cast(half8_t, __builtin_amdgcn_raw_buffer_load_b128(ars, lane * 16, so + 1024, 0));
+        }
+    };
+
+    // ---- staging: item it = (8-channel group cg = it / BN, row n = it % BN)
+    const int64_t xc = d.x_cstride;
+    const __amdgpu_buffer_rsrc_t xrs = ou_rsrc(d.x + (int64_t)b * d.x_bstride, (int64_t)d.cin * xc * 4);
+    float xv[F::UIE][8];
+    auto stage_load = [&](int q) {
+        q = min(q, nch - 1);
+#pragma unroll
+        for (int e = 0; e < F::UIE; ++e) {
+            const int it = tid + 256 * e;
+            const int n = it % F::BN, cg = it / F::BN;
+            const int u = fa + n;
+            const bool ok = it < F::UIT && u >= 0 && u < in_len;
+            const int base = ok ? ((q * 32 + cg * 8) * (int)xc + u) * 4 : kSentinel;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                xv[e][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, base, ok ? j * (int)xc * 4 : 0, 0));
+        }
+    };
+    float omax = 0.f;
+    auto stage_store = [&](int buf) {
+        _Float16* bh = ldsh + buf * 2 * F::UPLANE;
+#pragma unroll
+        for (int e = 0; e < F::UIE; ++e) {
+            const int it = tid + 256 * e;
+            if (F::UIT % 256 != 0 && it >= F::UIT) continue;
+            const int n = it % F::BN, cg = it / F::BN;
+            half8_t hi, lo;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float v = xv[e][j] * xsc;
+                v = v >= 0.f ? v : v * slope;
+                omax = fmaxf(omax, __builtin_fabsf(v));
+                hi[j] = (_Float16)v;
+                lo[j] = (_Float16)((v - (float)hi[j]) * 2048.f);
+            }
+            *(half8_t*)(bh + n * F::URS + cg * 8) = hi;
+            if constexpr (P == 1) *(half8_t*)(bh + F::UPLANE + n * F::URS + cg * 8) = lo;
+        }
+    };
+
+    floatx16 acc[MR][NR];
+    floatx16 accx[P == 1 ? MR : 1][P == 1 ? NR : 1];
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    if constexpr (P == 1) {
+#pragma unroll
+        for (int i = 0; i < MR; ++i)
+#pragma unroll
+            for (int j = 0; j < NR; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) accx[i][j][r] = 0.f;
+    }
+    const _Float16* bb = ldsh + (wn * 32 * NR + l32) * F::URS + 8 * h;
+    auto mfma_step = [&](int buf, int s) {
+        half8_t bq[NR], bl[NR];
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+            const _Float16* p = bb + buf * 2 * F::UPLANE + nr * 32 * F::URS + s * 16;
+            bq[nr] = *(const half8_t*)p;
+            if constexpr (P == 1) bl[nr] = *(const half8_t*)(p + F::UPLANE);
+        }
+#pragma unroll
+        for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+            for (int nr = 0; nr < NR; ++nr) {
+                acc[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][mr][0], bq[nr], acc[mr][nr], 0, 0, 0);
+                if constexpr (P == 1) {
+                    accx[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][mr][0], bl[nr], accx[mr][nr], 0, 0, 0);
+                    accx[mr][nr] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ra[s][mr][1], bq[nr], accx[mr][nr], 0, 0, 0);
+                }
+            }
+    };
+
+    stage_load(0);
+    load_a(0, 0);
+    load_a(0, 1);
+    stage_store(0);
+    __syncthreads();
+    for (int q = 0; q < nch; ++q) {
+        const int cur = q & 1;
+        stage_load(q + 1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            mfma_step(cur, s);
+            load_a(q + 1, s);
+        }
+        if (q + 1 < nch) stage_store(cur ^ 1);
+        __syncthreads();
+    }
+    if constexpr (P != 0) ou_range_flag(d.status, omax, 1, lane);
+
+    // ---- the transposed conv's outputs -> Y [channel of the workgroup][sample]
+    // (sample row index n R + ph for B row n, i.e. global sample (fa + n) R + ph)
+    float* Y = (float*)lds4;
+    const float sx = su * (1.f / 2048.f);
+#pragma unroll
+    for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int ml = (r & 3) + 8 * (r >> 2) + 4 * h;   // row within the m-tile
+                const int cl = ml / R, ph = ml - (ml / R) * R;
+                const float v = P == 1 ? fmaf(accx[mr][nr][r], sx, acc[mr][nr][r] * su) : acc[mr][nr][r] * su;
+                if (cl < F::CPT)
+                    Y[((wm * MR + mr) * F::CPT + cl) * F::YRS + (wn * 32 * NR + nr * 32 + l32) * R + ph] = v;
+            }
+    __syncthreads();
+
+    // ---- FIR over 4 consecutive output samples per item, bias, residuals, store
+    float tap[F::NT];
+    fir_taps<F::NT>(d, tap);
+    const int ylen = d.out_len, vlen = d.valid_len;
+    const int tend = min((min(u0 + BNO, d.f0 + d.n_frames)) * R, ylen);   // samples [u0 R, tend) are stored
+    const int c0 = mt0 * F::CPT;                                           // first channel of the workgroup
+    const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr, has_fm = d.film != nullptr;
+    const float s1e = has_r1 ? d.s1 : 1.f, s2e = has_r2 ? d.s2 : 1.f, fadd = has_fm ? 0.f : 1.f;
+    const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)cout * d.y_cstride * 4);
+    const __amdgpu_buffer_rsrc_t r1s =
+        ou_rsrc(has_r1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y, has_r1 ? (int64_t)cout * d.r1_cstride * 4 : 0);
+    const __amdgpu_buffer_rsrc_t r2s =
+        ou_rsrc(has_r2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y, has_r2 ? (int64_t)cout * d.r2_cstride * 4 : 0);
+    const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
+    const __amdgpu_buffer_rsrc_t fs =
+        ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y, has_fm ? (int64_t)cout * 8 : 0);
+    constexpr int NSG = (BNO * R + 3) / 4;   // 4-sample groups per channel
+    constexpr int NW = (4 + 2 * R + 3) / 4 * 4;   // window floats read (16-B reads)
+    for (int it = tid; it < F::UCH * NSG; it += 256) {
+        const int cw = it / NSG, g = it - (it / NSG) * NSG;
+        const int co = c0 + cw;
+        const int sig = 4 * g;            // output sample u0 R + sig <-> Y index sig + R
+        const int t0 = u0 * R + sig;
+        float w[NW];
+        const float* yr = Y + cw * F::YRS + sig;
+#pragma unroll
+        for (int k = 0; k < NW; k += 4) {
+            const float4 q4 = *(const float4*)(yr + k);
+            w[k] = q4.x, w[k + 1] = q4.y, w[k + 2] = q4.z, w[k + 3] = q4.w;
+        }
+        const bool cok = co < cout;
+        const float bias = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, cok ? co * 4 : kSentinel, 0, 0));
+        const float ga = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, cok ? co * 4 : kSentinel, 0, 0));
+        const float gb = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, cok ? (cout + co) * 4 : kSentinel, 0, 0));
+        int off[4];
+        float v1[4], v2[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int t = t0 + k;
+            off[k] = (cok && sig + k < BNO * R && t < tend) ? t : -1;
+            v1[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                r1s, off[k] >= 0 ? (co * (int)d.r1_cstride + t) * 4 : kSentinel, 0, 0));
+            v2[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                r2s, off[k] >= 0 ? (co * (int)d.r2_cstride + t) * 4 : kSentinel, 0, 0));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float f = 0.f;
+#pragma unroll
+            for (int j = 0; j < F::NT; ++j) f = fmaf(tap[j], w[k + j], f);
+            float v = f + bias;
+            if (off[k] >= vlen) v = 0.f;
+            v = (v + v1[k]) * s1e;
+            v = (ga + fadd) * v + gb;
+            v = (v + v2[k]) * s2e;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ys,
+                                                  off[k] >= 0 ? (co * (int)d.y_cstride + off[k]) * 4 : kSentinel, 0, 0);
+        }
+    }
+}
+
 // ---- tile table ------------------------------------------------------------
 struct Tile {
     int wm, wn, wk, mr, nr, big;
@@ -2769,6 +3206,58 @@ int launch_ss(const ou_conv_desc& d, int shape, hipStream_t s)
     }
 }
 
+// FIR shapes (tile bit 17): id, WM, WN, MR, NR (BM = 32 WM MR rows, BN = 32 WN NR frames)
+#define OU_FTILES(X) \
+    X(0, 2, 2, 1, 1) X(1, 4, 1, 1, 2) X(2, 2, 2, 2, 1) X(3, 1, 4, 2, 1) X(4, 2, 2, 1, 2) X(5, 4, 1, 2, 1) \
+    X(6, 2, 2, 2, 2) X(7, 4, 1, 1, 1)
+[[maybe_unused]] constexpr int kNumFTiles = 8;
+
+template <typename K>
+int fir_launch(K kern, int lds, dim3 grid, const ou_conv_desc& d, int mtiles, int64_t a_mt_stride, bool& attr,
+               hipStream_t s)
+{
+    if (!attr && lds > 64 * 1024) {
+        OU_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds),
+                     "conv: LDS attribute");
+        attr = true;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, d, mtiles, a_mt_stride);
+    return ou_check_launch("conv (FIR)");
+}
+
+template <int R, int WM, int WN, int MR, int NR>
+int launch_f(const ou_conv_desc& d, hipStream_t s)
+{
+    using F = FCfg<R, WM, WN, MR, NR>;
+    static bool attr[4] = {false, false, false, false};   // (direction, precision) opted in to > 64 KiB
+    if (d.fir == 1) {   // down: K = cin R in chunks of 16 channels
+        const int mtiles = (d.m + 31) / 32;
+        const int64_t a_mt_stride = (int64_t)((d.cin * R + kCinAlign - 1) / kCinAlign * kCinAlign) * 32;
+        const dim3 grid((d.n_frames + F::BN - 1) / F::BN, (mtiles + WM * MR - 1) / (WM * MR), d.batch);
+        return d.prec == 1
+                   ? fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 1>, F::DLDS, grid, d, mtiles, a_mt_stride, attr[0], s)
+                   : fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 2>, F::DLDS, grid, d, mtiles, a_mt_stride, attr[1], s);
+    }
+    // up: K = cin in chunks of 32; P = 32 / R whole channels per packed m-tile
+    const int mtiles = (d.m / R + F::CPT - 1) / F::CPT;
+    const int64_t a_mt_stride = (int64_t)((d.cin + kCinAlign - 1) / kCinAlign * kCinAlign) * 32;
+    const dim3 grid((d.n_frames + F::BN - 3) / (F::BN - 2), (mtiles + WM * MR - 1) / (WM * MR), d.batch);
+    return d.prec == 1
+               ? fir_launch(conv_fukernel<R, WM, WN, MR, NR, 1>, F::ULDS, grid, d, mtiles, a_mt_stride, attr[2], s)
+               : fir_launch(conv_fukernel<R, WM, WN, MR, NR, 2>, F::ULDS, grid, d, mtiles, a_mt_stride, attr[3], s);
+}
+
+template <int R>
+int launch_fr(const ou_conv_desc& d, int shape, hipStream_t s)
+{
+    switch (shape) {
+#define OU_FTILE_CASE(id, wm, wn, mr, nr) case id: return launch_f<R, wm, wn, mr, nr>(d, s);
+        OU_FTILES(OU_FTILE_CASE)
+#undef OU_FTILE_CASE
+    }
+    return ou_fail(-2, "conv: bad FIR tile %d", shape);
+}
+
 template <int KT>
 int launch_kt(const ou_conv_desc& d, int tile, int tpw, bool ws, hipStream_t s)
 {
@@ -2849,20 +3338,30 @@ int OU_CAT(ou_conv_launch_kt, OU_CONV_SPLIT_KT)(const ou_conv_desc& d, int tile,
     return launch_kt<OU_CONV_SPLIT_KT>(d, tile, tpw, ws, s);
 }
 int OU_CAT(ou_conv_lds_kt, OU_CONV_SPLIT_KT)(int tile) { return lds_bytes_kt<OU_CONV_SPLIT_KT>(tile); }
+#elif defined(OU_CONV_SPLIT_FIR)   // the FIR kernels of one rate R (-DOU_CONV_SPLIT_FIR=R)
+int OU_CAT(ou_conv_launch_fir, OU_CONV_SPLIT_FIR)(const ou_conv_desc& d, int shape, hipStream_t s)
+{
+    return launch_fr<OU_CONV_SPLIT_FIR>(d, shape, s);
+}
 #elif defined(OU_CONV_SPLIT_MAIN)
 #define OU_KT_DECL(K)                                                                           \
     int ou_conv_launch_kt##K(const ou_conv_desc& d, int tile, int tpw, bool ws, hipStream_t s); \
     int ou_conv_lds_kt##K(int tile);
 OU_KT_DECL(1) OU_KT_DECL(3) OU_KT_DECL(4) OU_KT_DECL(5)
 #undef OU_KT_DECL
+#define OU_FIR_DECL(R) int ou_conv_launch_fir##R(const ou_conv_desc& d, int shape, hipStream_t s);
+OU_FIR_DECL(2) OU_FIR_DECL(3) OU_FIR_DECL(4) OU_FIR_DECL(5) OU_FIR_DECL(8)
+#undef OU_FIR_DECL
 #define OU_LAUNCH_KT(K, ...) ou_conv_launch_kt##K(__VA_ARGS__)
 #define OU_LDS_KT(K, tile) ou_conv_lds_kt##K(tile)
+#define OU_LAUNCH_FIR(R, ...) ou_conv_launch_fir##R(__VA_ARGS__)
 #else
 #define OU_LAUNCH_KT(K, ...) launch_kt<K>(__VA_ARGS__)
 #define OU_LDS_KT(K, tile) lds_bytes_kt<K>(tile)
+#define OU_LAUNCH_FIR(R, ...) launch_fr<R>(__VA_ARGS__)
 #endif
 
-#if !defined(OU_CONV_SPLIT_KT)
+#if !defined(OU_CONV_SPLIT_KT) && !defined(OU_CONV_SPLIT_FIR)
 namespace {
 int lds_bytes(int kt, int tile)
 {
@@ -3025,6 +3524,30 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
             return ou_fail(-1, "conv: split-image output needs prec 1, rout 1, m %% 32 == 0, sy_rows >= out_len "
                                "(m %d rout %d rows %d out_len %d)", d.m, d.rout, d.sy_rows, d.out_len);
     }
+    if (d.fir || (d.tile >= 0 && (d.tile & kFirBit))) {   // FIR applied (bits 0-7: OU_FTILES shape)
+        const int R = d.fir == 1 ? d.frame : (d.rout < 0 ? -d.rout : d.rout);
+        if ((d.fir != 1 && d.fir != 2) || !d.fir_taps || (d.prec != 1 && d.prec != 2) || d.kt != 1 || d.pad ||
+            d.shift || d.in_scale || d.xs || (d.fir == 1 && (d.rout != 1 || d.cin % 16)) ||
+            (d.fir == 2 && (d.frame != 1 || d.cin % 32)) || (R != 2 && R != 3 && R != 4 && R != 5 && R != 8))
+            return ou_fail(-1, "conv: FIR mode %d needs prec 1/2, kt 1, pad 0, shift 0, no in_scale / xs, rate 2/3/4/5/8, "
+                               "cin %% 16 (down) / 32 (up) == 0 (cin %d frame %d rout %d kt %d)",
+                           d.fir, d.cin, d.frame, d.rout, d.kt);
+        if (!(d.w_unscale > 0.f)) return ou_fail(-1, "conv: FIR mode needs the w_unscale of ou_conv_pack_split_nat");
+        const int tile = d.tile >= 0 ? d.tile : (kFirBit | 2);
+        if (!(tile & kFirBit) || (tile & ~(kFirBit | kMajBit | 0xff)) || (tile & 0xff) >= kNumFTiles)
+            return ou_fail(-2, "conv: FIR mode needs a FIR tile (tile 0x%x)", d.tile);
+        ou_conv_desc dd = d;   // the kernels read their order bit from the tile
+        dd.tile = tile;
+        hipStream_t fs = (hipStream_t)stream;
+        switch (R) {
+        case 2: return OU_LAUNCH_FIR(2, dd, tile & 0xff, fs);
+        case 3: return OU_LAUNCH_FIR(3, dd, tile & 0xff, fs);
+        case 4: return OU_LAUNCH_FIR(4, dd, tile & 0xff, fs);
+        case 5: return OU_LAUNCH_FIR(5, dd, tile & 0xff, fs);
+        case 8: return OU_LAUNCH_FIR(8, dd, tile & 0xff, fs);
+        }
+        return ou_fail(-2, "conv: no FIR kernel for rate %d", R);
+    }
     if (d.xs || (d.tile >= 0 && (d.tile & kSsBit))) {   // split-image input (bits 0-7: NR - 1)
         // static choice: 64-frame workgroups while they still give one per CU
         const int tile = d.tile >= 0 ? d.tile
@@ -3116,6 +3639,8 @@ extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile_f
 extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int ou_conv_tile_ok(int kt, int tile)
 {
+    if (tile & kFirBit)   // FIR applied (ou_conv_desc.fir): shape (+ m-major order); one tap
+        return !(tile & ~(kFirBit | kMajBit | 0xff)) && (tile & 0xff) < kNumFTiles && kt == 1;
     if (tile & kSsBit)   // split-image input: shape = NR - 1 (+ m-major order)
         return !(tile & ~(kSsBit | kMajBit | 0xff)) && (tile & 0xff) < kNumSTiles && (kt == 1 || kt == 3 || kt == 5);
     if (tile & kRsBit)   // register-streamed: shape id (+ K slices, m-major order); LDS and chunks checked at launch

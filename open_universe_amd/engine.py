@@ -47,21 +47,19 @@ _PREP_PREC = None     # set by Engine while it packs its weights
 _PREP_STATUS = 0      # device int32* the split-f16 convs flag range errors into (outside an Engine)
 _PREP_ENGINE = None   # the Engine packing its weights: hands out per-layer range slots
 RANGE_SLOTS = 1024    # per-layer range-flag words after the engine's 4 status words
-_SPLIT_CONSUMERS = {}   # producer's range slot -> the ConvW whose split image it stores
 MAX_SHIFT = 40        # staging exponents past this fall back to f32 operands
 _PREP_KSWS = (0, 0)   # (device float*, bytes): the engine's K-slice workspace
 KSWS_BYTES = 64 << 20
 RS_BIT = 1 << 14      # ConvDesc.tile bit: the register-streamed conv kernel (conv_rkernel)
 
 _REC = None   # set while a plan records (begin_record)
-_TUNE_BATCH = None   # the plan's batch while it records sub-batches (ConvTuner.geometry)
 # lane the recorder is on (plan lanes run concurrently) and the plan slot
 # (plans of one model that may run at the same time on different streams,
 # Universe.enhance_many): convs recorded on (slot, lane) use K-slice workspace
 # slot * MAX_LANES + lane of their engine
 _LANE = 0
 _SLOT = 0
-MAX_LANES = 4   # 0 main (and the chunked pass's GRU), 1 conditioner, 2-3 the chunked pass's convs
+MAX_LANES = 4   # 0 main (score network), 1 conditioner, 2 mel front end + signal_cond_proj convs, 3 spare
 MAX_SLOTS = 2   # a third stream measured slower: the box gives a process 4 hardware queues
 
 
@@ -73,23 +71,7 @@ def set_lane(prog, i):
     _LANE = i
 
 
-SUB_LANE = 3   # the second score sub-batch's lane (plan.EnhancePlan)
 SC_LANE = 2    # the conditions' signal_cond_proj convs (after the mel front end on the same lane)
-
-
-def score_sub_batches(B):
-    """[(b0, b1), ...]: the score network's batch split in two halves on two
-    lanes (EnhancePlan), or None.  With two sub-batches one half's GRU chain
-    runs beside the other half's convolutions.  Opt-in (OUHIP_SUB_BATCH=1,
-    B >= 2): measured at C4's per-rank batch of 4 it is slower, 522-532
-    against 549-567 audio-s/s (profiles/c4_subbatch_r05s.txt) -- the halves'
-    convolutions lose more than the overlap hides."""
-    import os
-
-    if B < 2 or os.environ.get("OUHIP_SUB_BATCH", "0") != "1":
-        return None
-    h = (B + 1) // 2
-    return [(0, h), (h, B)]
 
 
 def overlap_enabled():
@@ -108,6 +90,26 @@ def split_images_enabled():
 
 
 _REC_DEVICE = None   # the recording engine's device (split-image buffers outside an arena)
+
+# Anti-aliased rate-change convs (PReLU_Conv with use_antialiasing,
+# blocks.py:214-226) have two forms: the (2r+1)-tap binomial FIR folded into
+# 3-frame weights (any kernel; three times the reference's dense MACs) and the
+# FIR applied by conv_fdkernel / conv_fukernel (tile bit 17, ou_conv_desc.fir;
+# the reference's MACs).  OUHIP_FIR=auto (default) times both per layer and
+# records the faster, 1 always the FIR-applied form, 0 always the folded one.
+FIR_RATES = (2, 3, 4, 5, 8)
+FIR_BIT = 1 << 17
+
+
+def fir_mode():
+    v = os.environ.get("OUHIP_FIR", "auto").strip().lower()
+    if v not in ("auto", "0", "1"):
+        raise ValueError(f"OUHIP_FIR={v!r}: expected auto, 0 or 1")
+    return v
+
+
+def fir_enabled():
+    return fir_mode() != "0"
 
 
 def begin_record(prec, device=None):
@@ -139,8 +141,7 @@ def _split_consumer(op, d):
     op that can read its operand from a split image, or None."""
     if op == L.OP_CONV:
         wn = getattr(d, "_w_nat", None)
-        if (wn is None or getattr(d, "_no_split", False) or d.prec != 1 or d.xs or d.in_scale or d.f0 or d.cin % 32
-                or getattr(d, "_full", None) is not None):
+        if wn is None or getattr(d, "_no_split", False) or d.prec != 1 or d.xs or d.in_scale or d.f0 or d.cin % 32:
             return None
         return (d.x, d.x_bstride, d.x_cstride, d.in_len, d.cin, d.slope, d.xs_shift, ("c", getattr(d, "_cw", None), 0))
     fw = getattr(d, "_fw", None)
@@ -153,7 +154,7 @@ def _split_producer(op, p):
     """(y ptr, bstride, cstride, out_len, channels, batch) of an op whose
     epilogue can store a split image, or None."""
     if op == L.OP_CONV:
-        if (p.prec != 1 or p.rout != 1 or p.m % 32 or p.sy or p.f0 or getattr(p, "_full", None) is not None):
+        if p.prec != 1 or p.rout != 1 or p.m % 32 or p.sy or p.f0:
             return None
         return (p.y, p.y_bstride, p.y_cstride, p.out_len, p.m, p.batch)
     if (p.prec != 1 or p.head.w or p.sy or p.channels % 32 or p.f0 or p.f1):
@@ -164,7 +165,23 @@ def _split_producer(op, p):
 SPLIT_STORE_BPMS = 4e9   # bytes per ms a producer's epilogue adds for its image (~4 TB/s)
 
 
-def _split_pays(d, buf, per_item, rows, shift, batch):
+def _split_ms(d, per_item, rows, shift, batch):
+    """Tuned ms per launch of conv ``d`` reading a split image, plus the
+    producer's extra image store (~ bytes / 4 TB/s), or None without a tuner.
+    The trial reads the image from d's own input (the same or more bytes:
+    timing only reads it), so no image memory is taken to decide."""
+    tuner = L.TUNER
+    if not hasattr(tuner, "pick"):
+        return None
+    trial = L.ConvDesc.from_buffer_copy(d)
+    trial.xs, trial.xs_bstride, trial.xs_rows, trial.xs_shift = d.x, per_item, rows, shift
+    trial.w, trial.w_unscale = d._w_nat
+    trial.tile = -1
+    _, ms_s = tuner.pick(trial)
+    return None if ms_s is None else ms_s + batch * per_item / SPLIT_STORE_BPMS
+
+
+def _split_pays(d, per_item, rows, shift, batch):
     """A conv consumer takes the split image only where the split-image
     kernel's best tile, plus the producer's extra image store, beats its best
     plain tile (both timed by the tuner; without one, always)."""
@@ -174,16 +191,10 @@ def _split_pays(d, buf, per_item, rows, shift, batch):
     plain = L.ConvDesc.from_buffer_copy(d)
     plain.tile = -1
     _, ms_p = tuner.pick(plain)
-    trial = L.ConvDesc.from_buffer_copy(d)
-    trial.xs, trial.xs_bstride, trial.xs_rows, trial.xs_shift = buf.data_ptr(), per_item, rows, shift
-    trial.w, trial.w_unscale = d._w_nat
-    trial.tile = -1
-    _, ms_s = tuner.pick(trial)
+    ms_s = _split_ms(d, per_item, rows, shift, batch)
     if ms_p is None or ms_s is None:
         return True
-    # the plan's batch (as the tuner's keys): sub-batched and whole plans decide alike
-    b = _TUNE_BATCH if _TUNE_BATCH is not None else batch
-    return ms_s + b * per_item / SPLIT_STORE_BPMS < ms_p
+    return ms_s < ms_p
 
 
 def _split_note(prog, idx, op, d):
@@ -204,40 +215,53 @@ def _split_note(prog, idx, op, d):
             writers[d.y] = (idx, op, d, y[0])
 
 
+def _split_link(prog, op, d):
+    """The split-image link op ``d`` would take (see split_hook), or None:
+    (producer index, producer op, producer desc, rows, batch, per-item
+    bytes, consumer tuple)."""
+    cons = _split_consumer(op, d)
+    pv = prog.__dict__.get("split_writers", {}).get(d.x if op == L.OP_CONV else d.h)
+    if cons is None or pv is None:
+        return None
+    idx, pop, p, _ = pv
+    prod = _split_producer(pop, p)
+    x, xb, xc, in_len, C, slope, shift, owner = cons
+    if (p is d or prod is None or prod[0] != x or prod[1] != xb or prod[2] != xc or prod[3] < in_len
+            or prod[4] != C or prod[5] < d.batch):
+        return None
+    rows, batch = prod[3], prod[5]
+    return idx, pop, p, rows, batch, (C // 32) * rows * 128, cons
+
+
 def split_hook(prog, op, d):
     """Program.add hook (split-f16 plans): link op ``d`` (a conv, or a fused
     block's conv1) to the split image of the op that last wrote d's input,
     when that op is a conv or a fused block (any lane: d reads that output,
     so the program already orders d after it).  The pairing follows the data,
     not the lanes, so plans that place unrelated ops differently (enhance and
-    enhance_many's) link the same pairs and compute the same bits."""
-    cons = _split_consumer(op, d)
-    pv = prog.__dict__.get("split_writers", {}).get(d.x if op == L.OP_CONV else d.h)
-    if cons is None or pv is None:
+    enhance_many's) link the same pairs and compute the same bits.  A conv
+    consumer is linked only where that pays (_split_pays, decided before any
+    image memory is taken)."""
+    link = _split_link(prog, op, d)
+    if link is None:
         return
-    idx, pop, p, _ = pv
-    prod = _split_producer(pop, p)
+    idx, pop, p, rows, batch, per_item, cons = link
     x, xb, xc, in_len, C, slope, shift, owner = cons
-    if (p is d or prod is None or prod[0] != x or prod[1] != xb or prod[2] != xc or prod[3] < in_len
-            or prod[4] != C or prod[5] < d.batch):
+    if op == L.OP_CONV and not _split_pays(d, per_item, rows, shift, batch):
         return
-    rows, batch = prod[3], prod[5]
-    per_item = (C // 32) * rows * 128
     # one image per activation buffer: every step of the score loop rewrites
     # the same activations in the same order, so their images too
     key = (x, xb, xc, rows, C, batch)
     cache = prog.__dict__.setdefault("split_bufs", {})
     buf = cache.get(key)
     if buf is None:
-        buf = empty((batch * per_item // 2,), dtype=torch.int16, device=_REC_DEVICE)
-    if op == L.OP_CONV and not _split_pays(d, buf, per_item, rows, shift, batch):
-        return
-    if key not in cache:
-        cache[key] = buf
+        buf = cache[key] = empty((batch * per_item // 2,), dtype=torch.int16, device=_REC_DEVICE)
         prog.keep.append(buf)
     prog.__dict__.setdefault("split_links", []).append((idx, len(prog.flops)))
     if p.status and owner[1] is not None:
-        _SPLIT_CONSUMERS[p.status] = owner   # a split-image range code (2 / 32) of p widens d's operand
+        # a split-image range code (2 / 32) of p widens d's operand: kept per
+        # program, so a plan's error resolves against the pairs it recorded
+        prog.__dict__.setdefault("split_consumers", {})[p.status] = owner
     p.sy, p.sy_bstride, p.sy_rows, p.sy_shift, p.sy_slope = buf.data_ptr(), per_item, rows, shift, slope
     prog.patch(idx, pop, p)
     d.xs, d.xs_bstride, d.xs_rows = p.sy, per_item, rows
@@ -292,10 +316,24 @@ class ConvW:
     w_nat: Optional[torch.Tensor] = None   # prec 1, cin % 32 == 0: ou_conv_pack_split_nat (split-image kernel)
     w_unscale_nat: float = 1.0
     xshift: int = 6          # split-f16 staging exponent of this conv's input (ConvDesc.xs_shift)
+    fir: Optional["FirW"] = None   # the FIR-applied form of an anti-aliased rate-change conv
 
     @property
     def cout(self):
         return self.m // self.rout
+
+
+@dataclass
+class FirW:
+    """The FIR-applied form of an anti-aliased rate-change conv (ou_conv_desc.fir,
+    tile bit 17): unfolded weights (K = cin * rate down, cin up; one tap) in
+    the kernels' order (include/ouhip.h), packed by ou_conv_pack_split_nat,
+    and the (2 rate + 1)-tap binomial FIR on the device."""
+    mode: int                # 1: FIR before a strided conv, 2: after a transposed conv
+    rate: int
+    w: torch.Tensor
+    unscale: float
+    taps: torch.Tensor
 
 
 @dataclass
@@ -312,6 +350,7 @@ class ConvSpec:
     shift: int = 0
     ref_macs: float = 0.0   # MACs of the replaced reference ops per output frame
     cm: bool = False        # rout > 1: rows ordered m = co * rout + ph (else ph * cout + co)
+    fir: Optional[tuple] = None   # (mode 1 down / 2 up, rate, unfolded logical weights, taps): FirW
 
 
 def make_conv(spec, device, prec=None):
@@ -337,9 +376,15 @@ def make_conv(spec, device, prec=None):
     if prec == 1 and spec.cin % 32 == 0 and kt in (1, 3, 5) and split_images_enabled():
         nat_np, unscale_nat = L.conv_pack_split_nat_np(w_logical)
         w_nat = torch.from_numpy(nat_np).to(device)
+    fir = None
+    if spec.fir is not None and prec in (1, 2) and fir_enabled():
+        mode, rate, wf, taps = spec.fir
+        fp_np, fun = L.conv_pack_split_nat_np(np.ascontiguousarray(wf, np.float32)[:, :, None])
+        fir = FirW(int(mode), int(rate), torch.from_numpy(fp_np).to(device), float(fun),
+                   torch.from_numpy(np.ascontiguousarray(taps, np.float32)).to(device))
     cw = ConvW(m, spec.cin, kt, spec.frame, spec.pad, spec.rout, float(spec.slope), cc, packed, b,
                spec.shift, spec.ref_macs, int(prec), float(unscale), _PREP_STATUS if prec else 0,
-               _PREP_KSWS, cm=bool(spec.cm), w_nat=w_nat, w_unscale_nat=float(unscale_nat))
+               _PREP_KSWS, cm=bool(spec.cm), w_nat=w_nat, w_unscale_nat=float(unscale_nat), fir=fir)
     if prec:
         cw.status = _range_slot(cw) or cw.status
     return cw
@@ -391,8 +436,13 @@ def spec_down(sd, p, r, antialias):
         for kk in range(r):
             wf[:, :, kk:kk + 2 * r + 1] += w[:, :, kk:kk + 1].astype(np.float64) * fir[None, None, :]
         wl = wf.reshape(cout, cin, 3, r).transpose(0, 1, 3, 2).reshape(cout, cin * r, 3)
+        fir = None
+        if cin % 16 == 0 and r in FIR_RATES:
+            # unfolded, K order k = (cb r + ph) 16 + c for ci = 16 cb + c (include/ouhip.h)
+            wu = w.reshape(cout, cin // 16, 16, r).transpose(0, 1, 3, 2).reshape(cout, cin * r)
+            fir = (1, r, wu, dsp.binomial_taps(2 * r + 1))
         return ConvSpec(wl, cin, r, 1, 1, _slope(sd, p), _bias(sd, p + ".bias"),
-                        ref_macs=float(cout * cin * r + cin * (2 * r + 1) * r))
+                        ref_macs=float(cout * cin * r + cin * (2 * r + 1) * r), fir=fir)
     return ConvSpec(w.reshape(cout, cin * r, 1), cin, r, 0, 1, _slope(sd, p),
                     _bias(sd, p + ".conv.bias"), ref_macs=float(cout * cin * r))
 
@@ -420,8 +470,19 @@ def spec_up(sd, p, r, antialias):
         cm = r >= 2
         if cm:
             wl = wl.transpose(1, 0, 2, 3)
+        fir = None
+        if cin % 32 == 0 and r in FIR_RATES and cm:
+            # unfolded: every 32-row m-tile holds P = 32 // r whole channels,
+            # row 32 (co // P) + (co % P) r + ph (include/ouhip.h)
+            P = 32 // r
+            wu = np.zeros((-(-cout // P) * 32, cin), dtype=np.float64)
+            co = np.arange(cout)
+            for ph in range(r):
+                wu[32 * (co // P) + (co % P) * r + ph] = w[:, :, ph].T
+            fir = (2, r, wu, dsp.binomial_taps(2 * r + 1))
         return ConvSpec(np.ascontiguousarray(wl).reshape(r * cout, cin, 3), cin, 1, 1, r, _slope(sd, p),
-                        _bias(sd, p + ".bias"), ref_macs=float(cin * cout * r + cout * (2 * r + 1) * r), cm=cm)
+                        _bias(sd, p + ".bias"), ref_macs=float(cin * cout * r + cout * (2 * r + 1) * r), cm=cm,
+                        fir=fir)
     wl = w.transpose(2, 1, 0)   # (r, cout, cin)
     cm = r >= 2
     if cm:
@@ -643,25 +704,10 @@ def new_act(B, C, T, device):
 
 def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=None,
               valid_len=None, in_scale=0, res1: Act = None, s1=1.0, film=0, film_bs=0,
-              res2: Act = None, s2=1.0, batch=None, rng=None):
-    """ou_conv descriptor.  rng = (a, b): output frames [a, b) only (a chunk
-    of the signal, in the frame coordinates of the whole op): the launch
-    keeps the tile of the whole op -- the same K order per output frame, so
-    chunks and the whole op agree bit for bit wherever both compute -- and
-    reads x only up to the last sample those frames need (the rest reads as
-    zero: a chunk's caller has produced x only there).  Its FLOP / byte
-    counts stay the whole op's (rec_block scales them by the chunk's share)."""
-    if rng is not None:
-        full = conv_desc(cw, x, y, in_len=in_len, n_frames=n_frames, out_len=out_len, valid_len=valid_len,
-                         in_scale=in_scale, res1=res1, s1=s1, film=film, film_bs=film_bs, res2=res2, s2=s2,
-                         batch=batch)
-        a, b = max(0, rng[0]), min(full.n_frames, rng[1])
-        assert 0 <= a < b, ("conv chunk", rng, full.n_frames)
-        d = L.ConvDesc.from_buffer_copy(full)
-        d._flops, d._bytes, d._full = full._flops, full._bytes, full   # add_conv pins the tile
-        d.in_len = max(1, min(d.in_len, (b - cw.pad + cw.kt - 1) * cw.frame + cw.shift))
-        d.f0, d.n_frames = a, b - a
-        return d
+              res2: Act = None, s2=1.0, batch=None):
+    """ou_conv descriptor of conv ``cw`` from x to y (include/ouhip.h), with
+    its shape guards and its algorithmic FLOP / byte counts (d._flops,
+    d._bytes: the roofline accounting)."""
     d = L.ConvDesc()
     d.x, d.x_bstride, d.x_cstride = x.ptr, x.bs, x.cs
     d.cin, d.in_len = cw.cin, x.T if in_len is None else in_len
@@ -672,6 +718,7 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
     d.xs_shift = cw.xshift
     d._w_nat = (cw.w_nat.data_ptr(), cw.w_unscale_nat) if cw.w_nat is not None else None
     d._cw = cw
+    d._fir = cw.fir
     d.ks_ws, d.ks_ws_bytes = cw.ks_ws
     if (_LANE or _SLOT) and d.ks_ws:   # the engine allocates MAX_SLOTS x MAX_LANES workspaces
         d.ks_ws += (_SLOT * MAX_LANES + _LANE) * d.ks_ws_bytes
@@ -711,50 +758,25 @@ def conv_desc(cw: ConvW, x: Act, y: Act, *, in_len=None, n_frames=None, out_len=
 
 def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film_bs=0,
               sc: Act = None, res2: Act = None, s2=1.0, cond_out: Act = None, skip_tail=False,
-              x_in=None, head=None, e_out: Act = None, rng=None, e_rng=None, share=1.0, after_c1=None):
+              x_in=None, head=None, e_out: Act = None, after_c1=None):
     """ConvBlock main stage (blocks.py:393-407):
        cond_out = conv1(h); c = (cond_out + sc)/sqrt2; c = film(c); c = conv3(conv2(c));
        out = (h + c)/sqrt2 [; out = (out + res2) * s2]
     and, for a down block given ``e_out``, its rate-change conv e_out =
     rate_conv(out) (blocks.py:268-275): fused into the block where ou_block
-    has the stage, else its own launch.
-
-    rng = (lo, hi): block outputs for frames [lo, hi) only (a chunk of the
-    signal; for a down block the rate conv runs over e frames e_rng, or
-    [lo / rate, ceil(hi / rate)) where it is fused).  Returns the h frames [a, b) the chunk reads, which
-    the caller must have produced.  share: the chunk's share of the whole
-    op (rec_block's ops count that fraction of its algorithmic FLOPs and
-    bytes: chunked plans recompute halo frames, which are not counted).
-    after_c1(): recorded as soon as conv1 (cond_out) is done -- right after
-    conv1's launch in the unfused form, after the block in the fused one."""
-    T = h.T
+    has the stage, else its own launch.  after_c1(): recorded as soon as
+    conv1 (cond_out) is done -- right after conv1's launch in the unfused
+    form, after the block in the fused one."""
     c1_out = cond_out if cond_out is not None else tA
-    if rng is None:
-        r1 = r2 = r3 = e_rng = hn = None
-    else:
-        r3 = (max(0, rng[0]), min(T, rng[1]))
-        assert r3[0] < r3[1], rng
-        if e_out is not None:
-            r = bw.rate
-            if bw.fused is not None and bw.down is not None and out.ptr != h.ptr:
-                # the fused rate-change conv covers e frames [lo / rate, ceil(hi / rate))
-                assert r3[0] % r == 0 and (r3[1] % r == 0 or r3[1] == T), ("rate-change range", r3, r)
-                e_rng = (r3[0] // r, -(-r3[1] // r))
-            else:
-                lo_, hi_ = need(bw.rate_conv, e_rng, T)
-                assert r3[0] <= lo_ and hi_ <= r3[1], ("rate-change conv reads past the block range", r3, e_rng)
-        r2 = need(bw.conv3, r3, T)
-        r1 = need(bw.conv2, r2, T)
-        hn = need(bw.conv1, r1, T)
-    d1 = conv_desc(bw.conv1, h, c1_out, res1=sc, s1=NF2, film=film, film_bs=film_bs, rng=r1)
+    d1 = conv_desc(bw.conv1, h, c1_out, res1=sc, s1=NF2, film=film, film_bs=film_bs)
     if skip_tail:
-        add_conv(prog, d1, share)
+        add_conv(prog, d1)
         if after_c1 is not None:
             after_c1()
         return
-    d2 = conv_desc(bw.conv2, c1_out, tB, rng=r2)
-    d3 = conv_desc(bw.conv3, tB, out, res1=h, s1=NF2, res2=res2, s2=s2, rng=r3)
-    d_rc = conv_desc(bw.rate_conv, out, e_out, rng=e_rng) if e_out is not None else None
+    d2 = conv_desc(bw.conv2, c1_out, tB)
+    d3 = conv_desc(bw.conv3, tB, out, res1=h, s1=NF2, res2=res2, s2=s2)
+    d_rc = conv_desc(bw.rate_conv, out, e_out) if e_out is not None else None
     if bw.fused is not None and out.ptr != h.ptr:
         fuse_rc = d_rc is not None and bw.down is not None
         descs = (d1, d2, d3) + ((x_in[4],) if x_in is not None else ()) + ((d_rc,) if fuse_rc else ())
@@ -762,64 +784,63 @@ def rec_block(prog, bw: BlockW, h: Act, out: Act, tA: Act, tB: Act, film=0, film
                         cond_out=cond_out, res2=res2, s2=s2,
                         x_in=x_in[:4] if x_in is not None else None, head=head,
                         e_out=e_out if fuse_rc else None)
-        if rng is not None:
-            # the kernel's internal window: the stored frames, the rate-change
-            # conv's taps and the head's taps, each through the conv chain
-            vin = r3
-            if fuse_rc:
-                vin = span_union(vin, need(bw.rate_conv, e_rng, T))
-            if head is not None:
-                vin = span_union(vin, (max(0, r3[0] - 1), min(T, r3[1] + 1)))   # head conv k3 (score.py:259)
-            hn = need(bw.conv1, need(bw.conv2, need(bw.conv3, vin, T), T), T)
-            bd.f0, bd.f1 = r3
-            bd.h0, bd.h1 = hn
-        prog.add(L.OP_BLOCK, scaled(bd, share))
+        prog.add(L.OP_BLOCK, bd)
         if after_c1 is not None:
             after_c1()
         if d_rc is not None and not fuse_rc:
-            add_conv(prog, d_rc, share)
-        return hn if rng is not None else True
+            add_conv(prog, d_rc)
+        return
     assert x_in is None and head is None, "input / head fusion needs the fused block"
-    add_conv(prog, d1, share)
+    add_conv(prog, d1)
     if after_c1 is not None:
         after_c1()
-    add_conv(prog, d2, share)
-    add_conv(prog, d3, share)
+    add_conv(prog, d2)
+    add_conv(prog, d3)
     if d_rc is not None:
-        add_conv(prog, d_rc, share)
-    return hn
+        add_conv(prog, d_rc)
 
 
-def add_conv(prog, d, share=1.0):
-    """Record an ou_conv; a chunk (conv_desc rng) gets the tile of its whole op."""
-    full = getattr(d, "_full", None)
-    if full is not None and d.tile < 0:
-        if full.tile < 0:
-            full.tile = L.TUNER(full) if L.TUNER is not None else L.load().ou_conv_pick_tile(ctypes.byref(full))
-        d.tile = full.tile
-    prog.add(L.OP_CONV, scaled(d, share))
+def fir_desc(d):
+    """The FIR-applied form (tile bit 17) of an anti-aliased rate-change
+    conv's folded descriptor ``d``: one tap, the unfolded weights and taps
+    of its FirW, the same buffers, geometry and epilogue."""
+    fw = d._fir
+    f = L.ConvDesc.from_buffer_copy(d)
+    f.kt, f.pad, f.tile = 1, 0, -1
+    f.w, f.w_unscale = fw.w.data_ptr(), fw.unscale
+    f.fir, f.fir_taps = fw.mode, fw.taps.data_ptr()
+    f._flops, f._bytes, f._cw, f._w_nat = d._flops, d._bytes, getattr(d, "_cw", None), None
+    return f
 
 
-def need(cw: ConvW, rng, in_len):
-    """Input samples [a, b) (clipped to [0, in_len)) that output frames rng
-    of conv ``cw`` read: frame u reads frame-view frames u - pad .. u - pad +
-    kt - 1 of ``frame`` samples each, from sample ``shift`` on (ou_conv_desc)."""
-    a = (rng[0] - cw.pad) * cw.frame + cw.shift
-    b = (rng[1] - cw.pad + cw.kt - 1) * cw.frame + cw.shift
-    return (max(0, a), min(in_len, b))
+def choose_fir(prog, d):
+    """The form an anti-aliased rate-change conv is recorded in (OUHIP_FIR):
+    with a tuner, the FIR-applied one where its best tile beats the folded
+    form's best tile and, where the conv would read a producer's split image,
+    that link's time too; without one, the FIR-applied form."""
+    mode = fir_mode()
+    if getattr(d, "_fir", None) is None or mode == "0" or d.prec not in (1, 2) or d.f0 or d.xs:
+        return d
+    f = fir_desc(d)
+    tuner = L.TUNER
+    if mode == "1" or not hasattr(tuner, "pick"):
+        return f
+    _, ms_f = tuner.pick(f)
+    _, ms_p = tuner.pick(d)
+    folded = [ms_p]
+    if L.ADD_HOOK is split_hook:
+        link = _split_link(prog, L.OP_CONV, d)
+        if link is not None:
+            _, _, _, rows, batch, per_item, cons = link
+            folded.append(_split_ms(d, per_item, rows, cons[6], batch))
+    folded = [t for t in folded if t is not None]
+    return f if ms_f is not None and (not folded or ms_f < min(folded)) else d
 
 
-def span_union(p, q):
-    return (min(p[0], q[0]), max(p[1], q[1]))
-
-
-def scaled(d, share):
-    """Scale a descriptor's algorithmic FLOP / byte counts (d._flops,
-    d._bytes: the roofline accounting) by ``share``."""
-    if share != 1.0:
-        d._flops = getattr(d, "_flops", 0.0) * share
-        d._bytes = getattr(d, "_bytes", 0.0) * share
-    return d
+def add_conv(prog, d):
+    """Record an ou_conv (an anti-aliased rate-change conv in the form
+    choose_fir picks)."""
+    prog.add(L.OP_CONV, choose_fir(prog, d))
 
 
 def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film_bs=0, cond_out: Act = None,
@@ -889,24 +910,16 @@ def rec_gru_ws_zero(prog, granules):
 
 
 def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, res: Act = None,
-            res_scale=1.0, steps=None, hstate=None, proj_rng=None, share=1.0, xcd=0):
+            res_scale=1.0, xcd=0):
     """Bidirectional GRU layer (input projection + recurrence, gru.py via
-    score.py:117-125).  steps = (t0, t1): only the recurrence steps [t0, t1)
-    of both directions (forward frames t0 .. t1 - 1, backward T - t1 .. T - 1
-    - t0), continuing from / leaving h in ``hstate`` [B][2][H]; the input
-    projection is then the caller's (proj_rng: record it for frames proj_rng
-    only, with no recurrence)."""
+    score.py:117-125)."""
     proj, w_hh, b_hh = gw.layers[layer]
     H = gw.hidden
     assert gi.C == 6 * H and gi.T == x.T and y.C == 2 * H and y.T == x.T and y.B == x.B
     if res is not None:
         assert res.C == 2 * H and res.T == x.T
     assert granules.numel() * 8 >= L.load().ou_gru_workspace_bytes(H, x.B)
-    if proj_rng is not None:
-        add_conv(prog, conv_desc(proj, x, gi, rng=proj_rng), share)
-        return
-    if steps is None:
-        prog.add(L.OP_CONV, conv_desc(proj, x, gi))
+    prog.add(L.OP_CONV, conv_desc(proj, x, gi))
     d = L.GruDesc()
     d.gi, d.gi_bstride = gi.ptr, gi.bs
     d.w_hh, d.b_hh = w_hh.data_ptr(), b_hh.data_ptr()
@@ -917,10 +930,7 @@ def rec_gru(prog, gw: GruW, layer, x: Act, gi: Act, y: Act, granules, status, re
     d.granules, d.status = granules.data_ptr(), status.data_ptr()
     d.flags = GRU_FLAGS if not xcd else (GRU_FLAGS if GRU_FLAGS >= 0 else 0x8000) | ((xcd & 7) << 12)
     d.ws_zeroed = 1 if _GRU_WS_ZEROED else 0
-    if steps is not None:
-        assert hstate is not None and hstate.numel() >= x.B * 2 * H and 0 <= steps[0] < steps[1] <= x.T
-        d.t_begin, d.t_end, d.hstate = steps[0], steps[1], hstate.data_ptr()
-    d._flops = 2.0 * 2 * 3 * H * H * (x.T if steps is None else steps[1] - steps[0]) * x.B
+    d._flops = 2.0 * 2 * 3 * H * H * x.T * x.B
     prog.add(L.OP_GRU, d)
 
 
@@ -981,12 +991,10 @@ class ConvTuner:
 
     @staticmethod
     def geometry(d):
-        # bool(ks_ws): K-slice tiles are only valid with a workspace.  The
-        # batch is the plan's (_TUNE_BATCH while a plan records sub-batches):
-        # a sub-batched plan and the whole-batch one run the same tiles
-        b = _TUNE_BATCH if _TUNE_BATCH is not None else d.batch
+        # bool(ks_ws): K-slice tiles are only valid with a workspace
+        b = d.batch
         return (d.m, d.cin, d.frame, d.kt, d.pad, b, d.rout, bool(d.res1), bool(d.film), bool(d.res2),
-                bool(d.in_scale), d.prec, bool(d.ks_ws), bool(d.xs))
+                bool(d.in_scale), d.prec, bool(d.ks_ws), bool(d.xs), d.fir)
 
     @classmethod
     def key(cls, d):
@@ -1032,7 +1040,9 @@ class ConvTuner:
         # workgroups per CU); elsewhere slices only add traffic
         small = -(-d.n_frames // 64) * -(-d.m // 64) * d.batch <= 1024
         ksl = (0, 1 << 12, 2 << 12, 3 << 12) if d.ks_ws and small else (0,)
-        if d.xs:   # a split-image input: the split-image kernel's shapes only
+        if d.fir:   # the FIR-applied rate-change kernels' shapes only
+            cands = [t | FIR_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | FIR_BIT)]
+        elif d.xs:   # a split-image input: the split-image kernel's shapes only
             cands = [t | L.SS_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | L.SS_BIT)]
         elif d.prec in (1, 2):
             cands = [t | k for t in range(lib.ou_conv_num_tiles()) if lib.ou_conv_tile_ok(d.kt, t | (1 << 11))
@@ -1052,6 +1062,30 @@ class ConvTuner:
         # the timing programs out of the recorder's split-image linking)
         status, d.status = d.status, None
         hook, L.ADD_HOOK = L.ADD_HOOK, None
+        try:
+            best, best_ms = self._time(d, cands, lib, stream, log)
+        finally:   # a candidate that raises leaves the recorder as it was
+            d.tile = -1
+            d.status = status
+            L.ADD_HOOK = hook
+        self.cache[k] = best
+        self.times[k] = best_ms
+        self.by_geom.setdefault(k[:-1], set()).add(k[-1])
+        if os.environ.get("OUHIP_TUNE_VERBOSE", "1") != "0":   # progress (long plan builds)
+            import sys
+
+            print(f"[ou tune] m={d.m} cin={d.cin} frame={d.frame} kt={d.kt} n={d.n_frames} b={d.batch} "
+                  f"rout={d.rout} prec={d.prec} fir={d.fir}: tile 0x{best:x} {best_ms * 1e3:.1f} us "
+                  f"({len(cands)} candidates)", file=sys.stderr, flush=True)
+        self._save()
+        return best
+
+    def _time(self, d, cands, lib, stream, log):
+        """(best tile, its ms per launch) over the candidate tiles of ``d``."""
+        import ctypes
+        import os
+
+        best, best_ms = -1, float("inf")
         for t in cands:
             d.tile = t
             if log:   # diagnostics: name every candidate before it runs
@@ -1096,20 +1130,7 @@ class ConvTuner:
                     ms = min(ms, e0.elapsed_time(e1) / self.reps)
             if ms < best_ms:
                 best, best_ms = t, ms
-        d.tile = -1
-        d.status = status
-        L.ADD_HOOK = hook
-        self.cache[k] = best
-        self.times[k] = best_ms
-        self.by_geom.setdefault(k[:-1], set()).add(k[-1])
-        if os.environ.get("OUHIP_TUNE_VERBOSE", "1") != "0":   # progress (long plan builds)
-            import sys
-
-            print(f"[ou tune] m={d.m} cin={d.cin} frame={d.frame} kt={d.kt} n={d.n_frames} b={d.batch} "
-                  f"rout={d.rout} prec={d.prec}: tile 0x{best:x} {best_ms * 1e3:.1f} us ({len(cands)} candidates)",
-                  file=sys.stderr, flush=True)
-        self._save()
-        return best
+        return best, best_ms
 
 
     def pick(self, d):
@@ -1184,7 +1205,7 @@ class Engine:
             _PREP_PREC, _PREP_STATUS, _PREP_KSWS, _PREP_ENGINE = saved
         enable_autotune(self.device.type == "cuda")
 
-    def widen_ranges(self, flags, step=8):
+    def widen_ranges(self, flags, step=8, consumers=None):
         """A range error's per-layer codes [(slot, code)] (plan.check): widen
         the staging exponent of every operand whose finite values left the
         split-f16 range by 2^step -- the conv's own input (code 1), a fused
@@ -1195,7 +1216,9 @@ class Engine:
         2 / 3 / 4 steps at once, so one rerun fixes what one replay saw.  Returns the
         number of exponents widened; 0 (nothing to widen, or an exponent past
         MAX_SHIFT) means the caller falls back to f32 operands.  Plans must
-        be recorded again: the exponents are read at record time."""
+        be recorded again: the exponents are read at record time.
+        ``consumers``: the failing plan's split-image pairs (producer range
+        word -> consumer operand; Program.split_consumers)."""
         n = 0
         for slot, code in flags:
             if slot < 0 or slot >= len(self.range_owners):
@@ -1208,7 +1231,7 @@ class Engine:
             elif code & 1:
                 targets.append(("c", own, 0))
             if code & (32 if isinstance(own, FusedW) else 2):   # its split image: the consumer's operand
-                cons = _SPLIT_CONSUMERS.get(own.status)
+                cons = (consumers or {}).get(own.status)
                 if cons is None:
                     return 0
                 targets.append(cons)
@@ -1360,7 +1383,7 @@ class Engine:
         self.sdl_b = float(sd[p + ".conv.bias"].reshape(-1)[0])
 
     # -------------------------------------------------------------- buffers
-    def alloc_score(self, B, T, chunked=False):
+    def alloc_score(self, B, T):
         dev = self.device
         Ts = level_lengths(T, self.rates)
         n_lvl = len(self.s_enc)
@@ -1373,15 +1396,6 @@ class Engine:
         H = self.s_gru.hidden
         bufs["GI"] = new_act(B, 6 * H, Ts[len(self.rates)], dev)
         bufs["gran"] = zeros((L.load().ou_gru_workspace_bytes(H, B) // 8,), dtype=torch.int64, device=dev)
-        if chunked:
-            # the chunked pass: GRU state between step segments, and a conv1
-            # temp for the unfused decoder levels below the top (whose E / V
-            # buffers hold the up-conv sum / the skip other chunks still read)
-            bufs["HS"] = empty((B, 2, H), dtype=torch.float32, device=dev)
-            for i in range(n_lvl - 1):
-                if self.s_dec[n_lvl - 1 - i].fused is None:
-                    li = min(i, len(self.rates))
-                    bufs[f"X{i}"] = new_act(B, Cs[li], Ts[li], dev)
         return bufs
 
     def score_levels(self):
@@ -1435,9 +1449,9 @@ class Engine:
             prog.label = f"score dec L{i}"
             if bw.kind == "up":
                 li = min(i, nr)
-                prog.add(L.OP_CONV, conv_desc(bw.rate_conv, h, bufs[f"V{i}"], n_frames=h.T,
-                                              out_len=bufs["T"][li], valid_len=bw.rate * h.T,
-                                              res1=bufs[f"V{i}"], s1=NF2))
+                add_conv(prog, conv_desc(bw.rate_conv, h, bufs[f"V{i}"], n_frames=h.T,
+                                         out_len=bufs["T"][li], valid_len=bw.rate * h.T,
+                                         res1=bufs[f"V{i}"], s1=NF2))
             # only the block's conv1 reads condition l (its input_cond
             # residual): the up conv above runs before the wait
             if before_level is not None:
@@ -1454,214 +1468,6 @@ class Engine:
                     prog.add(L.OP_HEAD, head)
                 return None
         return h
-
-    # ------------------------------------------------- chunked score pass
-    def chunk_plan(self, B, T, force=False):
-        """Split points of the chunked score pass for a (B, T) plan, or None
-        when it does not apply.  The pass cuts the bottleneck GRU (both
-        directions at once) into step segments [0, s1), [s1, s2), [s2, T4)
-        and runs the convs around it in chunks on two side lanes while the
-        recurrence runs on a third: the encoder outside-in (the forward
-        direction consumes frames from the left end, the backward one from
-        the right), the decoder middle-out (frame t has both directions once
-        max(t, T4 - 1 - t) steps are done).  Chunks recompute the convs' halo
-        frames; tiles are pinned to the whole ops', so every chunk computes
-        the bits the unchunked pass computes (tests/test_gpu_chunked.py).
-        Off unless OUHIP_CHUNK=1 or ``force``; OUHIP_CHUNK_SPLIT="f1,f2" sets
-        s1 / T4 and s2 / T4."""
-        import os
-
-        if not force:
-            if os.environ.get("OUHIP_CHUNK", "0") != "1":
-                return None
-            if B > int(os.environ.get("OUHIP_CHUNK_MAX_BATCH", "4")):
-                return None   # wide batches fill the chip without it
-        nr, n_lvl = len(self.rates), len(self.s_enc)
-        Ts = level_lengths(T, self.rates)
-        T4 = Ts[nr]
-        gw = self.s_gru
-        if T4 < 96 or gw.hidden % 64 or (GRU_FLAGS >= 0 and GRU_FLAGS & 32):
-            return None
-        b0, bl = self.s_enc[0], self.s_dec[-1]
-        if not (fuse_ends_enabled() and self.s_in_fusable and b0.fused is not None and b0.C == 32
-                and bl.fused is not None and bl.C == 32):
-            return None
-        if self.conv_prec == 0 or any(bw.conv1.prec == 0 for bw in self.s_enc + self.s_dec):
-            # f32 operands: the rate-change, up and GRU-projection convs (and
-            # unfused blocks) may tune to persistent f32 tiles, which take no
-            # frame offset
-            return None
-        f1, f2 = (float(v) for v in os.environ.get("OUHIP_CHUNK_SPLIT", "0.25,0.7").split(","))
-        h = T4 // 2
-        s1 = max(8, min(h - 8, int(round(f1 * T4))))
-        s2 = max(h + 8, min(T4 - 8, int(round(f2 * T4))))
-        D = math.prod(self.rates)
-        # middle decoder chunks: level-4 frames [m0, m1) = [T4 - s2 + g, s2 - g)
-        # with the smallest margin g whose chunks read only finished GRU frames
-        for g in range(0, s2 - h):
-            m0, m1 = T4 - s2 + g, s2 - g
-            if m1 - m0 < 4:
-                return None
-            q = [self._dec_ranges(T, (m0 * D, h * D))[0], self._dec_ranges(T, (h * D, min(Ts[0], m1 * D)))[0]]
-            if all(T4 - s2 <= a and b <= s2 for a, b in (r["h"] for r in q)):
-                break
-        else:
-            return None
-        return {"T4": T4, "s": (s1, s2), "h": h, "mid": (m0, m1), "D": D}
-
-    def _enc_ranges(self, T, O):
-        """Per encoder level (0 .. top): the block output range, the rate-change
-        output range (down levels) and the h range read, for a chunk that owns
-        bottleneck frames O."""
-        nr, n_lvl = len(self.rates), len(self.s_enc)
-        Ts = level_lengths(T, self.rates)
-        out = [None] * n_lvl
-        req = O   # required output range of the level above (E_{i+1}), or V_top
-        for i in range(n_lvl - 1, -1, -1):
-            bw = self.s_enc[i]
-            Ti = Ts[min(i, nr)]
-            if bw.kind == "down":
-                if bw.fused is not None and bw.down is not None:
-                    r3 = (req[0] * bw.rate, min(Ti, req[1] * bw.rate))
-                    e_rng = (r3[0] // bw.rate, -(-r3[1] // bw.rate))
-                    vin = span_union(r3, need(bw.rate_conv, e_rng, Ti))
-                else:
-                    r3 = need(bw.rate_conv, req, Ti)
-                    e_rng, vin = req, r3
-            else:
-                r3, e_rng, vin = req, None, req
-            hn = need(bw.conv1, need(bw.conv2, need(bw.conv3, vin, Ti), Ti), Ti)
-            out[i] = {"out": r3, "e": e_rng, "h": hn}
-            req = hn
-        return out
-
-    def _dec_ranges(self, T, P):
-        """Per decoder level l (0 = top .. last): the block output range, the
-        up-conv frame range (l >= 1) and the h range read, for a chunk that
-        owns output samples P of the last level (the head's x)."""
-        nr, n_lvl = len(self.rates), len(self.s_enc)
-        Ts = level_lengths(T, self.rates)
-        out = [None] * n_lvl
-        r3 = P
-        for l in range(n_lvl - 1, -1, -1):
-            i = n_lvl - 1 - l
-            bw = self.s_dec[l]
-            Ti = Ts[min(i, nr)]
-            vin = r3
-            if l == n_lvl - 1:   # the fused head's conv (k3) on the block output
-                vin = (max(0, r3[0] - 1), min(Ti, r3[1] + 1))
-            hn = need(bw.conv1, need(bw.conv2, need(bw.conv3, vin, Ti), Ti), Ti)
-            ent = {"out": r3, "h": hn}
-            if bw.kind == "up":
-                # h = skip + up(previous level): frames u of the level above
-                # make samples [u r, u r + r)
-                fr = (hn[0] // bw.rate, -(-hn[1] // bw.rate))
-                ent["up"] = fr
-                r3 = need(bw.rate_conv, fr, Ts[min(i + 1, nr)])
-            out[l] = ent
-        return out
-
-    def rec_score_chunked(self, prog, bufs, x: Act, film_base, film_bs, cp, in_scale=0, sc_list=None,
-                          before_level=None, head=None):
-        """The score network pass (rec_score) as chunks on lanes 2 / 3 around
-        the bottleneck GRU's step segments on lane 0 (chunk_plan).  Starts and
-        ends on lane 0.  before_level(l): as rec_score, called on each lane
-        before the lane's first decoder level l."""
-        n_lvl, nr = len(self.s_enc), len(self.rates)
-        top = n_lvl - 1
-        T = x.T
-        Ts = bufs["T"]
-        T4, (s1, s2), h, (m0, m1), D = cp["T4"], cp["s"], cp["h"], cp["mid"], cp["D"]
-        fb = lambda j: film_base + 4 * self.film_off[j]
-        p = prog
-        ev0 = p.signal()
-        to_lane = lambda l: set_lane(p, l)
-
-        def enc_chunk(O):
-            share = (O[1] - O[0]) / T4
-            rr = self._enc_ranges(T, O)
-            for i in range(n_lvl):
-                bw = self.s_enc[i]
-                x_in = None
-                if i == 0:
-                    d_in = conv_desc(self.s_input, x, bufs["E0"], in_scale=in_scale)
-                    x_in = (x, in_scale, self.s_in_w, self.s_in_b, d_in)
-                got = rec_block(p, bw, bufs[f"E{i}"], bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
-                                film=fb(i), film_bs=film_bs, x_in=x_in,
-                                e_out=bufs[f"E{i+1}"] if bw.kind == "down" else None,
-                                rng=rr[i]["out"], e_rng=rr[i]["e"], share=share)
-                assert i == 0 or got == rr[i]["h"], ("encoder chunk ranges", i, got, rr[i])
-            rec_gru(p, self.s_gru, 0, bufs[f"V{top}"], bufs["GI"], bufs[f"V{top}"], bufs["gran"], self.status,
-                    proj_rng=O, share=share)
-
-        def dec_chunk(P, waits):
-            share = (P[1] - P[0]) / Ts[0]
-            rr = self._dec_ranges(T, P)
-            h_act = None
-            for l in range(n_lvl):
-                i = top - l
-                bw = self.s_dec[l]
-                if waits and before_level is not None:
-                    before_level(l)
-                if bw.kind == "up":
-                    li = min(i, nr)
-                    add_conv(p, conv_desc(bw.rate_conv, h_act, bufs[f"E{i}"], n_frames=h_act.T, out_len=Ts[li],
-                                          valid_len=bw.rate * h_act.T, res1=bufs[f"V{i}"], s1=NF2,
-                                          rng=rr[l]["up"]), share)
-                    hin = bufs[f"E{i}"]
-                else:
-                    hin = bufs[f"V{i}"]
-                last = l == n_lvl - 1
-                tA = bufs[f"E{i}"] if i == top else bufs.get(f"X{i}", bufs[f"A{i}"])
-                got = rec_block(p, bw, hin, bufs[f"A{i}"], tA, bufs[f"B{i}"], film=fb(n_lvl + l), film_bs=film_bs,
-                                sc=sc_list[l], head=head if last else None, rng=rr[l]["out"], share=share)
-                assert got == rr[l]["h"], ("decoder chunk ranges", l, got, rr[l])
-                h_act = bufs[f"A{i}"]
-
-        gru = lambda st: rec_gru(p, self.s_gru, 0, bufs[f"V{top}"], bufs["GI"], bufs[f"V{top}"], bufs["gran"],
-                                 self.status, res=bufs[f"V{top}"], res_scale=NF2, steps=st, hstate=bufs["HS"])
-        # recorded in the order the work should run (the hipGraph executor
-        # launches nodes in capture order): outer encoder chunks, segment 1,
-        # inner chunks, segment 2, middle decoder chunks, segment 3, outer
-        # decoder chunks.  Every cross-lane edge goes through lane 0, which
-        # runs the recurrence: side lanes that wait on each other crash the
-        # HIP runtime's stream capture.
-        T0 = Ts[0]
-        L_, R_ = 2, 3
-        ev = {}
-        for lane, O in ((L_, (0, s1)), (R_, (T4 - s1, T4))):
-            to_lane(lane)
-            p.wait(ev0)
-            enc_chunk(O)
-            ev[lane, 1] = p.signal()
-        to_lane(0)
-        p.wait(ev[L_, 1])
-        p.wait(ev[R_, 1])
-        gru((0, s1))
-        for lane, O in ((L_, (s1, h)), (R_, (h, T4 - s1))):
-            to_lane(lane)
-            enc_chunk(O)
-            ev[lane, 2] = p.signal()
-        to_lane(0)
-        p.wait(ev[L_, 2])
-        p.wait(ev[R_, 2])
-        gru((s1, s2))
-        g2 = p.signal()
-        for lane, P in ((L_, (m0 * D, h * D)), (R_, (h * D, min(T0, m1 * D)))):
-            to_lane(lane)
-            p.wait(g2)
-            dec_chunk(P, True)
-        to_lane(0)
-        gru((s2, T4))
-        g3 = p.signal()
-        for lane, P in ((L_, (0, m0 * D)), (R_, (min(T0, m1 * D), T0))):
-            to_lane(lane)
-            p.wait(g3)
-            dec_chunk(P, False)
-            ev[lane, 3] = p.signal()
-        to_lane(0)
-        p.wait(ev[L_, 3])
-        p.wait(ev[R_, 3])
 
     def rec_sc(self, prog, conds, scs):
         for l, (c, s) in enumerate(zip(conds, scs)):

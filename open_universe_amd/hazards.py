@@ -15,9 +15,8 @@ strided boxes: base + item * bstride + row * cstride + [t0, t1) bytes.  Two
 boxes overlap iff some (item, row, byte) of one equals one of the other,
 which is decided exactly per item offset (no layout assumptions).  Weights,
 biases and other recorded constants are never written during a replay and
-are left out.  The opt-in chunked score pass is outside what this check can
-judge: its two conv lanes recompute each other's halo frames, overlapping
-writes of identical bits by construction."""
+are left out.  Every plan schedule the package records is checked
+(tests/test_hazards.py)."""
 from dataclasses import dataclass
 
 from . import _lib as L

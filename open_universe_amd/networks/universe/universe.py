@@ -366,7 +366,7 @@ class Universe(nn.Module):
             plan = self._arena_plan(key, slot, lambda ar: EnhancePlan(eng, B, T, int(n_steps), float(epsilon),
                                                                       keep_rms=bool(keep_rms),
                                                                       diff=dict(self.diff_kwargs), slot=slot,
-                                                                      arena=ar, st_lane=False, chunk=False))
+                                                                      arena=ar, st_lane=False))
             self._inflight.add(key)
             if pre_noise is not None:
                 pre_noise(i)
@@ -424,7 +424,8 @@ class Universe(nn.Module):
                 print(f"[ou range] round {self.range_widenings + 1}: "
                       + " ".join(f"{type(eng.range_owners[s]).__name__}#{s}:{c:#x}" for s, c in err.flags),
                       file=sys.stderr, flush=True)
-            if eng is None or not getattr(err, "flags", ()) or not eng.widen_ranges(err.flags):
+            if (eng is None or not getattr(err, "flags", ())
+                    or not eng.widen_ranges(err.flags, consumers=getattr(err, "consumers", None))):
                 break
             self.range_widenings += 1
             self._plans = collections.OrderedDict()   # exponents are read at record time

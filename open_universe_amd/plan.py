@@ -124,6 +124,7 @@ class _PlanBase:
             e = L.OuRangeError("split-f16 operand out of range (range codes %s%s)"
                                % (per_layer[:8], ", shared word %d" % flags[1] if flags[1] else ""))
             e.flags = per_layer if not flags[1] else []   # a shared-word flag names no layer
+            e.consumers = dict(self.prog.__dict__.get("split_consumers", {}))   # this plan's split-image pairs
             raise e
 
 
@@ -132,7 +133,7 @@ class EnhancePlan(_PlanBase):
 
     def __init__(self, eng, batch, mix_len, n_steps, epsilon, keep_rms=False,
                  use_aux_signal=False, warm_start=None, diff=None, ensemble=None,
-                 ensemble_mode=None, slot=0, arena=None, st_lane=True, chunk=None):
+                 ensemble_mode=None, slot=0, arena=None, st_lane=True):
         # arena: record every buffer into this Arena (engine.Arena; the caller
         # owns it and retries with a bigger one on ArenaFull)
         if arena is not None:
@@ -151,7 +152,6 @@ class EnhancePlan(_PlanBase):
         Tp = mix_len + self.pad
         self.Tp = Tp
         self.use_aux = use_aux_signal
-        self.chunks = None
         self.warm = warm_start
         diff = diff or eng.cfg["diffusion"]
         # sampler constants (universe.py:301-305)
@@ -198,11 +198,6 @@ class EnhancePlan(_PlanBase):
         # lane 0 waits for them right before the first decoder.  Not with the
         # aux / warm-start paths, whose initial sample needs the conditioner.
         self.overlap = E.overlap_enabled() and not use_aux_signal and warm_start is None
-        # the chunked score pass (Engine.chunk_plan): its chunks keep the whole
-        # ops' tiles, so a chunked plan records no split-image links at all
-        chunks = eng.chunk_plan(B, Tp, force=chunk is True) if chunk is not False and not use_aux_signal else None
-        if chunks is not None:
-            L.ADD_HOOK = None
         ev_cond = {}
         after_level = None
         if self.overlap:
@@ -216,11 +211,10 @@ class EnhancePlan(_PlanBase):
 
             # the projections run on their own lane (E.SC_LANE), so the
             # conditioner's next decoder level does not queue behind them --
-            # not in a chunked plan, whose conv chunks use that lane (the HIP
-            # runtime's capture crashed on the extra side-lane edges), nor in
-            # enhance_many's (st_lane=False): the side-lane streams are
-            # process-wide, and two plans in flight would serialise on it
-            sc_lane = chunks is None and st_lane
+            # not in enhance_many's plans (st_lane=False): the side-lane
+            # streams are process-wide, and two plans in flight would
+            # serialise on it
+            sc_lane = st_lane
 
             def after_level(l, cond):
                 if sc_lane:
@@ -242,7 +236,7 @@ class EnhancePlan(_PlanBase):
             else:
                 raise NotImplementedError("aux signal without a signal-decoupling layer")
         # lane 1's last signal (the sc lane took the conditions'): lane 0 joins it before finish
-        ev_c1 = p.signal() if self.overlap and chunks is None and st_lane else None
+        ev_c1 = p.signal() if self.overlap and st_lane else None
         if use_aux_signal:
             x_final = self.SIG
         else:
@@ -276,25 +270,8 @@ class EnhancePlan(_PlanBase):
                     c.update(c_score=f32(s_now * s_now))
                 coefs.append(c)
             self.WIN = torch.from_numpy(win).to(dev)
-            # the chunked score pass (Engine.chunk_plan): GRU segments on lane
-            # 0, conv chunks on side lanes 2 / 3 (rec_score_chunked)
-            self.chunks = chunks
-            # small batches: the score network as two sub-batches on lanes 0
-            # and E.SUB_LANE (E.score_sub_batches), the second half's first
-            # step starting behind the first half's encoder, so one half's
-            # GRU chain runs beside the other half's convolutions
-            subs = E.score_sub_batches(B) if chunks is None else None
-            self.subs = subs
-            if subs is None:
-                sbs = [eng.alloc_score(B, Tp, chunked=self.chunks is not None)]
-            else:
-                sbs = [eng.alloc_score(b1 - b0, Tp) for b0, b1 in subs]
-            # the plan owns every buffer its program points at: the second
-            # sub-batch's buffers too (freed, the caching allocator would hand
-            # their memory to the next tensor while the program still used it)
-            self.sb, self.score_bufs = sbs[0], sbs
-            for sb in sbs:
-                E.rec_gru_ws_zero(p, sb["gran"])   # lane 0, ahead of the first score GRU
+            self.sb = eng.alloc_score(B, Tp)
+            E.rec_gru_ws_zero(p, self.sb["gran"])   # lane 0, ahead of the first score GRU
             # initial sample (universe.py:322-331)
             if warm_start is None:
                 p.add(L.OP_SCALE, L.ScaleArgs(z=self.NZ.data_ptr(), y=self.X.ptr, n=B * Tp,
@@ -304,54 +281,17 @@ class EnhancePlan(_PlanBase):
                                               scale=float(sig[n_start]), add=self.SIG.ptr))
             film_base = self.FILM.data_ptr()
             zi = 1
-            ev_sub = []
-            saved_tb = E._TUNE_BATCH
-            if subs is not None:
-                E._TUNE_BATCH = B   # the sub-batches run the whole batch's tiles
-            try:
-                for n in steps:
-                    join = (lambda l: p.wait(ev_cond[l])) if (ev_cond and n == steps[0]) else None
-                    last = n == n_steps - 1
-                    film = film_base + 4 * n * eng.film_rows
-                    if self.chunks is not None:
-                        in_scale = self.WIN[n].data_ptr() if edm is not None else 0
-                        head = eng.head_desc(None, self.X.ptr, B, Tp, mode=2 if last else 1, x_ptr=self.X.ptr,
-                                             z_ptr=0 if last else self.NZ[zi].data_ptr(), coef=coefs[n])
-                        eng.rec_score_chunked(p, self.sb, self.X, film, 0, self.chunks,
-                                              in_scale=in_scale, sc_list=self.SC, before_level=join, head=head)
-                    for k, (b0, b1) in enumerate(subs or [(0, B)] if self.chunks is None else []):
-                        whole = subs is None
-                        xk = self.X if whole else Act(self.X.t[b0:b1])
-                        in_scale = self.WIN[n, b0:].data_ptr() if edm is not None else 0
-                        head = eng.head_desc(None, xk.ptr, b1 - b0, Tp, mode=2 if last else 1, x_ptr=xk.ptr,
-                                             z_ptr=0 if last else self.NZ[zi, b0].data_ptr(), coef=coefs[n])
-                        sc = self.SC if whole else [Act(a.t[b0:b1]) for a in self.SC]
-                        after = None
-                        if k == 1:
-                            E.set_lane(p, E.SUB_LANE)
-                            if n == steps[0]:
-                                p.wait(ev_sub[0])   # behind the first half's first encoder
-                        elif not whole and n == steps[0]:
-                            after = lambda: ev_sub.append(p.signal())
-                        eng.rec_score(p, sbs[k], xk, film, 0, in_scale=in_scale, sc_list=sc, before_level=join,
-                                      head=head, after_encoder=after, gru_xcd=4 * k)
-                        if k == 1:
-                            E.set_lane(p, 0)
-                    zi += 0 if last else 1
-            finally:
-                E._TUNE_BATCH = saved_tb
-            if subs is not None:   # lane 0 joins the second half
-                E.set_lane(p, E.SUB_LANE)
-                ev_end = p.signal()
-                E.set_lane(p, 0)
-                p.wait(ev_end)
+            for n in steps:
+                join = (lambda l: p.wait(ev_cond[l])) if (ev_cond and n == steps[0]) else None
+                last = n == n_steps - 1
+                film = film_base + 4 * n * eng.film_rows
+                in_scale = self.WIN[n].data_ptr() if edm is not None else 0
+                head = eng.head_desc(None, self.X.ptr, B, Tp, mode=2 if last else 1, x_ptr=self.X.ptr,
+                                     z_ptr=0 if last else self.NZ[zi].data_ptr(), coef=coefs[n])
+                eng.rec_score(p, self.sb, self.X, film, 0, in_scale=in_scale, sc_list=self.SC, before_level=join,
+                              head=head)
+                zi += 0 if last else 1
             x_final = self.X
-            if self.chunks is not None and ev_cond:
-                # the side lanes waited on the conditions; lane 0 joins lane 1
-                # through its last signal only (every event a stream waits on
-                # before its next node adds an edge to that node, and a capture
-                # whose node took 9 crashed in the HIP runtime)
-                p.wait(max(ev_cond.values()))
         if ev_c1 is not None:
             p.wait(ev_c1)   # long done: the conditions were waited on in the first step
         p.label = "finish"

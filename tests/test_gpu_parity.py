@@ -50,10 +50,13 @@ def _dev(a):
 
 
 # ----------------------------------------------------------------- layers
-def _run_conv(cw, x, out_shape, **kw):
+def _run_conv(cw, x, out_shape, form="folded", **kw):
     xa = E.Act(x.to(DEV).contiguous())
     y = E.new_act(*out_shape, DEV)
     d = E.conv_desc(cw, xa, y, **kw)
+    if form == "fir":   # the FIR-applied kernels (tile bit 17) instead of the folded weights
+        assert cw.fir is not None
+        d = E.fir_desc(d)
     L.run_now(L.OP_CONV, d, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     return y.t.cpu()
@@ -73,8 +76,9 @@ def test_same_conv_layer(pp16, lvl, T, conv, k):
     assert rel_rms(y, ref) < 1e-5
 
 
+@pytest.mark.parametrize("form", ["folded", "fir"])
 @pytest.mark.parametrize("lvl,r", [(0, 2), (1, 4), (3, 5)])
-def test_down_conv_layer(pp16, lvl, r):
+def test_down_conv_layer(pp16, lvl, r, form):
     d, cfg, m = pp16
     sd = {kk: v.cpu() for kk, v in m.state_dict().items()}
     p = f"_edm_model.encoder.ds_modules.{lvl}.rate_change_conv"
@@ -83,13 +87,14 @@ def test_down_conv_layer(pp16, lvl, r):
     x = torch.randn(2, C, T, generator=torch.Generator().manual_seed(7))
     cw = E.prep_down(sd, p, r, True, DEV)
     U = -(-T // r)
-    y = _run_conv(cw, x, (2, 2 * C, U))
+    y = _run_conv(cw, x, (2, 2 * C, U), form=form)
     ref = O.prelu_conv(sd, p, x, r, stride=r, antialias=True)
     assert rel_rms(y, ref) < 1e-5
 
 
+@pytest.mark.parametrize("form", ["folded", "fir"])
 @pytest.mark.parametrize("lvl,r", [(1, 5), (2, 4), (4, 2)])
-def test_up_conv_layer(pp16, lvl, r):
+def test_up_conv_layer(pp16, lvl, r, form):
     d, cfg, m = pp16
     sd = {kk: v.cpu() for kk, v in m.state_dict().items()}
     p = f"_edm_model.decoder.up_modules.{lvl}.rate_change_conv"
@@ -99,7 +104,7 @@ def test_up_conv_layer(pp16, lvl, r):
     res = torch.randn(1, Cin // 2, r * Tin, generator=torch.Generator().manual_seed(4))
     cw = E.prep_up(sd, p, r, True, DEV)
     resa = E.Act(res.to(DEV))
-    y = _run_conv(cw, x, (1, Cin // 2, r * Tin), n_frames=Tin, valid_len=r * Tin, res1=resa,
+    y = _run_conv(cw, x, (1, Cin // 2, r * Tin), form=form, n_frames=Tin, valid_len=r * Tin, res1=resa,
                   s1=float(E.NF2))
     ref = (O.prelu_conv(sd, p, x, r, stride=r, transpose=True, antialias=True) + res) * E.NF2
     assert rel_rms(y, ref) < 1e-5

@@ -254,6 +254,27 @@ def test_c4_real_shape_damped_split_f16_item0_vs_oracle():
     assert rel_rms(out[1:2], out[:1]) > 0.1
 
 
+def test_c4_real_shape_undamped_split_f16_item0_vs_oracle():
+    """BASELINE configs[3] at its real shape on the UNDAMPED synthetic PP24
+    weights (the bench's --undamped line): batch 32, 10 s clips.  The range
+    flags widen the staging exponents of the layers that overflow (at most
+    three reruns of the same noise), the batch stays on split-f16 operands,
+    and item 0 matches the fp32 oracle on the same noise slice."""
+    cfg, m = _synth_model("pp24", 0)
+    mix = _clips(32, 10.0, cfg["fs"], base=31)
+    with torch.no_grad():
+        out = m.enhance(mix.to(DEV), rng=torch.Generator().manual_seed(2024)).cpu()
+        eng = m._get_engine()
+        assert eng.conv_prec == 1 and m.range_fallbacks == 0 and m.range_widenings <= 3
+        assert int(eng.status.abs().sum()) == 0
+        assert out.shape == (32, 240000) and torch.isfinite(out).all()
+        nz = next(iter(m._plans.values())).NZ.cpu()   # (draws, 32, 1, Tp): the noise the GPU used
+        it = iter(range(nz.shape[0]))
+        ref = _oracle(m, cfg).enhance(mix[:1], noise_fn=lambda shp: nz[next(it), :1].reshape(shp))
+    assert rel_rms(out[:1], ref) < 1e-3 and si_sdr(out[:1], ref) > 60
+    assert rel_rms(out[1:2], out[:1]) > 0.1
+
+
 def test_c3_real_shape_item0_vs_oracle():
     """BASELINE configs[2] at its benched geometry: ORIG16 full width, batch 8,
     8 s clips, 60 diffusion steps (universe.py:301-343 with n_steps=60), split-
@@ -314,8 +335,14 @@ def test_c3_shape_enhance_vs_oracle():
 
 def test_c4_shape_enhance_vs_oracle():
     """BASELINE configs[3]: PP24 full width (GRU H = 384), batch 4, 0.5 s
-    clips, f32 operands (the synthetic weights leave the split range)."""
+    clips, on the undamped synthetic weights, against the fp32 oracle on the
+    same noise.  Their activations leave the split-f16 range at the default
+    2^-6 staging exponent: the flagged layers' exponents widen (at most three
+    reruns) and the result is still computed on split-f16 operands, with no
+    f32 fallback."""
     m, out, ref = _vs_oracle("pp24", 4, 0.5)
+    assert m._get_engine().conv_prec == 1 and m.range_fallbacks == 0
+    assert m.range_widenings <= 3
     assert out.shape == ref.shape == (4, 12000)
     assert rel_rms(out, ref) < 1e-3 and si_sdr(out, ref) > 60
 

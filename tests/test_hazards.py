@@ -85,9 +85,8 @@ def _check(plan):
 
 
 @pytest.mark.parametrize("tag", ["pp16_c4", "orig16_c4", "pp24_c4", "pp16"])
-@pytest.mark.parametrize("B,sub", [(1, "0"), (2, "0"), (2, "1"), (3, "1")])
-def test_enhance_plans_are_race_free(engines, tag, B, sub, monkeypatch):
-    monkeypatch.setenv("OUHIP_SUB_BATCH", sub)
+@pytest.mark.parametrize("B", [1, 2, 3])
+def test_enhance_plans_are_race_free(engines, tag, B):
     T = 16000 if tag == "pp16" else 4000
     _check(EnhancePlan(engines[tag], B, T, 8, 1.3))
 
@@ -95,18 +94,16 @@ def test_enhance_plans_are_race_free(engines, tag, B, sub, monkeypatch):
 @pytest.mark.parametrize("opts", [{"keep_rms": True}, {"use_aux_signal": True}, {"warm_start": 3},
                                   {"ensemble": 2, "ensemble_mode": 1}, {"st_lane": False}])
 def test_enhance_plan_options_are_race_free(engines, opts):
-    """(Not the opt-in chunked pass: its two conv lanes recompute each
-    other's halo frames -- overlapping writes of identical bits, by
-    construction, which a footprint check cannot tell from a race.)"""
     B = 2 * opts.get("ensemble", 1)
     _check(EnhancePlan(engines["pp16"], B, 16000, 8, 1.3, **opts))
 
 
-@pytest.mark.parametrize("env", [{"OUHIP_OVERLAP": "0"}, {"OUHIP_SPLIT_IMAGES": "0"}, {"OUHIP_SUB_BATCH": "1"}])
+@pytest.mark.parametrize("env", [{"OUHIP_OVERLAP": "0"}, {"OUHIP_SPLIT_IMAGES": "0"}, {"OUHIP_FIR": "1"},
+                                 {"OUHIP_FIR": "0"}])
 def test_enhance_plan_schedules_are_race_free(engines, env, monkeypatch):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    _check(EnhancePlan(engines["pp16_c4"], 4 if env.get("OUHIP_SUB_BATCH") else 2, 4000, 8, 1.3))
+    _check(EnhancePlan(engines["pp16_c4"], 2, 4000, 8, 1.3))
 
 
 def test_network_plans_are_race_free(engines):

@@ -123,39 +123,3 @@ def test_split_images_off_records_plain_convs(monkeypatch):
     eng = Engine(get_config("pp16"), golden_state_dict(d), "cpu", _record_only=True)
     plan = EnhancePlan(eng, 1, 16000, 8, 1.3)
     assert not getattr(plan.prog, "split_links", [])
-
-
-@pytest.mark.parametrize("B,subs", [(1, None), (2, [(0, 1), (1, 2)]), (3, [(0, 2), (2, 3)]),
-                                    (4, [(0, 2), (2, 4)]), (8, [(0, 4), (4, 8)])])
-def test_small_batches_record_two_score_sub_batches(B, subs, monkeypatch):
-    """OUHIP_SUB_BATCH=1: the score network as two sub-batches, the second on
-    its own lane (engine.SUB_LANE) behind the first half's first encoder; the
-    lane schedule validates and every score op is recorded once per half."""
-    from open_universe_amd import engine as E
-
-    monkeypatch.setenv("OUHIP_SUB_BATCH", "1")
-
-    d = load_golden("pp16_c4")
-    eng = Engine(get_config("pp16", 4), golden_state_dict(d), "cpu", _record_only=True)
-    plan = EnhancePlan(eng, B, 3000, 8, 1.3)
-    assert plan.subs == subs
-    assert L.load().ou_program_validate(plan.prog.h) == 0
-    lanes = {}
-    for k, lane in zip(plan.prog.op_kinds(), plan.prog.lanes):
-        if k == L.OP_GRU:
-            lanes[lane] = lanes.get(lane, 0) + 1
-    if subs is None:
-        assert E.SUB_LANE not in lanes
-    else:   # 8 score GRUs per half; the conditioner's two on lane 1
-        assert lanes[0] == 8 and lanes[E.SUB_LANE] == 8 and lanes[1] == 2
-
-
-def test_sub_batch_switch(monkeypatch):
-    from open_universe_amd import engine as E
-
-    monkeypatch.delenv("OUHIP_SUB_BATCH", raising=False)
-    assert E.score_sub_batches(4) is None   # opt-in
-    monkeypatch.setenv("OUHIP_SUB_BATCH", "0")
-    assert E.score_sub_batches(4) is None
-    monkeypatch.setenv("OUHIP_SUB_BATCH", "1")
-    assert E.score_sub_batches(16) == [(0, 8), (8, 16)] and E.score_sub_batches(1) is None

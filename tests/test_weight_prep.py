@@ -232,3 +232,78 @@ def test_numpy_natural_split_packing_matches_c(m, cin, kt):
     assert ua == ub and a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
     c, uc = L.conv_pack_split_np(w)
     assert uc == ua and np.array_equal(np.sort(a.view(np.uint16)), np.sort(c.view(np.uint16)))
+
+
+def emulate_fir(spec, x, n_frames, out_len, valid_len=None):
+    """The FIR-applied form (ou_conv_desc.fir, include/ouhip.h) from its
+    unfolded weights in the kernels' K / row order, float64."""
+    mode, r, wu, taps = spec.fir
+    x = torch.where(x.double() >= 0, x.double(), x.double() * spec.slope)
+    B, Cin, T = x.shape
+    t = torch.from_numpy(np.asarray(taps, np.float64))
+    fir = lambda v: F.conv1d(v, t[None, None].expand(v.shape[1], 1, -1), padding="same", groups=v.shape[1])
+    wu = torch.from_numpy(np.asarray(wu, np.float64))
+    if mode == 1:   # k = (cb r + ph) 16 + c for ci = 16 cb + c
+        f = fir(F.pad(x, (0, n_frames * r - T)))
+        bv = f.reshape(B, Cin // 16, 16, n_frames, r).permute(0, 1, 4, 2, 3).reshape(B, Cin * r, n_frames)
+        y = torch.einsum("mk,bku->bmu", wu, bv)
+    else:           # row 32 (co // P) + (co % P) r + ph
+        P = 32 // r
+        z = torch.einsum("mk,bku->bmu", wu, x)
+        cout = spec.w.shape[0] // r
+        co = torch.arange(cout)
+        rows = 32 * (co // P) + (co % P) * r
+        pre = torch.stack([z[:, rows + ph] for ph in range(r)], -1)   # (B, cout, U, r)
+        y = fir(pre.reshape(B, cout, n_frames * r))
+    if spec.bias is not None:
+        y = y + torch.from_numpy(np.asarray(spec.bias, np.float64))[None, :, None]
+    if valid_len is not None and valid_len < y.shape[-1]:
+        y[..., valid_len:] = 0
+    if y.shape[-1] < out_len:
+        y = F.pad(y, (0, out_len - y.shape[-1]))
+    return y[..., :out_len]
+
+
+def _sd_rc(direction, cin, cout, r, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    shape = (cout, cin, r) if direction == "down" else (cin, cout, r)
+    return {"p.conv.weight": torch.randn(shape, generator=g, dtype=torch.float64),
+            "p.prelu.weight": torch.tensor([0.25], dtype=torch.float64),
+            "p.bias": torch.randn(cout, generator=g, dtype=torch.float64)}
+
+
+@pytest.mark.parametrize("r", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("T", [40, 43])
+def test_fir_form_down_matches_folded(r, T):
+    """The unfolded K order of the FIR-applied down conv computes what the
+    folded 3-frame weights do (both = PReLU -> FIR -> strided conv)."""
+    sd = _sd_rc("down", 32, 48, r, seed=r)
+    spec = E.spec_down(sd, "p", r, True)
+    assert spec.fir is not None and spec.fir[0] == 1
+    x = _x(2, 32, T, seed=r)
+    U = -(-T // r)
+    torch.testing.assert_close(emulate_fir(spec, x, U, U), emulate(spec, x, U, U), rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("r", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("extra_len", [0, -3])
+def test_fir_form_up_matches_folded(r, extra_len):
+    """The padded whole-channel row order of the FIR-applied up conv
+    (32 // r channels per 32-row m-tile) computes what the folded weights do."""
+    sd = _sd_rc("up", 64, 40, r, seed=r)
+    spec = E.spec_up(sd, "p", r, True)
+    assert spec.fir is not None and spec.fir[0] == 2
+    x = _x(2, 64, 13, seed=r)
+    length = r * 13 + extra_len
+    torch.testing.assert_close(emulate_fir(spec, x, 13, length, valid_len=r * 13),
+                               emulate(spec, x, 13, length, valid_len=r * 13), rtol=1e-9, atol=1e-9)
+
+
+def test_fir_form_only_where_the_kernels_apply():
+    """No FIR form where the FIR kernels do not run: channel counts off the
+    16 / 32 grid, rates outside 2 / 3 / 4 / 5 / 8, no anti-aliasing."""
+    assert E.spec_down(_sd_rc("down", 24, 48, 2), "p", 2, True).fir is None
+    assert E.spec_down(_sd_rc("down", 32, 64, 6), "p", 6, True).fir is None
+    assert E.spec_down(_sd_rc("down", 32, 64, 2), "p", 2, False).fir is None
+    assert E.spec_up(_sd_rc("up", 48, 24, 2), "p", 2, True).fir is None
+    assert E.spec_up(_sd_rc("up", 64, 32, 2), "p", 2, False).fir is None

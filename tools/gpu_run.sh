@@ -10,15 +10,14 @@
 #   bench:CFG        bench.py --config CFG, default arguments (the driver's line)
 #   benchpmc:CFG     profile:CFG, then bench:CFG quoting `traffic` from that PMC summary
 #   shards           C4 at the per-rank batches of 2/4/8 GPUs (B = 16, 8, 4)
-#   subbatch[:B]     C4 at per-rank batch B (default 4), score sub-batches off / on, alternating
 #   c4u              C4 on the undamped synthetic weights (exponents widen in the warm-up)
 #   critical         tools/critical_path.py --config c2 (lane timeline, first step)
-#   chunk:CFG        whole pass vs chunked pass (OUHIP_CHUNK=0/1) at CFG
 #   ab:VAR=[A,]B     C2 bench with VAR=A / B / A / B (A defaults to 0; same box, alternating)
 #   ablib:NAME       C2 bench, in-tree libouhip.so vs variants/libouhip_NAME.so (3 pairs)
 #   convlib:NAME     tools/conv_bench.py deep-level layers, in-tree library vs the variant
 #   convsplit[:L,..] tools/conv_bench.py --split: the split-image kernel on the deep-level layers
 #   convsplitlib:A,B the same on the k3 layers, in-tree library then variants A, B (stamps: --sstamps)
+#   fir:CFG          tools/fir_bench.py: folded vs FIR-applied rate-change convs at CFG
 #
 #   e.g. tools/gpu_run.sh r04k profile:c2 critical bench:c1 bench:c3 bench:c5
 set -o pipefail
@@ -64,23 +63,10 @@ for step in "$@"; do
     c4u)
         OUHIP_TUNE_CACHE="$O/tune_${TAG}_c4.json" bench "$O/bench_${TAG}_config_c4_undamped" 900 --config c4 \
             --undamped --steps 3 --warmup 2 --no-f32-pass --no-cpu-baseline || exit 1 ;;
-    subbatch)
-        for i in 1 2; do
-            for v in 0 1; do
-                OUHIP_SUB_BATCH=$v OUHIP_TUNE_CACHE="$O/tune_${TAG}_c4.json" bench "$O/bench_${TAG}_c4_b${arg:-4}_sub${v}_$i" \
-                    300 --config c4 --batch "${arg:-4}" --steps 3 --warmup 1 --no-f32-pass --no-cpu-baseline \
-                    --traffic-json "" || exit 1
-            done
-        done ;;
     critical)
         OUHIP_TUNE_CACHE="$O/tune_${TAG}_c2.json" timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 \
             --ops --out "$O/cp_$TAG.json" > "$O/cp_$TAG.txt" 2>&1 || { tail -20 "$O/cp_$TAG.txt"; exit 1; }
         grep -v "ou tune\|amdgpu" "$O/cp_$TAG.txt" | grep -B2 -A1 "first step" ;;
-    chunk)
-        for c in 0 1; do
-            OUHIP_CHUNK=$c OUHIP_TUNE_CACHE="$O/tune_${TAG}_$arg.json" bench "$O/bench_${TAG}_${arg}_chunk$c" 300 \
-                --config "$arg" --steps 5 --warmup 2 --no-cpu-baseline || exit 1
-        done ;;
     ab)
         var=${arg%%=*}; val=${arg#*=}; base=0
         [[ "$val" == *,* ]] && { base=${val%%,*}; val=${val#*,}; }
@@ -112,6 +98,11 @@ for step in "$@"; do
                   > "$O/cbs_${TAG}_$lib.txt" 2>&1 ) || { tail -20 "$O/cbs_${TAG}_$lib.txt"; exit 1; }
             echo "## $lib"; grep -v amdgpu "$O/cbs_${TAG}_$lib.txt" | grep -v "^L\|^U\|^D\|^G" | cut -c1-200
         done ;;
+    fir)   # tools/fir_bench.py: folded vs FIR-applied rate-change convs at config ARG (c4: FIR form only)
+        fo=1; [ "${arg:-c4}" = c4 ] && fo=0
+        timeout -k 10 400 python3 tools/fir_bench.py --config "${arg:-c4}" --folded $fo > "$O/fir_${TAG}_${arg:-c4}.txt" 2>&1 \
+            || { tail -20 "$O/fir_${TAG}_${arg:-c4}.txt"; exit 1; }
+        grep -v "ou tune\|amdgpu" "$O/fir_${TAG}_${arg:-c4}.txt" ;;
     convlib)   # tools/conv_bench.py on the deep-level layers: in-tree library vs variant ARG
         for lib in main "$arg"; do
             ( [ "$lib" = main ] || export OUHIP_LIB="$ROOT/open_universe_amd/variants/libouhip_$lib.so"

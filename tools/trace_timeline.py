@@ -2,8 +2,7 @@
 """Timeline of the last enhance in a rocprofv3 ``*_kernel_trace.csv``: the
 GRU launches (their durations and the gaps between them -- the conv work on
 the critical path) and, between GRU launches, how much conv time ran on each
-hardware queue.  For the chunked score pass (three GRU segments per
-diffusion step) and the unchunked one alike.
+hardware queue.
 
     python tools/trace_timeline.py KERNEL_TRACE_CSV --gru-per-enhance N
 """
