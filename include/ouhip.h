@@ -144,9 +144,13 @@ typedef struct ou_conv_desc {
      *          strided conv over f's frame view: frame = R, rout 1, K = cin R;
      *   fir 2: the transposed conv (frame 1, rout = -R, K = cin), then the FIR
      *          over its R * in_len output samples (zero outside), then bias.
-     * R is 2, 3, 4, 5 or 8; kt 1, pad 0, shift 0, no in_scale, no xs; prec 1
-     * or 2; weights w_logical[m'][k] packed by ou_conv_pack_split_nat(kt 1):
-     *   fir 1: m' = co (m = cout rows),
+     *   fir 3: no FIR: a plain strided conv (frame = R any multiple of 4,
+     *          rout 1, K = cin R; the st_convs, condition.py:53-59) in fir 1's
+     *          K order, walked so that each input sample is read once;
+     * R is 2, 3, 4, 5 or 8 (fir 1 / 2); kt 1, pad 0, shift 0, no in_scale, no
+     * xs; prec 1 or 2; weights w_logical[m'][k] packed by
+     * ou_conv_pack_split_nat(kt 1):
+     *   fir 1, 3: m' = co (m = cout rows),
      *          k = (cb R + ph) 16 + c  for input channel ci = 16 cb + c
      *          (cin % 16 == 0) and conv tap ph;
      *   fir 2: every 32-row m-tile holds P = 32 / R whole channels, row
@@ -155,7 +159,7 @@ typedef struct ou_conv_desc {
      * fir 0: the other kernels (FIR folded into the weights). */
     int32_t fir;
     int32_t fir_pad_;
-    const float* fir_taps;     /* [2R + 1] FIR taps (device)                     */
+    const float* fir_taps;     /* [2R + 1] FIR taps (device; fir 1 / 2)          */
 } ou_conv_desc;
 
 /* Default channel chunk of the kernel for a tap count (informational: the

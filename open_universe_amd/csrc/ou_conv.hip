@@ -2418,6 +2418,14 @@ __global__ __launch_bounds__(256 + 64 * kWsLoaders) void conv_wkernel(ou_conv_de
 // through a register ring one K chunk deep (the slot a step's MFMAs used is
 // refilled with the next chunk's same step); B is double-buffered in LDS, one
 // barrier per chunk.  Split-f16 (P 1: three MFMAs per k-step) or f16 (P 2).
+//
+// conv_fdkernel<..., ST = 1> (ou_conv_desc.fir 3) is the same kernel without
+// the FIR for the conditioner's wide strided st_convs (condition.py:53-59:
+// kernel = stride = Rt of 20 .. 240): K = cin Rt in the same channel-block
+// order, walked as chunks of 16 channels x R phases (R = 4 or 8 dividing Rt),
+// the R phases of every frame being one contiguous run of samples -- so a
+// workgroup reads each input sample once (the frame-view kernels' phase-major
+// chunks re-read every line once per chunk of phases).
 // ---------------------------------------------------------------------------
 [[maybe_unused]] constexpr int kFirBit = 1 << 17;
 
@@ -2454,10 +2462,11 @@ __device__ __forceinline__ void fir_taps(const ou_conv_desc& d, float (&tap)[NT]
     for (int j = 0; j < NT; ++j) tap[j] = d.fir_taps[j];
 }
 
-template <int R, int WM, int WN, int MR, int NR, int P>
+template <int R, int WM, int WN, int MR, int NR, int P, int ST = 0>
 __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride)
 {
     using F = FCfg<R, WM, WN, MR, NR>;
+    constexpr int WIN = ST ? F::DF * R : F::DWIN;   // window samples per staging thread
     ou_kernarg_prefetch8();
     OU_DYNAMIC_LDS(float4, lds4);
     _Float16* ldsh = (_Float16*)lds4;
@@ -2471,13 +2480,15 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
     const int n0 = bx * F::BN + d.f0;     // first output frame (global)
     const int mt0 = by * (WM * MR);
     const int in_len = d.in_len;
-    const int nch = d.cin / 16;           // K chunks
+    const int Rt = ST ? d.frame : R;      // samples per frame
+    const int nsub = Rt / R;              // chunks (of R phases) per 16-channel block
+    const int nch = d.cin / 16 * nsub;    // K chunks: block cb = q / nsub, phases (q % nsub) R ..
     const float xsc = ou_exp2i(-d.xs_shift), su = d.w_unscale * ou_exp2i(d.xs_shift - kSplitShift);
     const float slope = d.slope;
     float tap[F::NT];
-    fir_taps<F::NT>(d, tap);
+    if constexpr (!ST) fir_taps<F::NT>(d, tap);
 
-    // ---- weights: chunk q, step s = phase -> 16-channel group q R + s
+    // ---- weights: chunk q, step s -> 16-channel group q R + s = cb Rt + ph
     const __amdgpu_buffer_rsrc_t ars = ou_rsrc(d.w, (int64_t)mtiles * a_mt_stride * 4);
     half8_t ra[R][MR][2];
     auto load_a = [&](int q, int s) {   // q uniform, clamped (a reload past the end is never used)
@@ -2494,21 +2505,25 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
 
     // ---- staging: thread (channel sc of the chunk, frame group sg) owns
     // frames n0 + sg F .. + F - 1; its window is samples [s0, s0 + (F + 2) R)
+    // (ST: the R-sample runs (n0 + sg F + f) Rt + sub R .. of its F frames f)
     const int sc = tid >> 4, sg = tid & 15;
     const int64_t xc = d.x_cstride;
     const __amdgpu_buffer_rsrc_t xrs = ou_rsrc(d.x + (int64_t)b * d.x_bstride, (int64_t)d.cin * xc * 4);
-    const int s0 = (n0 + sg * F::DF - 1) * R;
+    const int s0 = ST ? (n0 + sg * F::DF) * Rt : (n0 + sg * F::DF - 1) * R;
     // 16-B (R % 4 == 0) / 8-B (R == 2) loads where every row start is aligned
     constexpr int V = R % 4 == 0 ? 4 : (R == 2 ? 2 : 1);
     const bool vec = V > 1 && ((uintptr_t)d.x % (4 * V)) == 0 && d.x_bstride % V == 0 && xc % V == 0;
-    float xw[F::DWIN];
+    float xw[WIN];
     auto stage_load = [&](int q) {   // q uniform, clamped (the extra load is never stored)
         q = min(q, nch - 1);
-        const int row = (q * 16 + sc) * (int)xc;
+        const int cb = ST ? q / nsub : q;
+        const int row = (cb * 16 + sc) * (int)xc;
+        const int sb = ST ? s0 + (q - cb * nsub) * R : s0;   // the chunk's first sample
         if (vec) {
 #pragma unroll
-            for (int e = 0; e < F::DWIN; e += V) {
-                const int smp = s0 + e;   // a multiple of V: a group lies wholly left of 0 or right of it
+            for (int e = 0; e < WIN; e += V) {
+                // a multiple of V: a group lies wholly left of 0 or right of it
+                const int smp = sb + (ST ? (e / R) * Rt + e % R : e);
                 const int off = (smp >= 0 && smp < in_len) ? (row + smp) * 4 : kSentinel;
                 if constexpr (V == 4) {
                     const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);
@@ -2522,8 +2537,8 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
             }
         } else {
 #pragma unroll
-            for (int e = 0; e < F::DWIN; ++e) {
-                const int smp = s0 + e;
+            for (int e = 0; e < WIN; ++e) {
+                const int smp = sb + (ST ? (e / R) * Rt + e % R : e);
                 xw[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                     xrs, (smp >= 0 && smp < in_len) ? (row + smp) * 4 : kSentinel, 0, 0));
             }
@@ -2533,15 +2548,19 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
     auto stage_store = [&](int buf) {
         _Float16* bh = ldsh + buf * 2 * F::DPLANE + sg * F::DF * F::DRS + sc;
 #pragma unroll
-        for (int e = 0; e < F::DWIN; ++e) {
+        for (int e = 0; e < WIN; ++e) {
             const float v = xw[e] * xsc;   // 2^-s: exact
             xw[e] = v >= 0.f ? v : v * slope;
         }
 #pragma unroll
         for (int i = 0; i < F::DF * R; ++i) {
             float f = 0.f;
+            if constexpr (ST) {
+                f = xw[i];
+            } else {
 #pragma unroll
-            for (int j = 0; j < F::NT; ++j) f = fmaf(tap[j], xw[i + j], f);
+                for (int j = 0; j < F::NT; ++j) f = fmaf(tap[j], xw[i + j], f);
+            }
             omax = fmaxf(omax, __builtin_fabsf(f));
             const _Float16 hi = (_Float16)f;
             const int o = (i / R) * F::DRS + (i % R) * 16;
@@ -3230,10 +3249,18 @@ int launch_f(const ou_conv_desc& d, hipStream_t s)
 {
     using F = FCfg<R, WM, WN, MR, NR>;
     static bool attr[4] = {false, false, false, false};   // (direction, precision) opted in to > 64 KiB
-    if (d.fir == 1) {   // down: K = cin R in chunks of 16 channels
+    if (d.fir == 1 || d.fir == 3) {   // down / st_conv: K = cin frame in chunks of 16 channels x R phases
         const int mtiles = (d.m + 31) / 32;
-        const int64_t a_mt_stride = (int64_t)((d.cin * R + kCinAlign - 1) / kCinAlign * kCinAlign) * 32;
+        const int64_t a_mt_stride = (int64_t)((d.cin * d.frame + kCinAlign - 1) / kCinAlign * kCinAlign) * 32;
         const dim3 grid((d.n_frames + F::BN - 1) / F::BN, (mtiles + WM * MR - 1) / (WM * MR), d.batch);
+        if constexpr (R == 4 || R == 8) {
+            static bool sattr[2] = {false, false};
+            if (d.fir == 3)
+                return d.prec == 1 ? fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 1, 1>, F::DLDS, grid, d, mtiles,
+                                                a_mt_stride, sattr[0], s)
+                                   : fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 2, 1>, F::DLDS, grid, d, mtiles,
+                                                a_mt_stride, sattr[1], s);
+        }
         return d.prec == 1
                    ? fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 1>, F::DLDS, grid, d, mtiles, a_mt_stride, attr[0], s)
                    : fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 2>, F::DLDS, grid, d, mtiles, a_mt_stride, attr[1], s);
@@ -3525,12 +3552,14 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
                                "(m %d rout %d rows %d out_len %d)", d.m, d.rout, d.sy_rows, d.out_len);
     }
     if (d.fir || (d.tile >= 0 && (d.tile & kFirBit))) {   // FIR applied (bits 0-7: OU_FTILES shape)
-        const int R = d.fir == 1 ? d.frame : (d.rout < 0 ? -d.rout : d.rout);
-        if ((d.fir != 1 && d.fir != 2) || !d.fir_taps || (d.prec != 1 && d.prec != 2) || d.kt != 1 || d.pad ||
-            d.shift || d.in_scale || d.xs || (d.fir == 1 && (d.rout != 1 || d.cin % 16)) ||
-            (d.fir == 2 && (d.frame != 1 || d.cin % 32)) || (R != 2 && R != 3 && R != 4 && R != 5 && R != 8))
-            return ou_fail(-1, "conv: FIR mode %d needs prec 1/2, kt 1, pad 0, shift 0, no in_scale / xs, rate 2/3/4/5/8, "
-                               "cin %% 16 (down) / 32 (up) == 0 (cin %d frame %d rout %d kt %d)",
+        // fir 3 (st_convs, no FIR): chunks of R = 8 (or 4) of the frame's phases
+        const int R = d.fir == 1 ? d.frame : d.fir == 3 ? (d.frame % 8 == 0 ? 8 : 4) : (d.rout < 0 ? -d.rout : d.rout);
+        if (d.fir < 1 || d.fir > 3 || (d.fir != 3 && !d.fir_taps) || (d.prec != 1 && d.prec != 2) || d.kt != 1 ||
+            d.pad || d.shift || d.in_scale || d.xs || (d.fir != 2 && (d.rout != 1 || d.cin % 16)) ||
+            (d.fir == 2 && (d.frame != 1 || d.cin % 32)) || (d.fir == 3 && (d.frame < 4 || d.frame % 4)) ||
+            (R != 2 && R != 3 && R != 4 && R != 5 && R != 8))
+            return ou_fail(-1, "conv: FIR mode %d needs prec 1/2, kt 1, pad 0, shift 0, no in_scale / xs, rate 2/3/4/5/8 "
+                               "(mode 3: a multiple of 4), cin %% 16 (down) / 32 (up) == 0 (cin %d frame %d rout %d kt %d)",
                            d.fir, d.cin, d.frame, d.rout, d.kt);
         if (!(d.w_unscale > 0.f)) return ou_fail(-1, "conv: FIR mode needs the w_unscale of ou_conv_pack_split_nat");
         const int tile = d.tile >= 0 ? d.tile : (kFirBit | 2);

@@ -329,7 +329,7 @@ class FirW:
     tile bit 17): unfolded weights (K = cin * rate down, cin up; one tap) in
     the kernels' order (include/ouhip.h), packed by ou_conv_pack_split_nat,
     and the (2 rate + 1)-tap binomial FIR on the device."""
-    mode: int                # 1: FIR before a strided conv, 2: after a transposed conv
+    mode: int                # 1: FIR before a strided conv, 2: after a transposed conv, 3: no FIR (st_convs)
     rate: int
     w: torch.Tensor
     unscale: float
@@ -350,7 +350,7 @@ class ConvSpec:
     shift: int = 0
     ref_macs: float = 0.0   # MACs of the replaced reference ops per output frame
     cm: bool = False        # rout > 1: rows ordered m = co * rout + ph (else ph * cout + co)
-    fir: Optional[tuple] = None   # (mode 1 down / 2 up, rate, unfolded logical weights, taps): FirW
+    fir: Optional[tuple] = None   # (mode 1 down / 2 up / 3 plain strided, rate, unfolded weights, taps): FirW
 
 
 def make_conv(spec, device, prec=None):
@@ -443,8 +443,14 @@ def spec_down(sd, p, r, antialias):
             fir = (1, r, wu, dsp.binomial_taps(2 * r + 1))
         return ConvSpec(wl, cin, r, 1, 1, _slope(sd, p), _bias(sd, p + ".bias"),
                         ref_macs=float(cout * cin * r + cin * (2 * r + 1) * r), fir=fir)
+    fir = None
+    if cin % 16 == 0 and r % 4 == 0:
+        # the wide strided convs (st_convs, rates 20 .. 240) in the FIR kernels'
+        # K order without a FIR (ou_conv_desc.fir 3): each input sample read once
+        wu = w.reshape(cout, cin // 16, 16, r).transpose(0, 1, 3, 2).reshape(cout, cin * r)
+        fir = (3, r, wu, np.ones(1, np.float32))
     return ConvSpec(w.reshape(cout, cin * r, 1), cin, r, 0, 1, _slope(sd, p),
-                    _bias(sd, p + ".conv.bias"), ref_macs=float(cout * cin * r))
+                    _bias(sd, p + ".conv.bias"), ref_macs=float(cout * cin * r), fir=fir)
 
 
 def spec_up(sd, p, r, antialias):

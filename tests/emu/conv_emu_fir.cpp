@@ -10,6 +10,7 @@
 #include "../../open_universe_amd/csrc/ou_conv.hip"
 
 #include <cmath>
+#include <string>
 
 static uint32_t g_seed = 4242;
 static float rnd()
@@ -38,8 +39,79 @@ struct Case {
     int valid_cut;      // valid_len = full - cut
 };
 
+// fir 3 (st_convs): a plain strided conv, kernel = stride = Rt, in the FIR
+// kernels' blocked K order, walked in chunks of 8 (or 4) phases
+static int st_cases(int& n)
+{
+    int bad = 0;
+    const float slope = 0.25f;
+    const int rts[] = {20, 40, 24};
+    for (int Rt : rts) {
+        const int cin = 32, cout = 64, B = 2, T = 7 * Rt + 5, U = (T + Rt - 1) / Rt;
+        std::vector<float> w((size_t)cout * cin * Rt), x((size_t)B * cin * T), bias(cout);
+        for (auto* v : {&w, &x, &bias})
+            for (auto& e : *v) e = rnd();
+        std::vector<double> ref((size_t)B * cout * U);
+        for (int b = 0; b < B; ++b)
+            for (int co = 0; co < cout; ++co)
+                for (int u = 0; u < U; ++u) {
+                    double acc = bias[co];
+                    for (int ci = 0; ci < cin; ++ci)
+                        for (int ph = 0; ph < Rt; ++ph) {
+                            const int t = u * Rt + ph;
+                            if (t >= T) continue;
+                            double v = x[((size_t)b * cin + ci) * T + t];
+                            v = v >= 0 ? v : v * slope;
+                            acc += (double)w[((size_t)co * cin + ci) * Rt + ph] * v;
+                        }
+                    ref[((size_t)b * cout + co) * U + u] = acc;
+                }
+        const int keff = cin * Rt;
+        std::vector<float> wl((size_t)cout * keff);
+        for (int co = 0; co < cout; ++co)
+            for (int ci = 0; ci < cin; ++ci)
+                for (int ph = 0; ph < Rt; ++ph)
+                    wl[(size_t)co * keff + ((ci / 16) * Rt + ph) * 16 + ci % 16] = w[((size_t)co * cin + ci) * Rt + ph];
+        std::vector<float> packed(ou_conv_packed_size(cout, keff, 1, 0));
+        float unscale = 0.f;
+        ou_conv_pack_split_nat(wl.data(), cout, keff, 1, packed.data(), &unscale);
+        double rn = 0;
+        for (double v : ref) rn += v * v;
+        for (int shape = 0; shape < kNumFTiles; ++shape) {
+            std::vector<float> y(ref.size(), 1e30f);
+            ou_conv_desc d{};
+            d.x = x.data(); d.x_bstride = (int64_t)cin * T; d.x_cstride = T;
+            d.cin = cin; d.in_len = T; d.frame = Rt; d.slope = slope;
+            d.w = packed.data(); d.m = cout; d.kt = 1; d.pad = 0;
+            d.n_frames = U; d.batch = B; d.y = y.data(); d.y_bstride = (int64_t)cout * U; d.y_cstride = U;
+            d.rout = 1; d.out_len = U; d.valid_len = 1 << 30; d.bias = bias.data();
+            d.prec = 1; d.w_unscale = unscale; d.xs_shift = 6; d.fir = 3;
+            d.tile = kFirBit | shape;
+            if (ou_conv(&d, nullptr) != 0) {
+                std::printf("st Rt %d shape %d: launch error %s\n", Rt, shape, ouhip_detail::err_buf());
+                ++bad;
+                continue;
+            }
+            double en = 0;
+            for (size_t i = 0; i < y.size(); ++i) en += (y[i] - ref[i]) * (y[i] - ref[i]);
+            ++n;
+            if (!(std::sqrt(en / rn) < 2e-6)) {
+                std::printf("st Rt %d shape %d: rel err %.3g\n", Rt, shape, std::sqrt(en / rn));
+                ++bad;
+            }
+        }
+    }
+    return bad;
+}
+
 int main(int argc, char** argv)
 {
+    if (argc > 1 && std::string(argv[1]) == "st") {
+        int n = 0;
+        const int bad = st_cases(n);
+        std::printf("%s: %d launches checked, %d bad\n", bad ? "FAIL" : "ok", n, bad);
+        return bad ? 1 : 0;
+    }
     const int R = argc > 1 ? std::atoi(argv[1]) : 2;
     int bad = 0, n = 0;
     const Case cases[] = {

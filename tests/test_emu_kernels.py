@@ -178,12 +178,14 @@ def test_fir_values_match_reference(tmp_path):
     strided conv; ragged lengths, FiLM, the split-image output) and up (FIR
     after the transposed conv; residuals, FiLM, a cropped output, valid_len
     zero-fill) against a double-precision evaluation of the reference's op
-    order, at every rate the configs use (2, 3, 4, 5, 8)."""
+    order, at every rate the configs use (2, 3, 4, 5, 8); and the same
+    kernel without the FIR for the st_convs (fir 3: kernel = stride = 20, 24,
+    40; chunks of 4 / 8 phases)."""
     exe = str(tmp_path / "conv_emu_fir")
     _build("conv_emu_fir.cpp", exe, *ASAN, "-DOU_EMU_FIBERS")
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
     procs = [subprocess.Popen([exe, r], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
-             for r in ("2", "3", "4", "5", "8")]
+             for r in ("2", "3", "4", "5", "8", "st")]
     for p in procs:
         out, err = p.communicate(timeout=900)
         assert p.returncode == 0 and "ok:" in out, (out[-2000:], err[-2000:])

@@ -243,8 +243,9 @@ def emulate_fir(spec, x, n_frames, out_len, valid_len=None):
     t = torch.from_numpy(np.asarray(taps, np.float64))
     fir = lambda v: F.conv1d(v, t[None, None].expand(v.shape[1], 1, -1), padding="same", groups=v.shape[1])
     wu = torch.from_numpy(np.asarray(wu, np.float64))
-    if mode == 1:   # k = (cb r + ph) 16 + c for ci = 16 cb + c
-        f = fir(F.pad(x, (0, n_frames * r - T)))
+    if mode in (1, 3):   # k = (cb r + ph) 16 + c for ci = 16 cb + c (mode 3: no FIR)
+        f = F.pad(x, (0, n_frames * r - T))
+        f = fir(f) if mode == 1 else f
         bv = f.reshape(B, Cin // 16, 16, n_frames, r).permute(0, 1, 4, 2, 3).reshape(B, Cin * r, n_frames)
         y = torch.einsum("mk,bku->bmu", wu, bv)
     else:           # row 32 (co // P) + (co % P) r + ph
@@ -297,6 +298,19 @@ def test_fir_form_up_matches_folded(r, extra_len):
     length = r * 13 + extra_len
     torch.testing.assert_close(emulate_fir(spec, x, 13, length, valid_len=r * 13),
                                emulate(spec, x, 13, length, valid_len=r * 13), rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("r", [4, 20, 40, 120])
+def test_st_conv_form_matches_plain(r):
+    """The st_convs' blocked K order (ou_conv_desc.fir 3, no FIR) computes
+    what the plain frame-view weights do."""
+    sd = _sd_rc("down", 32, 48, r, seed=r)
+    spec = E.spec_down(sd, "p", r, False)
+    assert spec.fir is not None and spec.fir[0] == 3
+    T = 5 * r + 3
+    x = _x(2, 32, T, seed=r)
+    U = -(-T // r)
+    torch.testing.assert_close(emulate_fir(spec, x, U, U), emulate(spec, x, U, U), rtol=1e-9, atol=1e-9)
 
 
 def test_fir_form_only_where_the_kernels_apply():
