@@ -424,9 +424,7 @@ _MMAJOR_BYTES = float(os.environ.get("OUHIP_MMAJOR_MB", "128")) * 2**20
 
 
 def mmajor_order(desc):
-    # one-tile and register-streamed kernels, and the FIR kernels (tile bit 17,
-    # whose bits 8-9 are tiles per workgroup along the frames)
-    if not _MMAJOR or (desc.tile & ((3 << 8) | (1 << 10)) and not desc.tile & (1 << 17)):
+    if not _MMAJOR or desc.tile & ((3 << 8) | (1 << 10)):   # one-tile and register-streamed kernels only
         return False
     in_bytes = 4.0 * desc.batch * desc.cin * desc.frame * desc.n_frames
     return in_bytes > _MMAJOR_BYTES

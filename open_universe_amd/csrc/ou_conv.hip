@@ -2451,7 +2451,7 @@ struct FCfg {
     static constexpr int YRS = BN * R + 8;          // up: sample-row stride of the Y image (floats)
     static constexpr int ULDS_B = 2 * 2 * UPLANE * 2;
     static constexpr int ULDS_Y = UCH * YRS * 4;
-    static constexpr int ULDS = ULDS_B + ULDS_Y;    // Y beside the B buffers (multi-tile workgroups)
+    static constexpr int ULDS = ULDS_B > ULDS_Y ? ULDS_B : ULDS_Y;
 };
 
 // FIR taps of one launch (uniform addresses: scalar loads)
@@ -2477,19 +2477,12 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
     int bx, by, bz;
     if (d.tile & kMajBit) ou_xcd_block_m(bx, by, bz); else ou_xcd_block(bx, by, bz);
     const int b = bz;
-    // tile bits 8-9: the workgroup runs TPW consecutive frame tiles as one
-    // stream of (tile, chunk) items, so the next tile's first window loads
-    // while this tile's last MFMAs and its epilogue run
-    const int tpw = 1 << ((d.tile >> 8) & 3);
-    const int ntn = (d.n_frames + F::BN - 1) / F::BN;
-    const int nt = min(tpw, ntn - bx * tpw);   // tiles of this workgroup (>= 1: the grid is ceil(ntn / tpw))
+    const int n0 = bx * F::BN + d.f0;     // first output frame (global)
     const int mt0 = by * (WM * MR);
     const int in_len = d.in_len;
     const int Rt = ST ? d.frame : R;      // samples per frame
     const int nsub = Rt / R;              // chunks (of R phases) per 16-channel block
     const int nch = d.cin / 16 * nsub;    // K chunks: block cb = q / nsub, phases (q % nsub) R ..
-    const int nitems = nt * nch;          // item i: tile i / nch, chunk i % nch
-    auto n0_of = [&](int j) { return (bx * tpw + j) * F::BN + d.f0; };   // first output frame of tile j
     const float xsc = ou_exp2i(-d.xs_shift), su = d.w_unscale * ou_exp2i(d.xs_shift - kSplitShift);
     const float slope = d.slope;
     float tap[F::NT];
@@ -2498,8 +2491,8 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
     // ---- weights: chunk q, step s -> 16-channel group q R + s = cb Rt + ph
     const __amdgpu_buffer_rsrc_t ars = ou_rsrc(d.w, (int64_t)mtiles * a_mt_stride * 4);
     half8_t ra[R][MR][2];
-    auto load_a = [&](int i, int s) {   // item i uniform, clamped (a reload past the end is never used)
-        const int q = min(i, nitems - 1) % nch;
+    auto load_a = [&](int q, int s) {   // q uniform, clamped (a reload past the end is never used)
+        q = min(q, nch - 1);
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr) {
             const int mt = min(mt0 + wm * MR + mr, mtiles - 1);
@@ -2516,15 +2509,13 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
     const int sc = tid >> 4, sg = tid & 15;
     const int64_t xc = d.x_cstride;
     const __amdgpu_buffer_rsrc_t xrs = ou_rsrc(d.x + (int64_t)b * d.x_bstride, (int64_t)d.cin * xc * 4);
+    const int s0 = ST ? (n0 + sg * F::DF) * Rt : (n0 + sg * F::DF - 1) * R;
     // 16-B (R % 4 == 0) / 8-B (R == 2) loads where every row start is aligned
     constexpr int V = R % 4 == 0 ? 4 : (R == 2 ? 2 : 1);
     const bool vec = V > 1 && ((uintptr_t)d.x % (4 * V)) == 0 && d.x_bstride % V == 0 && xc % V == 0;
     float xw[WIN];
-    auto stage_load = [&](int i) {   // item i uniform, clamped (the extra load is never stored)
-        i = min(i, nitems - 1);
-        const int j = i / nch, q = i - (i / nch) * nch;
-        const int n0 = n0_of(j);
-        const int s0 = ST ? (n0 + sg * F::DF) * Rt : (n0 + sg * F::DF - 1) * R;
+    auto stage_load = [&](int q) {   // q uniform, clamped (the extra load is never stored)
+        q = min(q, nch - 1);
         const int cb = ST ? q / nsub : q;
         const int row = (cb * 16 + sc) * (int)xc;
         const int sb = ST ? s0 + (q - cb * nsub) * R : s0;   // the chunk's first sample
@@ -2621,48 +2612,37 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
     for (int s = 0; s < R; ++s) load_a(0, s);
     stage_store(0);
     __syncthreads();
-    const float sx = su * (1.f / 2048.f);
-    for (int i = 0; i < nitems; ++i) {
-        const int cur = i & 1;
-        stage_load(i + 1);   // the next item's window, in flight under this item's MFMAs
+    for (int q = 0; q < nch; ++q) {
+        const int cur = q & 1;
+        stage_load(q + 1);   // the next chunk's window, in flight under this chunk's MFMAs
 #pragma unroll
         for (int s = 0; s < R; ++s) {
             mfma_step(cur, s);
-            load_a(i + 1, s);   // refill the slot just used
+            load_a(q + 1, s);   // refill the slot just used
         }
-        if (i + 1 < nitems) stage_store(cur ^ 1);
-        if (i % nch == nch - 1) {   // the tile's last chunk (uniform): its epilogue
-#pragma unroll
-            for (int mr = 0; mr < MR; ++mr)
-#pragma unroll
-                for (int nr = 0; nr < NR; ++nr)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        acc[mr][nr][r] = P == 1 ? fmaf(accx[mr][nr][r], sx, acc[mr][nr][r] * su) : acc[mr][nr][r] * su;
-                        if constexpr (P == 1) accx[mr][nr][r] = 0.f;
-                    }
-            conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0_of(i / nch) + wn * (32 * NR), acc, lane);
-#pragma unroll
-            for (int mr = 0; mr < MR; ++mr)
-#pragma unroll
-                for (int nr = 0; nr < NR; ++nr)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[mr][nr][r] = 0.f;
-        }
+        if (q + 1 < nch) stage_store(cur ^ 1);
         __syncthreads();
     }
     if constexpr (P != 0) ou_range_flag(d.status, omax, 1, lane);
+    const float sx = su * (1.f / 2048.f);
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                acc[i][j][r] = P == 1 ? fmaf(accx[i][j][r], sx, acc[i][j][r] * su) : acc[i][j][r] * su;
+    conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane);
 }
 
 template <int R, int WM, int WN, int MR, int NR, int P>
 __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride)
 {
     using F = FCfg<R, WM, WN, MR, NR>;
-    constexpr int BNO = F::BN - 2;        // output frames per tile (one halo frame each side)
+    constexpr int BNO = F::BN - 2;        // output frames per workgroup (one halo frame each side)
     ou_kernarg_prefetch8();
     OU_DYNAMIC_LDS(float4, lds4);
     _Float16* ldsh = (_Float16*)lds4;
-    float* Y = (float*)(ldsh + 2 * 2 * F::UPLANE);   // the Y image, after the two B buffers
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wn = wave % WN, wm = wave / WN;
@@ -2670,23 +2650,19 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
     int bx, by, bz;
     if (d.tile & kMajBit) ou_xcd_block_m(bx, by, bz); else ou_xcd_block(bx, by, bz);
     const int b = bz;
-    // tile bits 8-9: TPW consecutive frame tiles per workgroup, one item stream
-    const int tpw = 1 << ((d.tile >> 8) & 3);
-    const int ntn = (d.n_frames + BNO - 1) / BNO;
-    const int nt = min(tpw, ntn - bx * tpw);
-    auto u0_of = [&](int j) { return (bx * tpw + j) * BNO + d.f0; };   // first output frame of tile j
+    const int u0 = bx * BNO + d.f0;       // first output frame
+    const int fa = u0 - 1;                // frame of B row 0
     const int mt0 = by * (WM * MR);       // first packed m-tile
     const int in_len = d.in_len;
     const int nch = d.cin / 32;
-    const int nitems = nt * nch;
     const int cout = d.m / R;
     const float xsc = ou_exp2i(-d.xs_shift), su = d.w_unscale * ou_exp2i(d.xs_shift - kSplitShift);
     const float slope = d.slope;
 
     const __amdgpu_buffer_rsrc_t ars = ou_rsrc(d.w, (int64_t)mtiles * a_mt_stride * 4);
     half8_t ra[2][MR][2];
-    auto load_a = [&](int i, int s) {
-        const int q = min(i, nitems - 1) % nch;
+    auto load_a = [&](int q, int s) {
+        q = min(q, nch - 1);
 #pragma unroll
         for (int mr = 0; mr < MR; ++mr) {
             const int mt = min(mt0 + wm * MR + mr, mtiles - 1);
@@ -2697,13 +2673,12 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
         }
     };
 
-    // ---- staging: element e = (8-channel group cg = it / BN, row n = it % BN)
+    // ---- staging: item it = (8-channel group cg = it / BN, row n = it % BN)
     const int64_t xc = d.x_cstride;
     const __amdgpu_buffer_rsrc_t xrs = ou_rsrc(d.x + (int64_t)b * d.x_bstride, (int64_t)d.cin * xc * 4);
     float xv[F::UIE][8];
-    auto stage_load = [&](int i) {
-        i = min(i, nitems - 1);
-        const int q = i % nch, fa = u0_of(i / nch) - 1;   // frame of B row 0
+    auto stage_load = [&](int q) {
+        q = min(q, nch - 1);
 #pragma unroll
         for (int e = 0; e < F::UIE; ++e) {
             const int it = tid + 256 * e;
@@ -2740,18 +2715,20 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
 
     floatx16 acc[MR][NR];
     floatx16 accx[P == 1 ? MR : 1][P == 1 ? NR : 1];
-    auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    if constexpr (P == 1) {
 #pragma unroll
         for (int i = 0; i < MR; ++i)
 #pragma unroll
             for (int j = 0; j < NR; ++j)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    acc[i][j][r] = 0.f;
-                    if constexpr (P == 1) accx[i][j][r] = 0.f;
-                }
-    };
-    zero_acc();
+                for (int r = 0; r < 16; ++r) accx[i][j][r] = 0.f;
+    }
     const _Float16* bb = ldsh + (wn * 32 * NR + l32) * F::URS + 8 * h;
     auto mfma_step = [&](int buf, int s) {
         half8_t bq[NR], bl[NR];
@@ -2773,11 +2750,48 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
             }
     };
 
-    // ---- the epilogue's constants
+    stage_load(0);
+    load_a(0, 0);
+    load_a(0, 1);
+    stage_store(0);
+    __syncthreads();
+    for (int q = 0; q < nch; ++q) {
+        const int cur = q & 1;
+        stage_load(q + 1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            mfma_step(cur, s);
+            load_a(q + 1, s);
+        }
+        if (q + 1 < nch) stage_store(cur ^ 1);
+        __syncthreads();
+    }
+    if constexpr (P != 0) ou_range_flag(d.status, omax, 1, lane);
+
+    // ---- the transposed conv's outputs -> Y [channel of the workgroup][sample]
+    // (sample row index n R + ph for B row n, i.e. global sample (fa + n) R + ph)
+    float* Y = (float*)lds4;
+    const float sx = su * (1.f / 2048.f);
+#pragma unroll
+    for (int mr = 0; mr < MR; ++mr)
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int ml = (r & 3) + 8 * (r >> 2) + 4 * h;   // row within the m-tile
+                const int cl = ml / R, ph = ml - (ml / R) * R;
+                const float v = P == 1 ? fmaf(accx[mr][nr][r], sx, acc[mr][nr][r] * su) : acc[mr][nr][r] * su;
+                if (cl < F::CPT)
+                    Y[((wm * MR + mr) * F::CPT + cl) * F::YRS + (wn * 32 * NR + nr * 32 + l32) * R + ph] = v;
+            }
+    __syncthreads();
+
+    // ---- FIR over 4 consecutive output samples per item, bias, residuals, store
     float tap[F::NT];
     fir_taps<F::NT>(d, tap);
     const int ylen = d.out_len, vlen = d.valid_len;
-    const int c0 = mt0 * F::CPT;          // first channel of the workgroup
+    const int tend = min((min(u0 + BNO, d.f0 + d.n_frames)) * R, ylen);   // samples [u0 R, tend) are stored
+    const int c0 = mt0 * F::CPT;                                           // first channel of the workgroup
     const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr, has_fm = d.film != nullptr;
     const float s1e = has_r1 ? d.s1 : 1.f, s2e = has_r2 ? d.s2 : 1.f, fadd = has_fm ? 0.f : 1.f;
     const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)cout * d.y_cstride * 4);
@@ -2788,97 +2802,49 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
     const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
     const __amdgpu_buffer_rsrc_t fs =
         ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y, has_fm ? (int64_t)cout * 8 : 0);
-    const float sx = su * (1.f / 2048.f);
-
-    // the transposed conv's outputs of a tile -> Y [channel of the workgroup][sample]
-    // (sample row index n R + ph for B row n, i.e. global sample (u0 - 1 + n) R + ph)
-    auto write_y = [&]() {
+    constexpr int NSG = (BNO * R + 3) / 4;   // 4-sample groups per channel
+    constexpr int NW = (4 + 2 * R + 3) / 4 * 4;   // window floats read (16-B reads)
+    for (int it = tid; it < F::UCH * NSG; it += 256) {
+        const int cw = it / NSG, g = it - (it / NSG) * NSG;
+        const int co = c0 + cw;
+        const int sig = 4 * g;            // output sample u0 R + sig <-> Y index sig + R
+        const int t0 = u0 * R + sig;
+        float w[NW];
+        const float* yr = Y + cw * F::YRS + sig;
 #pragma unroll
-        for (int mr = 0; mr < MR; ++mr)
-#pragma unroll
-            for (int nr = 0; nr < NR; ++nr)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int ml = (r & 3) + 8 * (r >> 2) + 4 * h;   // row within the m-tile
-                    const int cl = ml / R, ph = ml - (ml / R) * R;
-                    const float v = P == 1 ? fmaf(accx[mr][nr][r], sx, acc[mr][nr][r] * su) : acc[mr][nr][r] * su;
-                    if (cl < F::CPT)
-                        Y[((wm * MR + mr) * F::CPT + cl) * F::YRS + (wn * 32 * NR + nr * 32 + l32) * R + ph] = v;
-                }
-    };
-    // FIR over 4 consecutive output samples per item, bias, residuals, store
-    auto fir_out = [&](int u0) {
-        const int tend = min((min(u0 + BNO, d.f0 + d.n_frames)) * R, ylen);   // samples [u0 R, tend) are stored
-        constexpr int NSG = (BNO * R + 3) / 4;        // 4-sample groups per channel
-        constexpr int NW = (4 + 2 * R + 3) / 4 * 4;   // window floats read (16-B reads)
-        for (int it = tid; it < F::UCH * NSG; it += 256) {
-            const int cw = it / NSG, g = it - (it / NSG) * NSG;
-            const int co = c0 + cw;
-            const int sig = 4 * g;            // output sample u0 R + sig <-> Y index sig + R
-            const int t0 = u0 * R + sig;
-            float w[NW];
-            const float* yr = Y + cw * F::YRS + sig;
-#pragma unroll
-            for (int k = 0; k < NW; k += 4) {
-                const float4 q4 = *(const float4*)(yr + k);
-                w[k] = q4.x, w[k + 1] = q4.y, w[k + 2] = q4.z, w[k + 3] = q4.w;
-            }
-            const bool cok = co < cout;
-            const float bias = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, cok ? co * 4 : kSentinel, 0, 0));
-            const float ga = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, cok ? co * 4 : kSentinel, 0, 0));
-            const float gb =
-                __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, cok ? (cout + co) * 4 : kSentinel, 0, 0));
-            int off[4];
-            float v1[4], v2[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int t = t0 + k;
-                off[k] = (cok && sig + k < BNO * R && t < tend) ? t : -1;
-                v1[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                    r1s, off[k] >= 0 ? (co * (int)d.r1_cstride + t) * 4 : kSentinel, 0, 0));
-                v2[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                    r2s, off[k] >= 0 ? (co * (int)d.r2_cstride + t) * 4 : kSentinel, 0, 0));
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                float f = 0.f;
-#pragma unroll
-                for (int j = 0; j < F::NT; ++j) f = fmaf(tap[j], w[k + j], f);
-                float v = f + bias;
-                if (off[k] >= vlen) v = 0.f;
-                v = (v + v1[k]) * s1e;
-                v = (ga + fadd) * v + gb;
-                v = (v + v2[k]) * s2e;
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ys,
-                                                      off[k] >= 0 ? (co * (int)d.y_cstride + off[k]) * 4 : kSentinel, 0, 0);
-            }
+        for (int k = 0; k < NW; k += 4) {
+            const float4 q4 = *(const float4*)(yr + k);
+            w[k] = q4.x, w[k + 1] = q4.y, w[k + 2] = q4.z, w[k + 3] = q4.w;
         }
-    };
-
-    stage_load(0);
-    load_a(0, 0);
-    load_a(0, 1);
-    stage_store(0);
-    __syncthreads();
-    for (int i = 0; i < nitems; ++i) {
-        const int cur = i & 1;
-        const bool last = i % nch == nch - 1;   // the tile's last chunk (uniform)
-        stage_load(i + 1);   // the next item's frames (the next tile's after a last chunk)
+        const bool cok = co < cout;
+        const float bias = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, cok ? co * 4 : kSentinel, 0, 0));
+        const float ga = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, cok ? co * 4 : kSentinel, 0, 0));
+        const float gb = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, cok ? (cout + co) * 4 : kSentinel, 0, 0));
+        int off[4];
+        float v1[4], v2[4];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            mfma_step(cur, s);
-            load_a(i + 1, s);
+        for (int k = 0; k < 4; ++k) {
+            const int t = t0 + k;
+            off[k] = (cok && sig + k < BNO * R && t < tend) ? t : -1;
+            v1[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                r1s, off[k] >= 0 ? (co * (int)d.r1_cstride + t) * 4 : kSentinel, 0, 0));
+            v2[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                r2s, off[k] >= 0 ? (co * (int)d.r2_cstride + t) * 4 : kSentinel, 0, 0));
         }
-        if (i + 1 < nitems) stage_store(cur ^ 1);
-        if (last) {
-            __syncthreads();   // the previous tile's FIR pass is done with Y
-            write_y();
-            zero_acc();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float f = 0.f;
+#pragma unroll
+            for (int j = 0; j < F::NT; ++j) f = fmaf(tap[j], w[k + j], f);
+            float v = f + bias;
+            if (off[k] >= vlen) v = 0.f;
+            v = (v + v1[k]) * s1e;
+            v = (ga + fadd) * v + gb;
+            v = (v + v2[k]) * s2e;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ys,
+                                                  off[k] >= 0 ? (co * (int)d.y_cstride + off[k]) * 4 : kSentinel, 0, 0);
         }
-        __syncthreads();
-        if (last) fir_out(u0_of(i / nch));
     }
-    if constexpr (P != 0) ou_range_flag(d.status, omax, 1, lane);
 }
 
 // ---- tile table ------------------------------------------------------------
@@ -3286,8 +3252,7 @@ int launch_f(const ou_conv_desc& d, hipStream_t s)
     if (d.fir == 1 || d.fir == 3) {   // down / st_conv: K = cin frame in chunks of 16 channels x R phases
         const int mtiles = (d.m + 31) / 32;
         const int64_t a_mt_stride = (int64_t)((d.cin * d.frame + kCinAlign - 1) / kCinAlign * kCinAlign) * 32;
-        const int tpw = 1 << ((d.tile >> 8) & 3), ntn = (d.n_frames + F::BN - 1) / F::BN;
-        const dim3 grid((ntn + tpw - 1) / tpw, (mtiles + WM * MR - 1) / (WM * MR), d.batch);
+        const dim3 grid((d.n_frames + F::BN - 1) / F::BN, (mtiles + WM * MR - 1) / (WM * MR), d.batch);
         if constexpr (R == 4 || R == 8) {
             static bool sattr[2] = {false, false};
             if (d.fir == 3)
@@ -3303,8 +3268,7 @@ int launch_f(const ou_conv_desc& d, hipStream_t s)
     // up: K = cin in chunks of 32; P = 32 / R whole channels per packed m-tile
     const int mtiles = (d.m / R + F::CPT - 1) / F::CPT;
     const int64_t a_mt_stride = (int64_t)((d.cin + kCinAlign - 1) / kCinAlign * kCinAlign) * 32;
-    const int tpw = 1 << ((d.tile >> 8) & 3), ntn = (d.n_frames + F::BN - 3) / (F::BN - 2);
-    const dim3 grid((ntn + tpw - 1) / tpw, (mtiles + WM * MR - 1) / (WM * MR), d.batch);
+    const dim3 grid((d.n_frames + F::BN - 3) / (F::BN - 2), (mtiles + WM * MR - 1) / (WM * MR), d.batch);
     return d.prec == 1
                ? fir_launch(conv_fukernel<R, WM, WN, MR, NR, 1>, F::ULDS, grid, d, mtiles, a_mt_stride, attr[2], s)
                : fir_launch(conv_fukernel<R, WM, WN, MR, NR, 2>, F::ULDS, grid, d, mtiles, a_mt_stride, attr[3], s);
@@ -3599,7 +3563,7 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
                            d.fir, d.cin, d.frame, d.rout, d.kt);
         if (!(d.w_unscale > 0.f)) return ou_fail(-1, "conv: FIR mode needs the w_unscale of ou_conv_pack_split_nat");
         const int tile = d.tile >= 0 ? d.tile : (kFirBit | 2);
-        if (!(tile & kFirBit) || (tile & ~(kFirBit | kMajBit | 0x3ff)) || (tile & 0xff) >= kNumFTiles)
+        if (!(tile & kFirBit) || (tile & ~(kFirBit | kMajBit | 0xff)) || (tile & 0xff) >= kNumFTiles)
             return ou_fail(-2, "conv: FIR mode needs a FIR tile (tile 0x%x)", d.tile);
         ou_conv_desc dd = d;   // the kernels read their order bit from the tile
         dd.tile = tile;
@@ -3704,8 +3668,8 @@ extern "C" int ou_conv_pick_tile(const ou_conv_desc* d) { return d ? pick_tile_f
 extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int ou_conv_tile_ok(int kt, int tile)
 {
-    if (tile & kFirBit)   // FIR applied (ou_conv_desc.fir): shape, log2 tiles per workgroup (bits 8-9), m-major; one tap
-        return !(tile & ~(kFirBit | kMajBit | 0x3ff)) && (tile & 0xff) < kNumFTiles && kt == 1;
+    if (tile & kFirBit)   // FIR applied (ou_conv_desc.fir): shape (+ m-major order); one tap
+        return !(tile & ~(kFirBit | kMajBit | 0xff)) && (tile & 0xff) < kNumFTiles && kt == 1;
     if (tile & kSsBit)   // split-image input: shape = NR - 1 (+ m-major order)
         return !(tile & ~(kSsBit | kMajBit | 0xff)) && (tile & 0xff) < kNumSTiles && (kt == 1 || kt == 3 || kt == 5);
     if (tile & kRsBit)   // register-streamed: shape id (+ K slices, m-major order); LDS and chunks checked at launch

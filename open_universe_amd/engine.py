@@ -1046,9 +1046,8 @@ class ConvTuner:
         # workgroups per CU); elsewhere slices only add traffic
         small = -(-d.n_frames // 64) * -(-d.m // 64) * d.batch <= 1024
         ksl = (0, 1 << 12, 2 << 12, 3 << 12) if d.ks_ws and small else (0,)
-        if d.fir:   # the FIR kernels' shapes x tiles per workgroup (bits 8-9)
-            cands = [t | FIR_BIT | (k << 8) for t in range(16) for k in range(4)
-                     if lib.ou_conv_tile_ok(d.kt, t | FIR_BIT | (k << 8))]
+        if d.fir:   # the FIR-applied rate-change kernels' shapes only
+            cands = [t | FIR_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | FIR_BIT)]
         elif d.xs:   # a split-image input: the split-image kernel's shapes only
             cands = [t | L.SS_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | L.SS_BIT)]
         elif d.prec in (1, 2):

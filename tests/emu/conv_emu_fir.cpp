@@ -86,7 +86,7 @@ static int st_cases(int& n)
             d.n_frames = U; d.batch = B; d.y = y.data(); d.y_bstride = (int64_t)cout * U; d.y_cstride = U;
             d.rout = 1; d.out_len = U; d.valid_len = 1 << 30; d.bias = bias.data();
             d.prec = 1; d.w_unscale = unscale; d.xs_shift = 6; d.fir = 3;
-            d.tile = kFirBit | shape | ((shape % 4) << 8);   // 1, 2, 4, 8 tiles per workgroup
+            d.tile = kFirBit | shape;
             if (ou_conv(&d, nullptr) != 0) {
                 std::printf("st Rt %d shape %d: launch error %s\n", Rt, shape, ouhip_detail::err_buf());
                 ++bad;
@@ -220,7 +220,7 @@ int main(int argc, char** argv)
                 d.res2 = c.res2 ? r2.data() : nullptr; d.r2_bstride = d.y_bstride; d.r2_cstride = out_len; d.s2 = 0.5f;
                 d.prec = prec; d.w_unscale = unscale; d.xs_shift = s;
                 d.fir = c.dir; d.fir_taps = tap.data();
-                d.tile = kFirBit | shape | (shape == 3 ? kMajBit : 0) | ((shape % 4) << 8);   // 1 .. 8 tiles per workgroup
+                d.tile = kFirBit | shape | (shape == 3 ? kMajBit : 0);
                 if (down && c.sy && prec == 1) {
                     img.assign((size_t)c.B * (c.cout / 32) * rows * 64, 0x7e00);
                     d.sy = img.data(); d.sy_bstride = (int64_t)(c.cout / 32) * rows * 128; d.sy_rows = rows;
