@@ -2462,7 +2462,54 @@ __device__ __forceinline__ void fir_taps(const ou_conv_desc& d, float (&tap)[NT]
     for (int j = 0; j < NT; ++j) tap[j] = d.fir_taps[j];
 }
 
-template <int R, int WM, int WN, int MR, int NR, int P, int ST = 0>
+// The down / st_conv epilogue when the layer has no residuals and no FiLM (the
+// rate-change convs of the encoders and the st_convs): bias, zero-fill past
+// valid_len, the store and the optional split image -- a fraction of
+// conv_epilogue's registers, so more workgroups stay resident per CU.
+template <int MR, int NR>
+__device__ __forceinline__ void conv_epilogue_lean(const ou_conv_desc& d, int b, int mtb, int ub,
+                                                   floatx16 (&acc)[MR][NR], int lane)
+{
+    const int h = lane >> 5, l32 = lane & 31;
+    const int M = d.m;
+    const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)M * d.y_cstride * 4);
+    const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)M * 4 : 0);
+    const SplitOut so = split_ctx(d, b, M);
+    const int uend = min(d.f0 + d.n_frames, d.out_len);
+    float somax = 0.f;
+#pragma unroll
+    for (int mr = 0; mr < MR; ++mr) {
+        const int m0 = (mtb + mr) * 32 + 4 * h;   // rows m0 + (r & 3) + 8 (r >> 2)
+        float bias[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            bias[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, min(m0 + (r & 3) + 8 * (r >> 2), M - 1) * 4, 0, 0));
+#pragma unroll
+        for (int nr = 0; nr < NR; ++nr) {
+            const int u = ub + nr * 32 + l32;
+            const bool uok = u < uend;
+            const bool zero = u >= d.valid_len;
+            float sv[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + (r & 3) + 8 * (r >> 2);
+                const float v = zero ? 0.f : acc[mr][nr][r] + bias[r];
+                sv[r] = v;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ys,
+                                                      (uok && m < M) ? (m * (int)d.y_cstride + u) * 4 : kSentinel, 0, 0);
+            }
+            if (d.sy) {
+                const bool ok = (mtb + mr) * 32 < M && uok;
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    split_store4(so, m0 + 8 * g, u, ok, sv[4 * g], sv[4 * g + 1], sv[4 * g + 2], sv[4 * g + 3], somax);
+            }
+        }
+    }
+    if (d.sy) ou_range_flag(d.status, somax, 2, lane);
+}
+
+template <int R, int WM, int WN, int MR, int NR, int P, int ST = 0, int LEAN = 0>
 __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride)
 {
     using F = FCfg<R, WM, WN, MR, NR>;
@@ -2632,7 +2679,10 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 acc[i][j][r] = P == 1 ? fmaf(accx[i][j][r], sx, acc[i][j][r] * su) : acc[i][j][r] * su;
-    conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane);
+    if constexpr (LEAN)
+        conv_epilogue_lean<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane);
+    else
+        conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane);
 }
 
 template <int R, int WM, int WN, int MR, int NR, int P>
@@ -2804,6 +2854,13 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
         ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y, has_fm ? (int64_t)cout * 8 : 0);
     constexpr int NSG = (BNO * R + 3) / 4;   // 4-sample groups per channel
     constexpr int NW = (4 + 2 * R + 3) / 4 * 4;   // window floats read (16-B reads)
+    // 16-B residual loads and stores where the tile's first sample and every
+    // row start are 16-B aligned (uniform over the workgroup)
+    auto al4 = [&](const float* p, int64_t bst, int64_t cst) {
+        return !p || (((uintptr_t)p % 16) == 0 && bst % 4 == 0 && cst % 4 == 0);
+    };
+    const bool v4 = ((u0 * R) & 3) == 0 && al4(d.y, d.y_bstride, d.y_cstride) &&
+                    al4(d.res1, d.r1_bstride, d.r1_cstride) && al4(d.res2, d.r2_bstride, d.r2_cstride);
     for (int it = tid; it < F::UCH * NSG; it += 256) {
         const int cw = it / NSG, g = it - (it / NSG) * NSG;
         const int co = c0 + cw;
@@ -2820,6 +2877,26 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
         const float bias = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, cok ? co * 4 : kSentinel, 0, 0));
         const float ga = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, cok ? co * 4 : kSentinel, 0, 0));
         const float gb = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, cok ? (cout + co) * 4 : kSentinel, 0, 0));
+        if (v4 && cok && sig + 3 < BNO * R && t0 + 3 < tend) {   // a whole aligned group: 16-B accesses
+            const auto a1 = __builtin_amdgcn_raw_buffer_load_b128(r1s, (co * (int)d.r1_cstride + t0) * 4, 0, 0);
+            const auto a2 = __builtin_amdgcn_raw_buffer_load_b128(r2s, (co * (int)d.r2_cstride + t0) * 4, 0, 0);
+            float o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float f = 0.f;
+#pragma unroll
+                for (int j = 0; j < F::NT; ++j) f = fmaf(tap[j], w[k + j], f);
+                float v = f + bias;
+                if (t0 + k >= vlen) v = 0.f;
+                v = (v + __uint_as_float(a1[k])) * s1e;
+                v = (ga + fadd) * v + gb;
+                o[k] = (v + __uint_as_float(a2[k])) * s2e;
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(
+                ou_u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])}, ys,
+                (co * (int)d.y_cstride + t0) * 4, 0, 0);
+            continue;
+        }
         int off[4];
         float v1[4], v2[4];
 #pragma unroll
@@ -3253,14 +3330,22 @@ int launch_f(const ou_conv_desc& d, hipStream_t s)
         const int mtiles = (d.m + 31) / 32;
         const int64_t a_mt_stride = (int64_t)((d.cin * d.frame + kCinAlign - 1) / kCinAlign * kCinAlign) * 32;
         const dim3 grid((d.n_frames + F::BN - 1) / F::BN, (mtiles + WM * MR - 1) / (WM * MR), d.batch);
+        const bool lean = !d.res1 && !d.res2 && !d.film;   // bias (+ split image) only: the lean epilogue
         if constexpr (R == 4 || R == 8) {
             static bool sattr[2] = {false, false};
-            if (d.fir == 3)
-                return d.prec == 1 ? fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 1, 1>, F::DLDS, grid, d, mtiles,
+            if (d.fir == 3 && lean)
+                return d.prec == 1 ? fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 1, 1, 1>, F::DLDS, grid, d, mtiles,
                                                 a_mt_stride, sattr[0], s)
-                                   : fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 2, 1>, F::DLDS, grid, d, mtiles,
+                                   : fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 2, 1, 1>, F::DLDS, grid, d, mtiles,
                                                 a_mt_stride, sattr[1], s);
+            if (d.fir == 3) return ou_fail(-2, "conv: FIR mode 3 takes no residual / FiLM epilogue");
         }
+        if (d.fir == 3) return ou_fail(-2, "conv: FIR mode 3 needs rate 4 or 8 chunks");
+        static bool lattr[2] = {false, false};
+        if (lean)
+            return d.prec == 1
+                       ? fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 1, 0, 1>, F::DLDS, grid, d, mtiles, a_mt_stride, lattr[0], s)
+                       : fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 2, 0, 1>, F::DLDS, grid, d, mtiles, a_mt_stride, lattr[1], s);
         return d.prec == 1
                    ? fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 1>, F::DLDS, grid, d, mtiles, a_mt_stride, attr[0], s)
                    : fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 2>, F::DLDS, grid, d, mtiles, a_mt_stride, attr[1], s);

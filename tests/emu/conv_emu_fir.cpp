@@ -37,6 +37,7 @@ struct Case {
     int cin, cout, T, B;
     bool res1, res2, film, sy;
     int valid_cut;      // valid_len = full - cut
+    int crop;           // up: out_len = T R - crop (-1: 1 when R > 2)
 };
 
 // fir 3 (st_convs): a plain strided conv, kernel = stride = Rt, in the FIR
@@ -115,17 +116,19 @@ int main(int argc, char** argv)
     const int R = argc > 1 ? std::atoi(argv[1]) : 2;
     int bad = 0, n = 0;
     const Case cases[] = {
-        {1, 32, 64, 157, 2, false, false, true, true, 0},
-        {1, 16, 32, 29, 1, true, false, false, false, 1},
-        {2, 64, 32, 41, 2, true, false, false, false, 3},
-        {2, 32, 16, 13, 1, true, true, true, false, 0},
+        {1, 32, 64, 157, 2, false, false, true, true, 0, 0},
+        {1, 16, 32, 29, 1, true, false, false, false, 1, 0},
+        {1, 48, 96, 203, 2, false, false, false, true, 2, 0},   // bias only: the lean epilogue (+ split image)
+        {2, 64, 32, 41, 2, true, false, false, false, 3, -1},
+        {2, 32, 16, 13, 1, true, true, true, false, 0, -1},
+        {2, 32, 32, 40, 2, true, false, false, false, 0, 0},    // rows 16-B aligned: the 16-B epilogue
     };
     const std::vector<float> tap = binomial(2 * R + 1);
     const float slope = 0.25f;
     for (const Case& c : cases) {
         const bool down = c.dir == 1;
         const int U = down ? (c.T + R - 1) / R : c.T;          // frames (output frames down, input frames up)
-        const int out_len = down ? U : c.T * R - (R > 2 ? 1 : 0);
+        const int out_len = down ? U : c.T * R - (c.crop < 0 ? (R > 2 ? 1 : 0) : c.crop);
         const int full = down ? U : c.T * R;
         const int valid = full - c.valid_cut;
         const int s = 5 + R % 3;   // staging exponent

@@ -35,6 +35,15 @@ def layers(cfg):
         out.append((f"down{i}_r{r}", "down", c, 2 * c, r, t, B))
         out.append((f"up{i}_r{r}", "up", 2 * c, c, r, -(-t // r), B))
         t = -(-t // r)
+    # the conditioner's st_convs (condition.py:53-59): level i -> the bottleneck,
+    # kernel = stride = the product of the rates below level i (fir mode 3)
+    t, top = T, C * 2 ** len(rates)
+    for i in range(len(rates) - 1):
+        rt = 1
+        for r in rates[i:]:
+            rt *= r
+        out.append((f"st{i}_r{rt}", "st", C * 2 ** i, top, rt, t, B))
+        t = -(-t // rates[i])
     return out
 
 
@@ -53,13 +62,14 @@ def main():
         if a.only and a.only != name:
             continue
         g = torch.Generator().manual_seed(0)
-        shape = (cout, cin, r) if direction == "down" else (cin, cout, r)
+        shape = (cin, cout, r) if direction == "up" else (cout, cin, r)
         sd = {"p.conv.weight": torch.randn(shape, generator=g) * 0.1, "p.prelu.weight": torch.tensor([0.25]),
               "p.bias": torch.randn(cout, generator=g)}
-        spec = E.spec_down(sd, "p", r, True) if direction == "down" else E.spec_up(sd, "p", r, True)
+        spec = (E.spec_down(sd, "p", r, direction == "down") if direction in ("down", "st")
+                else E.spec_up(sd, "p", r, True))
         cw = E.make_conv(spec, dev, prec=a.prec)
         x = E.Act(torch.randn(B, cin, T, device=dev))
-        if direction == "down":
+        if direction != "up":
             y = E.new_act(B, cout, -(-T // r), dev)
             d = E.conv_desc(cw, x, y)
         else:
