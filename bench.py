@@ -48,6 +48,9 @@ FS = 16000
 CLIP_S = 8.0
 FP32_PEAK_TF = 157.3   # MI355X dense FP32 matrix peak (MI355X_MICROARCH.md)
 F16_PEAK_TF = 2516.6   # dense F16/BF16 MFMA peak; split-f16 spends 3 MFMAs per f32 MAC
+# the kernels of the conv stack (roofline.traffic sums their PMC bytes)
+CONV_STACK_KERNELS = ("conv_kernel", "conv_rkernel", "conv_skernel", "conv_rreduce", "conv_fdkernel", "conv_fukernel",
+                      "block_kernel")
 HBM_PEAK = 8000.0      # GB/s
 
 
@@ -492,7 +495,7 @@ def main():
                 with open(args.traffic_json) as fh:
                     pmc = json.load(fh)
                 rows = [r for k, r in pmc.get("kernels", {}).items()
-                        if k in ("conv_kernel", "conv_rkernel", "conv_skernel", "conv_rreduce", "block_kernel")]
+                        if k in CONV_STACK_KERNELS]
                 lib_now = lib_sha16()
                 if pmc.get("lib_sha16") != lib_now:
                     # counters of another build of the kernels: not quoted
@@ -523,8 +526,9 @@ def main():
             out["roofline"] = {
                 **rl, "traffic": traffic,
                 "traffic_source": tsrc,
-                "kernel": "conv stack: ou_conv (conv_kernel, conv_rkernel + conv_rreduce, conv_skernel) + fused "
-                          "ConvBlock ou_block (block_kernel), all launches of one enhance",
+                "kernel": "conv stack: ou_conv (conv_kernel, conv_rkernel + conv_rreduce, conv_skernel, the "
+                          "FIR-applied rate-change conv_fdkernel / conv_fukernel) + fused ConvBlock ou_block "
+                          "(block_kernel), all launches of one enhance",
                 "launches": prof["n_conv"],
                 "fused_block_launches": prof["n_block"],
                 "avg_launch_ms": round(prof["conv_ms"] / prof["n_conv"], 5),

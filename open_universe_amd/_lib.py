@@ -479,7 +479,7 @@ class Program:
         if op == OP_CONV:
             self.info.append({"m": desc.m, "cin": desc.cin, "frame": desc.frame, "kt": desc.kt,
                               "n": desc.n_frames, "b": desc.batch, "rout": desc.rout,
-                              "tile": desc.tile})
+                              "tile": desc.tile, "fir": desc.fir})
         elif op == OP_GRU:
             self.info.append({"H": desc.hidden, "T": desc.steps, "b": desc.batch})
         elif op == OP_BLOCK:

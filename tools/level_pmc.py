@@ -32,7 +32,8 @@ import sys
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, HERE)
 
-CONV_KERNELS = ("conv_kernel", "conv_rkernel", "conv_pkernel", "conv_wkernel", "conv_rreduce", "block_kernel")
+CONV_KERNELS = ("conv_kernel", "conv_rkernel", "conv_skernel", "conv_pkernel", "conv_wkernel", "conv_rreduce",
+                "conv_fdkernel", "conv_fukernel", "block_kernel")
 HBM = 8000.0e9
 PEAK = {0: 157.3e12, 1: 2516.6e12 / 3, 2: 2516.6e12}
 
@@ -119,7 +120,7 @@ def label(r):
         tag = "+down" if r.get("rate") else ("+in" if r.get("in") else ("+head" if r.get("head") else ""))
         return f"block C{r['C']}{tag} n{r['n']}"
     return f"conv m{r['m']} cin{r['cin']} fr{r['frame']} k{r['kt']} n{r['n']}" + (
-        f" rout{r['rout']}" if r.get("rout") else "")
+        f" rout{r['rout']}" if r.get("rout") else "") + (f" fir{r['fir']}" if r.get("fir") else "")
 
 
 def analyze(a):
