@@ -748,7 +748,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
 #pragma unroll
                 for (int mr = 0; mr < MR; ++mr)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) hv[mr][nr][r] = in_conv(row(mr, r), xl, xm, xr);
+                    for (int r = 0; r < 16; ++r) hv[mr][nr][r] = in_conv(rowc(mr, r), xl, xm, xr);
             } else {
                 // frames outside [h0, h1) (a chunk's caller has not produced
                 // them) feed no stored output; zero, so that kEpiDown's
@@ -827,7 +827,7 @@ __global__ __launch_bounds__(block_threads<C>(), block_min_wgs<C>()) void block_
                         v = (v + hv[mr][nr][r]) * d.s_res;
                         v = v >= 0.f ? v : v * hd.slope1;
                         v = v >= 0.f ? v : v * hd.slope2;
-                        if (w < F + 2) Y[w * YS + row(mr, r)] = inside ? v : 0.f;
+                        if (w < F + 2 && rok(mr, r)) Y[w * YS + row(mr, r)] = inside ? v : 0.f;
                     }
                 }
             __syncthreads();
@@ -1008,7 +1008,7 @@ int launch_epi(const ou_block_desc& d, hipStream_t s)
     case kEpiCond: return launch<C, NT, P, kEpiCond>(d, s);
     case kEpiRes2: return launch<C, NT, P, kEpiRes2>(d, s);
     }
-    if constexpr (C == 32) {   // the score network's ends (32 channels at level 0)
+    if constexpr (C == 32 || C == 48) {   // the score network's ends (32 / 48 channels at level 0)
         switch (epi) {
         case kEpiFilm | kEpiIn: return launch<C, NT, P, kEpiFilm | kEpiIn>(d, s);
         case kEpiFilm | kEpiSc | kEpiHead: return launch<C, NT, P, kEpiFilm | kEpiSc | kEpiHead>(d, s);

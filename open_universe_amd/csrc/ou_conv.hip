@@ -3332,13 +3332,17 @@ int launch_f(const ou_conv_desc& d, hipStream_t s)
         const dim3 grid((d.n_frames + F::BN - 1) / F::BN, (mtiles + WM * MR - 1) / (WM * MR), d.batch);
         const bool lean = !d.res1 && !d.res2 && !d.film;   // bias (+ split image) only: the lean epilogue
         if constexpr (R == 4 || R == 8) {
-            static bool sattr[2] = {false, false};
+            static bool sattr[4] = {false, false, false, false};
             if (d.fir == 3 && lean)
                 return d.prec == 1 ? fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 1, 1, 1>, F::DLDS, grid, d, mtiles,
                                                 a_mt_stride, sattr[0], s)
                                    : fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 2, 1, 1>, F::DLDS, grid, d, mtiles,
                                                 a_mt_stride, sattr[1], s);
-            if (d.fir == 3) return ou_fail(-2, "conv: FIR mode 3 takes no residual / FiLM epilogue");
+            if (d.fir == 3)   // the st_convs' running sum: residuals in the epilogue
+                return d.prec == 1 ? fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 1, 1, 0>, F::DLDS, grid, d, mtiles,
+                                                a_mt_stride, sattr[2], s)
+                                   : fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 2, 1, 0>, F::DLDS, grid, d, mtiles,
+                                                a_mt_stride, sattr[3], s);
         }
         if (d.fir == 3) return ou_fail(-2, "conv: FIR mode 3 needs rate 4 or 8 chunks");
         static bool lattr[2] = {false, false};

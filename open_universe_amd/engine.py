@@ -561,6 +561,11 @@ def fuse_blocks_enabled():
     return os.environ.get("OUHIP_FUSE_BLOCKS", "1") != "0"
 
 
+# channel counts of the score network's level-0 blocks whose ou_block
+# instantiations take the input conv (kEpiIn) and the head (kEpiHead)
+ENDS_C = (32, 48)
+
+
 def fuse_ends_enabled():
     """OUHIP_FUSE_ENDS=0 keeps the score input conv and head as their own launches."""
     import os
@@ -885,11 +890,11 @@ def block_desc(bw: BlockW, h: Act, out: Act, descs, sc: Act = None, film=0, film
     d._fw = fw   # split-image linking (split_hook)
     if x_in is not None:
         xa, scale, w_in, b_in = x_in
-        assert bw.C == 32 and xa.C == 1 and xa.T == h.T and xa.B >= h.B
+        assert bw.C in ENDS_C and xa.C == 1 and xa.T == h.T and xa.B >= h.B
         d.x, d.x_bstride, d.in_scale = xa.ptr, xa.bs, scale or 0
         d.w_in, d.b_in = w_in.data_ptr(), b_in.data_ptr()
     if head is not None:
-        assert bw.C == 32 and head.length == h.T and head.channels == bw.C
+        assert bw.C in ENDS_C and head.length == h.T and head.channels == bw.C
         d.head = head
     if e_out is not None:
         dn = bw.down
@@ -1428,7 +1433,7 @@ class Engine:
         # input conv (score.py:244-246, 285)
         prog.label = "score enc"
         d_in = conv_desc(self.s_input, x, bufs["E0"], in_scale=in_scale)
-        fuse_in = (self.s_enc[0].fused is not None and self.s_enc[0].C == 32 and self.s_in_fusable
+        fuse_in = (self.s_enc[0].fused is not None and self.s_enc[0].C in ENDS_C and self.s_in_fusable
                    and fuse_ends_enabled())
         if not fuse_in:
             prog.add(L.OP_CONV, d_in)
@@ -1463,7 +1468,7 @@ class Engine:
             if before_level is not None:
                 before_level(l)
             last = l == n_lvl - 1
-            fuse_head = (last and head is not None and bw.fused is not None and bw.C == 32
+            fuse_head = (last and head is not None and bw.fused is not None and bw.C in ENDS_C
                          and fuse_ends_enabled())
             rec_block(prog, bw, bufs[f"V{i}"], bufs[f"A{i}"], bufs[f"A{i}"], bufs[f"B{i}"],
                       film=fb(n_lvl + l), film_bs=film_bs, sc=sc_list[l], head=head if fuse_head else None)
@@ -1639,7 +1644,7 @@ class Engine:
                     # line, or on lane 0 behind a wait) must not change its
                     # bits -- enhance_many's plans keep it in line
                     dst._no_split = True
-                    prog.add(L.OP_CONV, dst)
+                    add_conv(prog, dst)   # the FIR kernels' st_conv form (fir 3) where it is faster
                     prog.label = f"cond enc L{i}"
                     if st_lane is not None:
                         set_lane(prog, side)

@@ -149,11 +149,13 @@ int main(int argc, char** argv)
                 cases.push_back({C, T, 1, prec, true, true, false, false, false, false, 0, 0});
                 cases.push_back({C, T, 2, prec, false, false, true, false, false, false, 0, 0});
                 cases.push_back({C, T, 1, prec, false, false, false, true, false, false, 0, 0});
-                if (C == 32) {   // the score network's ends and the encoder rate changes
+                if (C == 32 || C == 48) {   // the score network's ends
                     cases.push_back({C, T, 2, prec, true, false, false, false, true, false, 0, 0});
                     cases.push_back({C, T, 1, prec, false, false, false, false, true, false, 0, 0});
                     cases.push_back({C, T, 2, prec, true, true, false, false, false, true, 0, 0});
                     cases.push_back({C, T, 1, prec, false, false, false, false, false, true, 0, 0});
+                }
+                if (C == 32) {   // the encoder rate changes
                     for (int kt : {3, 1}) {
                         cases.push_back({C, T, 2, prec, false, false, false, false, false, false, 2, kt});
                         cases.push_back({C, T, 1, prec, true, false, false, false, false, false, 2, kt});

@@ -49,9 +49,11 @@ static int st_cases(int& n)
     const int rts[] = {20, 40, 24};
     for (int Rt : rts) {
         const int cin = 32, cout = 64, B = 2, T = 7 * Rt + 5, U = (T + Rt - 1) / Rt;
-        std::vector<float> w((size_t)cout * cin * Rt), x((size_t)B * cin * T), bias(cout);
-        for (auto* v : {&w, &x, &bias})
+        std::vector<float> w((size_t)cout * cin * Rt), x((size_t)B * cin * T), bias(cout),
+            r1((size_t)B * cout * U), r2(r1.size());
+        for (auto* v : {&w, &x, &bias, &r1, &r2})
             for (auto& e : *v) e = rnd();
+        const bool res = Rt == 40;   // the running st_conv sum: two residuals (the generic epilogue)
         std::vector<double> ref((size_t)B * cout * U);
         for (int b = 0; b < B; ++b)
             for (int co = 0; co < cout; ++co)
@@ -65,7 +67,8 @@ static int st_cases(int& n)
                             v = v >= 0 ? v : v * slope;
                             acc += (double)w[((size_t)co * cin + ci) * Rt + ph] * v;
                         }
-                    ref[((size_t)b * cout + co) * U + u] = acc;
+                    const size_t o = ((size_t)b * cout + co) * U + u;
+                    ref[o] = res ? (acc + r1[o] + r2[o]) : acc;
                 }
         const int keff = cin * Rt;
         std::vector<float> wl((size_t)cout * keff);
@@ -87,6 +90,10 @@ static int st_cases(int& n)
             d.n_frames = U; d.batch = B; d.y = y.data(); d.y_bstride = (int64_t)cout * U; d.y_cstride = U;
             d.rout = 1; d.out_len = U; d.valid_len = 1 << 30; d.bias = bias.data();
             d.prec = 1; d.w_unscale = unscale; d.xs_shift = 6; d.fir = 3;
+            if (res) {
+                d.res1 = r1.data(); d.r1_bstride = d.y_bstride; d.r1_cstride = U; d.s1 = 1.f;
+                d.res2 = r2.data(); d.r2_bstride = d.y_bstride; d.r2_cstride = U; d.s2 = 1.f;
+            }
             d.tile = kFirBit | shape;
             if (ou_conv(&d, nullptr) != 0) {
                 std::printf("st Rt %d shape %d: launch error %s\n", Rt, shape, ouhip_detail::err_buf());

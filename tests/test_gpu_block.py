@@ -133,20 +133,22 @@ def test_block_range_flag():
     assert int(status[1]) == 1
 
 
-def test_score_ends_fused_equal_unfused(monkeypatch):
+@pytest.mark.parametrize("name", ["pp16", "pp24"])
+def test_score_ends_fused_equal_unfused(monkeypatch, name):
     """The score input conv fused into the first encoder block and the head
     (EDM wrapper + sampler update) fused into the last decoder block give the
     same enhance as separate ou_conv / ou_head launches (f32 summation-order
-    level), and the fused program has fewer launches."""
+    level), and the fused program has fewer launches.  PP24's level-0 blocks
+    have 48 channels: padded MFMA rows in the fused input conv and head."""
     from conftest import golden_state_dict, load_golden
     from open_universe_amd.configs import get_config
     from open_universe_amd.networks.universe import UniverseGAN
 
-    d = load_golden("pp16")
+    d = load_golden(name)
     outs, nops = {}, {}
     for fuse in ("1", "0"):
         monkeypatch.setenv("OUHIP_FUSE_ENDS", fuse)
-        cfg = get_config("pp16", None)
+        cfg = get_config(name, None)
         m = UniverseGAN(**{k: v for k, v in cfg.items() if k != "_target_"})
         m.load_state_dict(golden_state_dict(d), strict=False)
         m = m.to(DEV).eval()

@@ -53,6 +53,9 @@ def main():
     ap.add_argument("--prec", type=int, default=1)
     ap.add_argument("--only", default=None)
     ap.add_argument("--folded", type=int, default=1, help="0: skip tuning the folded form (slow at C4 sizes)")
+    ap.add_argument("--tile", type=lambda v: int(v, 0), default=None,
+                    help="with --only: run the FIR form on this tile --reps times, no tuning (PMC passes)")
+    ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     dev = "cuda:0"
     E.enable_autotune(True)
@@ -75,6 +78,22 @@ def main():
         else:
             y = E.new_act(B, cout, r * T, dev)
             d = E.conv_desc(cw, x, y, n_frames=T, valid_len=r * T, res1=y, s1=float(E.NF2))
+        if a.tile is not None:   # a fixed FIR tile, launched --reps times (counter passes)
+            f = E.fir_desc(d)
+            f.tile = a.tile
+            lib = E.L.load()
+            st = torch.cuda.current_stream().cuda_stream
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            E.L.run_now(E.L.OP_CONV, f, st)
+            e0.record()
+            for _ in range(a.reps):
+                E.L.run_now(E.L.OP_CONV, f, st)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / a.reps
+            print(f"{name:12s} FIR tile 0x{a.tile:x}: {ms * 1e3:9.1f} us, {d._flops / 1e9 / ms:6.1f} TF/s, "
+                  f"{d._bytes / 1e9 / ms:6.2f} TB/s")
+            continue
         tp, ms_p = tuner.pick(d) if a.folded else (-1, float("nan"))
         if cw.fir is None:
             print(f"{name:12s} folded {ms_p * 1e3:9.1f} us  (no FIR form)")

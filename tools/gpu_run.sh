@@ -18,6 +18,7 @@
 #   convsplit[:L,..] tools/conv_bench.py --split: the split-image kernel on the deep-level layers
 #   convsplitlib:A,B the same on the k3 layers, in-tree library then variants A, B (stamps: --sstamps)
 #   fir:CFG          tools/fir_bench.py: folded vs FIR-applied rate-change convs at CFG
+#   sqfir:CFG/L/T    SQ counters (two rocprofv3 --pmc passes) of FIR layer L on tile T
 #
 #   e.g. tools/gpu_run.sh r04k profile:c2 critical bench:c1 bench:c3 bench:c5
 set -o pipefail
@@ -103,6 +104,22 @@ for step in "$@"; do
         timeout -k 10 400 python3 tools/fir_bench.py --config "${arg:-c4}" --folded $fo > "$O/fir_${TAG}_${arg:-c4}.txt" 2>&1 \
             || { tail -20 "$O/fir_${TAG}_${arg:-c4}.txt"; exit 1; }
         grep -v "ou tune\|amdgpu" "$O/fir_${TAG}_${arg:-c4}.txt" ;;
+    sqfir)   # SQ counters of one FIR-kernel layer on a fixed tile: ARG = CFG/LAYER/TILE (e.g. c4/up0_r2/0x20000)
+        IFS=/ read -r cfg lay til <<< "$arg"
+        out="$O/sqfir_${TAG}_${lay}"
+        ( cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY \
+              SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
+              -d "${out}_a" -o pmc -- python3 "$ROOT/tools/fir_bench.py" --config "$cfg" --only "$lay" --tile "$til" \
+              --reps 10 > "${out}_a.txt" 2>&1 ) || { tail -20 "${out}_a.txt"; exit 1; }
+        ( cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
+              SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv \
+              -d "${out}_b" -o pmc -- python3 "$ROOT/tools/fir_bench.py" --config "$cfg" --only "$lay" --tile "$til" \
+              --reps 10 > "${out}_b.txt" 2>&1 ) || { tail -20 "${out}_b.txt"; exit 1; }
+        k=conv_fdkernel; [[ "$lay" == up* ]] && k=conv_fukernel
+        { grep -v amdgpu "${out}_a.txt" | tail -1
+          python3 tools/pmc_avg.py "$(find "${out}_a" -name '*counter_collection.csv' | head -n1)" $k
+          python3 tools/pmc_avg.py "$(find "${out}_b" -name '*counter_collection.csv' | head -n1)" $k; } > "$out.txt"
+        cat "$out.txt" ;;
     convlib)   # tools/conv_bench.py on the deep-level layers: in-tree library vs variant ARG
         for lib in main "$arg"; do
             ( [ "$lib" = main ] || export OUHIP_LIB="$ROOT/open_universe_amd/variants/libouhip_$lib.so"
