@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define OUHIP_ABI_VERSION 7
+#define OUHIP_ABI_VERSION 8
 
 int ou_abi_version(void);
 const char* ou_last_error(void);
@@ -150,9 +150,12 @@ typedef struct ou_conv_desc {
      * R is 2, 3, 4, 5 or 8 (fir 1 / 2); kt 1, pad 0, shift 0, no in_scale, no
      * xs; prec 1 or 2; weights w_logical[m'][k] packed by
      * ou_conv_pack_split_nat(kt 1):
-     *   fir 1, 3: m' = co (m = cout rows),
-     *          k = (cb R + ph) 16 + c  for input channel ci = 16 cb + c
-     *          (cin % 16 == 0) and conv tap ph;
+     *   fir 1, 3: m' = co (m = cout rows), K in chunks of 16 channels x Q
+     *          phases (Q = R for fir 1; 8 if R % 8 == 0 else 4 for fir 3),
+     *          channel-major inside a chunk:
+     *          k = ((cb R / Q + s) 16 + c) Q + p  for input channel
+     *          ci = 16 cb + c (cin % 16 == 0) and conv tap ph = s Q + p
+     *          (fir 1: k = ci R + ph, the frame view's order);
      *   fir 2: every 32-row m-tile holds P = 32 / R whole channels, row
      *          m' = 32 (co / P) + (co % P) R + ph (rows past P R zero), so
      *          ceil(cout / P) * 32 packed rows; k = ci (cin % 32 == 0).

@@ -12,7 +12,7 @@ from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OUHIP_LIB", os.path.join(_HERE, "libouhip.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 fp = c_void_p  # device pointers are passed as integers
 

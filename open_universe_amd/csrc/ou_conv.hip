@@ -451,11 +451,13 @@ __device__ __forceinline__ void conv_epi_store(const ou_conv_desc& d, const EpiC
 // The one-phase epilogue of the chunked / persistent kernels: per m-tile
 // and frame tile, its loads then its stores (live ranges stay one tile's
 // worth -- those kernels hold MR x NR tiles).
+// col: the lane's frame within its 32-frame tile (default lane & 31; the FIR
+// down kernel's B rows are a permutation of the frames, conv_fdkernel)
 template <int MR, int NR>
 __device__ __forceinline__ void conv_epilogue(const ou_conv_desc& d, int b, int mtb, int ub,
-                                              floatx16 (&acc)[MR][NR], int lane)
+                                              floatx16 (&acc)[MR][NR], int lane, int col = -1)
 {
-    const int h = lane >> 5, l32 = lane & 31;
+    const int h = lane >> 5, l32 = col >= 0 ? col : lane & 31;
     // Branch-free: every out-of-range element gets a sentinel offset, so its
     // buffer load returns 0 and its buffer store is dropped.  All residual
     // loads of the tile are issued before any arithmetic, so their latency is
@@ -2406,8 +2408,9 @@ __global__ __launch_bounds__(256 + 64 * kWsLoaders) void conv_wkernel(ou_conv_de
 //     thread (channel c, frame group g) holds F R + 2 R consecutive PReLU'd
 //     samples of its channel in registers, slides the FIR over them and
 //     writes the F R results, split into f16 hi / lo, into the B image
-//     [frame][phase][16 channels] (row stride 16 R + 8 halves: an odd number
-//     of 16-B slots, so the ds_read_b128 fragment reads are conflict-free);
+//     [frame][16 channels][phase] (channel-major K: a frame's R phases are one
+//     16 / 8 / 4-B store; row stride 16 R + 8 halves, an odd number of 16-B
+//     slots, so the ds_read_b128 fragment reads are conflict-free);
 //   conv_fukernel (up): the workgroup computes the transposed conv over BN
 //     frames (one frame of halo each side: BN - 2 output frames), keeping
 //     P = 32 / R whole channels per 32-row m-tile (packed rows 32 (co / P) +
@@ -2468,9 +2471,9 @@ __device__ __forceinline__ void fir_taps(const ou_conv_desc& d, float (&tap)[NT]
 // conv_epilogue's registers, so more workgroups stay resident per CU.
 template <int MR, int NR>
 __device__ __forceinline__ void conv_epilogue_lean(const ou_conv_desc& d, int b, int mtb, int ub,
-                                                   floatx16 (&acc)[MR][NR], int lane)
+                                                   floatx16 (&acc)[MR][NR], int lane, int col)
 {
-    const int h = lane >> 5, l32 = lane & 31;
+    const int h = lane >> 5, l32 = col;
     const int M = d.m;
     const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)M * d.y_cstride * 4);
     const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)M * 4 : 0);
@@ -2535,7 +2538,8 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
     float tap[F::NT];
     if constexpr (!ST) fir_taps<F::NT>(d, tap);
 
-    // ---- weights: chunk q, step s -> 16-channel group q R + s = cb Rt + ph
+    // ---- weights: chunk q (16 channels x R phases, channel-major), step s =
+    // its K values 16 s .. 16 s + 15
     const __amdgpu_buffer_rsrc_t ars = ou_rsrc(d.w, (int64_t)mtiles * a_mt_stride * 4);
     half8_t ra[R][MR][2];
     auto load_a = [&](int q, int s) {   // q uniform, clamped (a reload past the end is never used)
@@ -2552,8 +2556,17 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
 
     // ---- staging: thread (channel sc of the chunk, frame group sg) owns
     // frames n0 + sg F .. + F - 1; its window is samples [s0, s0 + (F + 2) R)
-    // (ST: the R-sample runs (n0 + sg F + f) Rt + sub R .. of its F frames f)
-    const int sc = tid >> 4, sg = tid & 15;
+    // (ST: the R-sample runs (n0 + sg F + f) Rt + sub R .. of its F frames f).
+    // Frame groups fastest (neighbouring lanes read neighbouring windows); a
+    // frame's R phases are R consecutive halves sc R .. of its B row
+    // (channel-major K: one 16 / 8 / 4-B store), and the rows interleave the
+    // groups inside each 32-frame tile -- frame 32 t + g F + f (group g of the
+    // S = 32 / F groups of tile t) at row 32 t + f S + g -- so the lanes of a
+    // store hit consecutive rows (odd 16-B-slot stride: <= 2-way conflicts).
+    // The MFMA column of B row 32 t + j is frame 32 t + FCOL(j) (epilogue).
+    const int sg = tid & 15, sc = tid >> 4;
+    constexpr int SG = 32 / F::DF;   // frame groups per 32-frame tile
+    const int srow = (sg / SG) * 32 + sg % SG;
     const int64_t xc = d.x_cstride;
     const __amdgpu_buffer_rsrc_t xrs = ou_rsrc(d.x + (int64_t)b * d.x_bstride, (int64_t)d.cin * xc * 4);
     const int s0 = ST ? (n0 + sg * F::DF) * Rt : (n0 + sg * F::DF - 1) * R;
@@ -2592,28 +2605,50 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
         }
     };
     float omax = 0.f;
+    // stores of VW consecutive halves (a frame's phases): 16 / 8 / 4 / 2 B
+    constexpr int VW = R % 8 == 0 ? 8 : R % 4 == 0 ? 4 : R % 2 == 0 ? 2 : 1;
+    auto store_h = [](_Float16* p, const _Float16 (&v)[VW]) {
+        if constexpr (VW == 8) {
+            *(half8_t*)p = half8_t{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+        } else if constexpr (VW == 4) {
+            *(ou_h4_t*)p = ou_h4_t{v[0], v[1], v[2], v[3]};
+        } else if constexpr (VW == 2) {
+            *(uint32_t*)p = (uint32_t)__builtin_bit_cast(uint16_t, v[0]) |
+                            ((uint32_t)__builtin_bit_cast(uint16_t, v[1]) << 16);
+        } else {
+            *p = v[0];
+        }
+    };
     auto stage_store = [&](int buf) {
-        _Float16* bh = ldsh + buf * 2 * F::DPLANE + sg * F::DF * F::DRS + sc;
+        _Float16* bh = ldsh + buf * 2 * F::DPLANE + srow * F::DRS + sc * R;
 #pragma unroll
         for (int e = 0; e < WIN; ++e) {
             const float v = xw[e] * xsc;   // 2^-s: exact
             xw[e] = v >= 0.f ? v : v * slope;
         }
 #pragma unroll
-        for (int i = 0; i < F::DF * R; ++i) {
-            float f = 0.f;
-            if constexpr (ST) {
-                f = xw[i];
-            } else {
+        for (int f = 0; f < F::DF; ++f)
 #pragma unroll
-                for (int j = 0; j < F::NT; ++j) f = fmaf(tap[j], xw[i + j], f);
+            for (int p0 = 0; p0 < R; p0 += VW) {
+                _Float16 hv[VW], lv[VW];
+#pragma unroll
+                for (int j = 0; j < VW; ++j) {
+                    const int i = f * R + p0 + j;
+                    float v = 0.f;
+                    if constexpr (ST) {
+                        v = xw[i];
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < F::NT; ++t) v = fmaf(tap[t], xw[i + t], v);
+                    }
+                    omax = fmaxf(omax, __builtin_fabsf(v));
+                    hv[j] = (_Float16)v;
+                    lv[j] = (_Float16)((v - (float)hv[j]) * 2048.f);
+                }
+                _Float16* o = bh + f * SG * F::DRS + p0;
+                store_h(o, hv);
+                if constexpr (P == 1) store_h(o + F::DPLANE, lv);
             }
-            omax = fmaxf(omax, __builtin_fabsf(f));
-            const _Float16 hi = (_Float16)f;
-            const int o = (i / R) * F::DRS + (i % R) * 16;
-            bh[o] = hi;
-            if constexpr (P == 1) bh[F::DPLANE + o] = (_Float16)((f - (float)hi) * 2048.f);
-        }
     };
 
     floatx16 acc[MR][NR];
@@ -2632,7 +2667,7 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
 #pragma unroll
                 for (int r = 0; r < 16; ++r) accx[i][j][r] = 0.f;
     }
-    // B fragments of (buffer, phase s): row wn 32 NR + nr 32 + l32, halves s 16 + 8 h
+    // B fragments of (buffer, step s): row wn 32 NR + nr 32 + l32, halves s 16 + 8 h
     const _Float16* bb = ldsh + (wn * 32 * NR + l32) * F::DRS + 8 * h;
     auto mfma_step = [&](int buf, int s) {
         half8_t bq[NR], bl[NR];
@@ -2679,10 +2714,11 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 acc[i][j][r] = P == 1 ? fmaf(accx[i][j][r], sx, acc[i][j][r] * su) : acc[i][j][r] * su;
+    const int col = (l32 % SG) * F::DF + l32 / SG;   // FCOL: this lane's frame in its 32-frame tile
     if constexpr (LEAN)
-        conv_epilogue_lean<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane);
+        conv_epilogue_lean<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane, col);
     else
-        conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane);
+        conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane, col);
 }
 
 template <int R, int WM, int WN, int MR, int NR, int P>

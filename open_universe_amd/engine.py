@@ -423,6 +423,23 @@ def spec_plain(sd, p, k, slope=1.0):
                     ref_macs=float(w.size))
 
 
+def fir_chunk(mode, r):
+    """Phases per K chunk of the down-type FIR kernels (conv_fdkernel): the
+    whole frame for mode 1, 8 (or 4) of the st_convs' r phases for mode 3 --
+    the device's choice in ou_conv (ou_conv.hip)."""
+    return r if mode == 1 else (8 if r % 8 == 0 else 4)
+
+
+def fir_k_order(w, mode, r):
+    """(cout, cin, r) strided-conv weights -> (cout, cin r) in conv_fdkernel's
+    K order (include/ouhip.h): chunks of 16 channels x R = fir_chunk(mode, r)
+    phases, channel-major inside a chunk, k = ((cb r / R + sub) 16 + c) R + p
+    for ci = 16 cb + c, phase sub R + p.  Mode 1 (R = r): k = ci r + ph."""
+    cout, cin, _ = w.shape
+    R = fir_chunk(mode, r)
+    return w.reshape(cout, cin // 16, 16, r // R, R).transpose(0, 1, 3, 2, 4).reshape(cout, cin * r)
+
+
 def spec_down(sd, p, r, antialias):
     """Strided PReLU_Conv(C, 2C, r, stride=r) (blocks.py:203-231, 268-275).
     Frame view: channel c' = ci*r + p.  With anti-aliasing the 2r+1-tap
@@ -438,17 +455,15 @@ def spec_down(sd, p, r, antialias):
         wl = wf.reshape(cout, cin, 3, r).transpose(0, 1, 3, 2).reshape(cout, cin * r, 3)
         fir = None
         if cin % 16 == 0 and r in FIR_RATES:
-            # unfolded, K order k = (cb r + ph) 16 + c for ci = 16 cb + c (include/ouhip.h)
-            wu = w.reshape(cout, cin // 16, 16, r).transpose(0, 1, 3, 2).reshape(cout, cin * r)
-            fir = (1, r, wu, dsp.binomial_taps(2 * r + 1))
+            # unfolded, in the frame view's K order k = ci r + ph (include/ouhip.h)
+            fir = (1, r, fir_k_order(w, 1, r), dsp.binomial_taps(2 * r + 1))
         return ConvSpec(wl, cin, r, 1, 1, _slope(sd, p), _bias(sd, p + ".bias"),
                         ref_macs=float(cout * cin * r + cin * (2 * r + 1) * r), fir=fir)
     fir = None
     if cin % 16 == 0 and r % 4 == 0:
         # the wide strided convs (st_convs, rates 20 .. 240) in the FIR kernels'
         # K order without a FIR (ou_conv_desc.fir 3): each input sample read once
-        wu = w.reshape(cout, cin // 16, 16, r).transpose(0, 1, 3, 2).reshape(cout, cin * r)
-        fir = (3, r, wu, np.ones(1, np.float32))
+        fir = (3, r, fir_k_order(w, 3, r), np.ones(1, np.float32))
     return ConvSpec(w.reshape(cout, cin * r, 1), cin, r, 0, 1, _slope(sd, p),
                     _bias(sd, p + ".conv.bias"), ref_macs=float(cout * cin * r), fir=fir)
 

@@ -71,11 +71,13 @@ static int st_cases(int& n)
                     ref[o] = res ? (acc + r1[o] + r2[o]) : acc;
                 }
         const int keff = cin * Rt;
+        const int R = Rt % 8 == 0 ? 8 : 4;   // phases per K chunk (ou_conv)
         std::vector<float> wl((size_t)cout * keff);
         for (int co = 0; co < cout; ++co)
             for (int ci = 0; ci < cin; ++ci)
                 for (int ph = 0; ph < Rt; ++ph)
-                    wl[(size_t)co * keff + ((ci / 16) * Rt + ph) * 16 + ci % 16] = w[((size_t)co * cin + ci) * Rt + ph];
+                    wl[(size_t)co * keff + (((ci / 16) * (Rt / R) + ph / R) * 16 + ci % 16) * R + ph % R] =
+                        w[((size_t)co * cin + ci) * Rt + ph];
         std::vector<float> packed(ou_conv_packed_size(cout, keff, 1, 0));
         float unscale = 0.f;
         ou_conv_pack_split_nat(wl.data(), cout, keff, 1, packed.data(), &unscale);
@@ -199,7 +201,7 @@ int main(int argc, char** argv)
             for (int co = 0; co < c.cout; ++co)
                 for (int ci = 0; ci < c.cin; ++ci)
                     for (int ph = 0; ph < R; ++ph)
-                        wl[(size_t)co * keff + ((ci / 16) * R + ph) * 16 + ci % 16] = W(co, ci, ph);
+                        wl[(size_t)co * keff + ci * R + ph] = W(co, ci, ph);
         } else {
             const int P = 32 / R;
             mrows = (c.cout + P - 1) / P * 32, keff = c.cin;

@@ -243,10 +243,11 @@ def emulate_fir(spec, x, n_frames, out_len, valid_len=None):
     t = torch.from_numpy(np.asarray(taps, np.float64))
     fir = lambda v: F.conv1d(v, t[None, None].expand(v.shape[1], 1, -1), padding="same", groups=v.shape[1])
     wu = torch.from_numpy(np.asarray(wu, np.float64))
-    if mode in (1, 3):   # k = (cb r + ph) 16 + c for ci = 16 cb + c (mode 3: no FIR)
+    if mode in (1, 3):   # k = ((cb r / R + sub) 16 + c) R + p, phase sub R + p (mode 3: no FIR)
+        R = 8 if mode == 3 and r % 8 == 0 else 4 if mode == 3 else r
         f = F.pad(x, (0, n_frames * r - T))
         f = fir(f) if mode == 1 else f
-        bv = f.reshape(B, Cin // 16, 16, n_frames, r).permute(0, 1, 4, 2, 3).reshape(B, Cin * r, n_frames)
+        bv = f.reshape(B, Cin // 16, 16, n_frames, r // R, R).permute(0, 1, 4, 2, 5, 3).reshape(B, Cin * r, n_frames)
         y = torch.einsum("mk,bku->bmu", wu, bv)
     else:           # row 32 (co // P) + (co % P) r + ph
         P = 32 // r

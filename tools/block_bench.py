@@ -1,8 +1,9 @@
 #!/usr/bin/env python
 """Microbenchmark: one fused ConvBlock (ou_block) against the three tuned
-ou_conv launches it replaces, at the PP16 level geometries (B = 1, 8 s).
+ou_conv launches it replaces, at the PP16 level geometries (B = 1, 8 s) or
+PP24's at C4's clip (--family pp24 --batch 32).
 
-    python tools/block_bench.py [--reps 50] [--levels 0,1,2,3]
+    python tools/block_bench.py [--reps 50] [--levels 0,1,2,3] [--family pp24 --batch 32 --fused-only]
 """
 import argparse
 import json
@@ -18,6 +19,8 @@ from open_universe_amd import engine as E  # noqa: E402
 
 DEV = "cuda:0"
 LEVELS = [(32, 128160), (64, 64080), (128, 16020), (256, 4005), (512, 801)]
+# PP24 at C4's clip (10.01 s at 24 kHz; run with --batch 32 for the bench's batch)
+LEVELS24 = [(48, 240240), (96, 120120), (192, 40040), (384, 8008), (768, 1001)]
 
 
 def specs(C, g):
@@ -57,6 +60,8 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--levels", default="0,1,2,3")
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--family", default="pp16", choices=["pp16", "pp24"])
+    ap.add_argument("--fused-only", action="store_true", help="skip the three-launch form (counter passes)")
     ap.add_argument("--dbg", default="", help="comma list of ou_block diagnostic masks to time as well "
                                                 "(1 no input loads, 2 no MFMA stages, 4 no output pass)")
     a = ap.parse_args()
@@ -67,7 +72,7 @@ def main():
     E._PREP_KSWS = (ks.data_ptr(), E.KSWS_BYTES)
     rows = []
     for li in [int(x) for x in a.levels.split(",")]:
-        C, T = LEVELS[li]
+        C, T = (LEVELS24 if a.family == "pp24" else LEVELS)[li]
         g = torch.Generator().manual_seed(li)
         sp = specs(C, g)
         cws = [E.make_conv(s, DEV, prec=1) for s in sp]
@@ -77,7 +82,7 @@ def main():
         h = E.Act(torch.randn(B, C, T, device=DEV))
         out, tA, tB = (E.new_act(B, C, T, DEV) for _ in range(3))
         res = {}
-        for fz in (True, False):
+        for fz in (True,) if a.fused_only else (True, False):
             if not fz:
                 bw.fused = None
             prog = L.Program()

@@ -19,6 +19,9 @@
 #   convsplitlib:A,B the same on the k3 layers, in-tree library then variants A, B (stamps: --sstamps)
 #   fir:CFG          tools/fir_bench.py: folded vs FIR-applied rate-change convs at CFG
 #   sqfir:CFG/L/T    SQ counters (two rocprofv3 --pmc passes) of FIR layer L on tile T
+#   sqconv:L/T       the same for tools/conv_bench.py layer L on conv_kernel tile T
+#   sqblock:LEVEL    the same for a PP24 fused block at C4's batch (tools/block_bench.py)
+#   firtile:CFG/L/T1,T2  FIR layer L timed on each listed tile
 #
 #   e.g. tools/gpu_run.sh r04k profile:c2 critical bench:c1 bench:c3 bench:c5
 set -o pipefail
@@ -104,6 +107,30 @@ for step in "$@"; do
         timeout -k 10 400 python3 tools/fir_bench.py --config "${arg:-c4}" --folded $fo > "$O/fir_${TAG}_${arg:-c4}.txt" 2>&1 \
             || { tail -20 "$O/fir_${TAG}_${arg:-c4}.txt"; exit 1; }
         grep -v "ou tune\|amdgpu" "$O/fir_${TAG}_${arg:-c4}.txt" ;;
+    firtile)   # one FIR-kernel layer on each of a list of tiles: ARG = CFG/LAYER/T1,T2,..
+        IFS=/ read -r cfg lay tils <<< "$arg"
+        for til in ${tils//,/ }; do
+            timeout -k 10 120 python3 tools/fir_bench.py --config "$cfg" --only "$lay" --tile "$til" --reps 20 \
+                2>&1 | grep "FIR tile" | tee -a "$O/firtile_${TAG}_${lay}.txt"
+        done ;;
+    sqconv|sqblock)   # SQ counters: sqconv:LAYER/TILE (tools/conv_bench.py), sqblock:LEVEL (PP24 block, B 32)
+        if [ "$name" = sqconv ]; then
+            IFS=/ read -r lay til <<< "$arg"; k=conv_kernel; out="$O/sqconv_${TAG}_$lay"
+            cmd=(python3 "$ROOT/tools/conv_bench.py" --layer "$lay" --tile "$til" --reps 10)
+        else
+            k=block_kernel; out="$O/sqblock_${TAG}_L$arg"
+            cmd=(python3 "$ROOT/tools/block_bench.py" --family pp24 --batch 32 --levels "$arg" --fused-only --reps 10)
+        fi
+        ( cd /tmp && timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY \
+              SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
+              -d "${out}_a" -o pmc -- "${cmd[@]}" > "${out}_a.txt" 2>&1 ) || { tail -20 "${out}_a.txt"; exit 1; }
+        ( cd /tmp && timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
+              SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv \
+              -d "${out}_b" -o pmc -- "${cmd[@]}" > "${out}_b.txt" 2>&1 ) || { tail -20 "${out}_b.txt"; exit 1; }
+        { grep -v amdgpu "${out}_a.txt" | tail -2
+          python3 tools/pmc_avg.py "$(find "${out}_a" -name '*counter_collection.csv' | head -n1)" $k
+          python3 tools/pmc_avg.py "$(find "${out}_b" -name '*counter_collection.csv' | head -n1)" $k; } > "$out.txt"
+        cat "$out.txt" ;;
     sqfir)   # SQ counters of one FIR-kernel layer on a fixed tile: ARG = CFG/LAYER/TILE (e.g. c4/up0_r2/0x20000)
         IFS=/ read -r cfg lay til <<< "$arg"
         out="$O/sqfir_${TAG}_${lay}"
