@@ -423,8 +423,12 @@ _MMAJOR = os.environ.get("OUHIP_MMAJOR", "1") != "0"
 _MMAJOR_BYTES = float(os.environ.get("OUHIP_MMAJOR_MB", "128")) * 2**20
 
 
+FIR_BIT = 1 << 17   # FIR-applied rate-change kernels (bits 0-7 shape, bit 8 early epilogue loads)
+
+
 def mmajor_order(desc):
-    if not _MMAJOR or desc.tile & ((3 << 8) | (1 << 10)):   # one-tile and register-streamed kernels only
+    multi = desc.tile & ((3 << 8) | (1 << 10)) and not desc.tile & FIR_BIT
+    if not _MMAJOR or multi:   # one-tile, register-streamed and FIR kernels only
         return False
     in_bytes = 4.0 * desc.batch * desc.cin * desc.frame * desc.n_frames
     return in_bytes > _MMAJOR_BYTES

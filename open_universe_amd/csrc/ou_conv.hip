@@ -2431,6 +2431,12 @@ __global__ __launch_bounds__(256 + 64 * kWsLoaders) void conv_wkernel(ou_conv_de
 // chunks re-read every line once per chunk of phases).
 // ---------------------------------------------------------------------------
 [[maybe_unused]] constexpr int kFirBit = 1 << 17;
+// tile bit 9 (down fir 1 without residuals / FiLM, up without bit 8): two
+// input chunks in flight per thread (PD = 2) -- the raw x window of chunk
+// q + 2 is requested while chunk q's MFMAs run, for the layers whose chunks
+// are too short to cover an HBM round trip; costs 10-60 VGPRs
+[[maybe_unused]] constexpr int kFirDeep = 1 << 9;
+[[maybe_unused]] constexpr int kFirEarly = 1 << 8;   // up (fir 2): epilogue loads before the main loop
 
 template <int R, int WM, int WN, int MR, int NR>
 struct FCfg {
@@ -2512,7 +2518,7 @@ __device__ __forceinline__ void conv_epilogue_lean(const ou_conv_desc& d, int b,
     if (d.sy) ou_range_flag(d.status, somax, 2, lane);
 }
 
-template <int R, int WM, int WN, int MR, int NR, int P, int ST = 0, int LEAN = 0>
+template <int R, int WM, int WN, int MR, int NR, int P, int ST = 0, int LEAN = 0, int PD = 1>
 __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride)
 {
     using F = FCfg<R, WM, WN, MR, NR>;
@@ -2573,8 +2579,8 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
     // 16-B (R % 4 == 0) / 8-B (R == 2) loads where every row start is aligned
     constexpr int V = R % 4 == 0 ? 4 : (R == 2 ? 2 : 1);
     const bool vec = V > 1 && ((uintptr_t)d.x % (4 * V)) == 0 && d.x_bstride % V == 0 && xc % V == 0;
-    float xw[WIN];
-    auto stage_load = [&](int q) {   // q uniform, clamped (the extra load is never stored)
+    float xws[PD][WIN];   // PD raw windows in flight
+    auto stage_load = [&](int q, float (&xw)[WIN]) {   // q uniform, clamped (the extra load is never stored)
         q = min(q, nch - 1);
         const int cb = ST ? q / nsub : q;
         const int row = (cb * 16 + sc) * (int)xc;
@@ -2619,7 +2625,7 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
             *p = v[0];
         }
     };
-    auto stage_store = [&](int buf) {
+    auto stage_store = [&](int buf, float (&xw)[WIN]) {
         _Float16* bh = ldsh + buf * 2 * F::DPLANE + srow * F::DRS + sc * R;
 #pragma unroll
         for (int e = 0; e < WIN; ++e) {
@@ -2689,21 +2695,41 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
             }
     };
 
-    stage_load(0);
+#pragma unroll
+    for (int j = 0; j < PD; ++j) stage_load(j, xws[j]);
 #pragma unroll
     for (int s = 0; s < R; ++s) load_a(0, s);
-    stage_store(0);
+    stage_store(0, xws[0]);
     __syncthreads();
-    for (int q = 0; q < nch; ++q) {
-        const int cur = q & 1;
-        stage_load(q + 1);   // the next chunk's window, in flight under this chunk's MFMAs
+    if constexpr (PD == 1) {   // (kept as its own loop: the generic one measured slower at PD 1)
+        for (int q = 0; q < nch; ++q) {
+            const int cur = q & 1;
+            stage_load(q + 1, xws[0]);   // the next chunk's window, in flight under this chunk's MFMAs
 #pragma unroll
-        for (int s = 0; s < R; ++s) {
-            mfma_step(cur, s);
-            load_a(q + 1, s);   // refill the slot just used
+            for (int s = 0; s < R; ++s) {
+                mfma_step(cur, s);
+                load_a(q + 1, s);   // refill the slot just used
+            }
+            if (q + 1 < nch) stage_store(cur ^ 1, xws[0]);
+            __syncthreads();
         }
-        if (q + 1 < nch) stage_store(cur ^ 1);
-        __syncthreads();
+    } else {
+        for (int q0 = 0; q0 < nch; q0 += PD) {
+#pragma unroll
+            for (int j = 0; j < PD; ++j) {   // chunk q: window set j (stored), set j + 1 holds chunk q + 1
+                const int q = q0 + j;
+                if (q >= nch) break;
+                const int cur = q & 1;
+                stage_load(q + PD, xws[j]);   // in flight under the next PD chunks' MFMAs (clamped)
+#pragma unroll
+                for (int s = 0; s < R; ++s) {
+                    mfma_step(cur, s);
+                    load_a(q + 1, s);   // refill the slot just used
+                }
+                if (q + 1 < nch) stage_store(cur ^ 1, xws[(j + 1) % PD]);
+                __syncthreads();
+            }
+        }
     }
     if constexpr (P != 0) ou_range_flag(d.status, omax, 1, lane);
     const float sx = su * (1.f / 2048.f);
@@ -2721,7 +2747,7 @@ __global__ __launch_bounds__(256) void conv_fdkernel(ou_conv_desc d, int mtiles,
         conv_epilogue<MR, NR>(d, b, mt0 + wm * MR, n0 + wn * (32 * NR), acc, lane, col);
 }
 
-template <int R, int WM, int WN, int MR, int NR, int P>
+template <int R, int WM, int WN, int MR, int NR, int P, int EARLY = 0, int PD = 1>
 __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles, int64_t a_mt_stride)
 {
     using F = FCfg<R, WM, WN, MR, NR>;
@@ -2762,8 +2788,8 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
     // ---- staging: item it = (8-channel group cg = it / BN, row n = it % BN)
     const int64_t xc = d.x_cstride;
     const __amdgpu_buffer_rsrc_t xrs = ou_rsrc(d.x + (int64_t)b * d.x_bstride, (int64_t)d.cin * xc * 4);
-    float xv[F::UIE][8];
-    auto stage_load = [&](int q) {
+    float xvs[PD][F::UIE][8];   // PD chunks in flight
+    auto stage_load = [&](int q, float (&xv)[F::UIE][8]) {
         q = min(q, nch - 1);
 #pragma unroll
         for (int e = 0; e < F::UIE; ++e) {
@@ -2778,7 +2804,7 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
         }
     };
     float omax = 0.f;
-    auto stage_store = [&](int buf) {
+    auto stage_store = [&](int buf, float (&xv)[F::UIE][8]) {
         _Float16* bh = ldsh + buf * 2 * F::UPLANE;
 #pragma unroll
         for (int e = 0; e < F::UIE; ++e) {
@@ -2836,21 +2862,95 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
             }
     };
 
-    stage_load(0);
+    // ---- epilogue operands: item it = (channel cw = it / NSG, 4-sample group
+    // g).  EARLY (tile bit 8): the skip residual (the up conv's res1) and the
+    // bias of every item of this thread are requested before the main loop, so
+    // their HBM round trip overlaps the GEMM instead of following the FIR (at
+    // the price of 20-60 VGPRs held across it; the tuner times both)
+    const int ylen = d.out_len, vlen = d.valid_len;
+    const int tend = min((min(u0 + BNO, d.f0 + d.n_frames)) * R, ylen);   // samples [u0 R, tend) are stored
+    const int c0 = mt0 * F::CPT;                                           // first channel of the workgroup
+    const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr, has_fm = d.film != nullptr;
+    const float s1e = has_r1 ? d.s1 : 1.f, s2e = has_r2 ? d.s2 : 1.f, fadd = has_fm ? 0.f : 1.f;
+    const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)cout * d.y_cstride * 4);
+    const __amdgpu_buffer_rsrc_t r1s =
+        ou_rsrc(has_r1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y, has_r1 ? (int64_t)cout * d.r1_cstride * 4 : 0);
+    const __amdgpu_buffer_rsrc_t r2s =
+        ou_rsrc(has_r2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y, has_r2 ? (int64_t)cout * d.r2_cstride * 4 : 0);
+    const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
+    const __amdgpu_buffer_rsrc_t fs =
+        ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y, has_fm ? (int64_t)cout * 8 : 0);
+    constexpr int NSG = (BNO * R + 3) / 4;        // 4-sample groups per channel
+    constexpr int NIT = F::UCH * NSG;             // epilogue items of the workgroup
+    constexpr int UEI = (NIT + 255) / 256;        // per thread
+    // 16-B residual loads and stores where the tile's first sample and every
+    // row start are 16-B aligned (uniform over the workgroup)
+    auto al4 = [&](const float* p, int64_t bst, int64_t cst) {
+        return !p || (((uintptr_t)p % 16) == 0 && bst % 4 == 0 && cst % 4 == 0);
+    };
+    const bool v4 = ((u0 * R) & 3) == 0 && al4(d.y, d.y_bstride, d.y_cstride) &&
+                    al4(d.res1, d.r1_bstride, d.r1_cstride) && al4(d.res2, d.r2_bstride, d.r2_cstride);
+    auto ep_load = [&](int e, float (&r1)[4], float& bias) {   // item tid + 256 e (clamped)
+        const int it = min(tid + 256 * e, NIT - 1);
+        const int cw = it / NSG, g = it - (it / NSG) * NSG;
+        const int co = c0 + cw, sig = 4 * g, t0 = u0 * R + sig;
+        const bool cok = co < cout;
+        bias = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, cok ? co * 4 : kSentinel, 0, 0));
+        if (v4 && cok && sig + 3 < BNO * R && t0 + 3 < tend) {
+            const auto a1 = __builtin_amdgcn_raw_buffer_load_b128(r1s, (co * (int)d.r1_cstride + t0) * 4, 0, 0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r1[k] = __uint_as_float(a1[k]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int t = t0 + k;
+                const bool ok = cok && sig + k < BNO * R && t < tend;
+                r1[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    r1s, ok ? (co * (int)d.r1_cstride + t) * 4 : kSentinel, 0, 0));
+            }
+        }
+    };
+    float pr1[EARLY ? UEI : 1][4], pbias[EARLY ? UEI : 1];
+    if constexpr (EARLY) {
+#pragma unroll
+        for (int e = 0; e < UEI; ++e) ep_load(e, pr1[e], pbias[e]);
+    }
+
+#pragma unroll
+    for (int j = 0; j < PD; ++j) stage_load(j, xvs[j]);
     load_a(0, 0);
     load_a(0, 1);
-    stage_store(0);
+    stage_store(0, xvs[0]);
     __syncthreads();
-    for (int q = 0; q < nch; ++q) {
-        const int cur = q & 1;
-        stage_load(q + 1);
+    if constexpr (PD == 1) {
+        for (int q = 0; q < nch; ++q) {
+            const int cur = q & 1;
+            stage_load(q + 1, xvs[0]);
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            mfma_step(cur, s);
-            load_a(q + 1, s);
+            for (int s = 0; s < 2; ++s) {
+                mfma_step(cur, s);
+                load_a(q + 1, s);
+            }
+            if (q + 1 < nch) stage_store(cur ^ 1, xvs[0]);
+            __syncthreads();
         }
-        if (q + 1 < nch) stage_store(cur ^ 1);
-        __syncthreads();
+    } else {
+        for (int q0 = 0; q0 < nch; q0 += PD) {
+#pragma unroll
+            for (int j = 0; j < PD; ++j) {
+                const int q = q0 + j;
+                if (q >= nch) break;
+                const int cur = q & 1;
+                stage_load(q + PD, xvs[j]);   // clamped
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    mfma_step(cur, s);
+                    load_a(q + 1, s);
+                }
+                if (q + 1 < nch) stage_store(cur ^ 1, xvs[(j + 1) % PD]);
+                __syncthreads();
+            }
+        }
     }
     if constexpr (P != 0) ou_range_flag(d.status, omax, 1, lane);
 
@@ -2875,29 +2975,11 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
     // ---- FIR over 4 consecutive output samples per item, bias, residuals, store
     float tap[F::NT];
     fir_taps<F::NT>(d, tap);
-    const int ylen = d.out_len, vlen = d.valid_len;
-    const int tend = min((min(u0 + BNO, d.f0 + d.n_frames)) * R, ylen);   // samples [u0 R, tend) are stored
-    const int c0 = mt0 * F::CPT;                                           // first channel of the workgroup
-    const bool has_r1 = d.res1 != nullptr, has_r2 = d.res2 != nullptr, has_fm = d.film != nullptr;
-    const float s1e = has_r1 ? d.s1 : 1.f, s2e = has_r2 ? d.s2 : 1.f, fadd = has_fm ? 0.f : 1.f;
-    const __amdgpu_buffer_rsrc_t ys = ou_rsrc(d.y + (int64_t)b * d.y_bstride, (int64_t)cout * d.y_cstride * 4);
-    const __amdgpu_buffer_rsrc_t r1s =
-        ou_rsrc(has_r1 ? d.res1 + (int64_t)b * d.r1_bstride : d.y, has_r1 ? (int64_t)cout * d.r1_cstride * 4 : 0);
-    const __amdgpu_buffer_rsrc_t r2s =
-        ou_rsrc(has_r2 ? d.res2 + (int64_t)b * d.r2_bstride : d.y, has_r2 ? (int64_t)cout * d.r2_cstride * 4 : 0);
-    const __amdgpu_buffer_rsrc_t bs = ou_rsrc(d.bias, d.bias ? (int64_t)cout * 4 : 0);
-    const __amdgpu_buffer_rsrc_t fs =
-        ou_rsrc(has_fm ? d.film + (int64_t)b * d.film_bstride : d.y, has_fm ? (int64_t)cout * 8 : 0);
-    constexpr int NSG = (BNO * R + 3) / 4;   // 4-sample groups per channel
     constexpr int NW = (4 + 2 * R + 3) / 4 * 4;   // window floats read (16-B reads)
-    // 16-B residual loads and stores where the tile's first sample and every
-    // row start are 16-B aligned (uniform over the workgroup)
-    auto al4 = [&](const float* p, int64_t bst, int64_t cst) {
-        return !p || (((uintptr_t)p % 16) == 0 && bst % 4 == 0 && cst % 4 == 0);
-    };
-    const bool v4 = ((u0 * R) & 3) == 0 && al4(d.y, d.y_bstride, d.y_cstride) &&
-                    al4(d.res1, d.r1_bstride, d.r1_cstride) && al4(d.res2, d.r2_bstride, d.r2_cstride);
-    for (int it = tid; it < F::UCH * NSG; it += 256) {
+#pragma unroll
+    for (int e = 0; e < UEI; ++e) {
+        const int it = tid + 256 * e;
+        if (NIT % 256 != 0 && it >= NIT) break;
         const int cw = it / NSG, g = it - (it / NSG) * NSG;
         const int co = c0 + cw;
         const int sig = 4 * g;            // output sample u0 R + sig <-> Y index sig + R
@@ -2910,11 +2992,17 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
             w[k] = q4.x, w[k + 1] = q4.y, w[k + 2] = q4.z, w[k + 3] = q4.w;
         }
         const bool cok = co < cout;
-        const float bias = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bs, cok ? co * 4 : kSentinel, 0, 0));
+        float r1v[4], bias;
+        if constexpr (EARLY) {
+            bias = pbias[e];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r1v[k] = pr1[e][k];
+        } else {
+            ep_load(e, r1v, bias);
+        }
         const float ga = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, cok ? co * 4 : kSentinel, 0, 0));
         const float gb = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(fs, cok ? (cout + co) * 4 : kSentinel, 0, 0));
         if (v4 && cok && sig + 3 < BNO * R && t0 + 3 < tend) {   // a whole aligned group: 16-B accesses
-            const auto a1 = __builtin_amdgcn_raw_buffer_load_b128(r1s, (co * (int)d.r1_cstride + t0) * 4, 0, 0);
             const auto a2 = __builtin_amdgcn_raw_buffer_load_b128(r2s, (co * (int)d.r2_cstride + t0) * 4, 0, 0);
             float o[4];
 #pragma unroll
@@ -2924,7 +3012,7 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
                 for (int j = 0; j < F::NT; ++j) f = fmaf(tap[j], w[k + j], f);
                 float v = f + bias;
                 if (t0 + k >= vlen) v = 0.f;
-                v = (v + __uint_as_float(a1[k])) * s1e;
+                v = (v + r1v[k]) * s1e;
                 v = (ga + fadd) * v + gb;
                 o[k] = (v + __uint_as_float(a2[k])) * s2e;
             }
@@ -2934,13 +3022,11 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
             continue;
         }
         int off[4];
-        float v1[4], v2[4];
+        float v2[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int t = t0 + k;
             off[k] = (cok && sig + k < BNO * R && t < tend) ? t : -1;
-            v1[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                r1s, off[k] >= 0 ? (co * (int)d.r1_cstride + t) * 4 : kSentinel, 0, 0));
             v2[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                 r2s, off[k] >= 0 ? (co * (int)d.r2_cstride + t) * 4 : kSentinel, 0, 0));
         }
@@ -2951,7 +3037,7 @@ __global__ __launch_bounds__(256) void conv_fukernel(ou_conv_desc d, int mtiles,
             for (int j = 0; j < F::NT; ++j) f = fmaf(tap[j], w[k + j], f);
             float v = f + bias;
             if (off[k] >= vlen) v = 0.f;
-            v = (v + v1[k]) * s1e;
+            v = (v + r1v[k]) * s1e;
             v = (ga + fadd) * v + gb;
             v = (v + v2[k]) * s2e;
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ys,
@@ -3381,7 +3467,13 @@ int launch_f(const ou_conv_desc& d, hipStream_t s)
                                                 a_mt_stride, sattr[3], s);
         }
         if (d.fir == 3) return ou_fail(-2, "conv: FIR mode 3 needs rate 4 or 8 chunks");
-        static bool lattr[2] = {false, false};
+        static bool lattr[4] = {false, false, false, false};
+        if (lean && (d.tile & kFirDeep))
+            return d.prec == 1 ? fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 1, 0, 1, 2>, F::DLDS, grid, d, mtiles,
+                                            a_mt_stride, lattr[2], s)
+                               : fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 2, 0, 1, 2>, F::DLDS, grid, d, mtiles,
+                                            a_mt_stride, lattr[3], s);
+        if (d.tile & kFirDeep) return ou_fail(-2, "conv: FIR tile bit 9 needs a down conv without residuals / FiLM");
         if (lean)
             return d.prec == 1
                        ? fir_launch(conv_fdkernel<R, WM, WN, MR, NR, 1, 0, 1>, F::DLDS, grid, d, mtiles, a_mt_stride, lattr[0], s)
@@ -3394,6 +3486,19 @@ int launch_f(const ou_conv_desc& d, hipStream_t s)
     const int mtiles = (d.m / R + F::CPT - 1) / F::CPT;
     const int64_t a_mt_stride = (int64_t)((d.cin + kCinAlign - 1) / kCinAlign * kCinAlign) * 32;
     const dim3 grid((d.n_frames + F::BN - 3) / (F::BN - 2), (mtiles + WM * MR - 1) / (WM * MR), d.batch);
+    if (d.tile & kFirDeep) {
+        if (d.tile & kFirEarly) return ou_fail(-2, "conv: FIR tile bits 8 and 9 together");
+        static bool pattr[2] = {false, false};
+        return d.prec == 1
+                   ? fir_launch(conv_fukernel<R, WM, WN, MR, NR, 1, 0, 2>, F::ULDS, grid, d, mtiles, a_mt_stride, pattr[0], s)
+                   : fir_launch(conv_fukernel<R, WM, WN, MR, NR, 2, 0, 2>, F::ULDS, grid, d, mtiles, a_mt_stride, pattr[1], s);
+    }
+    if (d.tile & kFirEarly) {
+        static bool eattr[2] = {false, false};
+        return d.prec == 1
+                   ? fir_launch(conv_fukernel<R, WM, WN, MR, NR, 1, 1>, F::ULDS, grid, d, mtiles, a_mt_stride, eattr[0], s)
+                   : fir_launch(conv_fukernel<R, WM, WN, MR, NR, 2, 1>, F::ULDS, grid, d, mtiles, a_mt_stride, eattr[1], s);
+    }
     return d.prec == 1
                ? fir_launch(conv_fukernel<R, WM, WN, MR, NR, 1>, F::ULDS, grid, d, mtiles, a_mt_stride, attr[2], s)
                : fir_launch(conv_fukernel<R, WM, WN, MR, NR, 2>, F::ULDS, grid, d, mtiles, a_mt_stride, attr[3], s);
@@ -3688,7 +3793,7 @@ extern "C" int ou_conv(const ou_conv_desc* dp, void* stream)
                            d.fir, d.cin, d.frame, d.rout, d.kt);
         if (!(d.w_unscale > 0.f)) return ou_fail(-1, "conv: FIR mode needs the w_unscale of ou_conv_pack_split_nat");
         const int tile = d.tile >= 0 ? d.tile : (kFirBit | 2);
-        if (!(tile & kFirBit) || (tile & ~(kFirBit | kMajBit | 0xff)) || (tile & 0xff) >= kNumFTiles)
+        if (!(tile & kFirBit) || (tile & ~(kFirBit | kMajBit | kFirEarly | kFirDeep | 0xff)) || (tile & 0xff) >= kNumFTiles)
             return ou_fail(-2, "conv: FIR mode needs a FIR tile (tile 0x%x)", d.tile);
         ou_conv_desc dd = d;   // the kernels read their order bit from the tile
         dd.tile = tile;
@@ -3794,7 +3899,7 @@ extern "C" int ou_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int ou_conv_tile_ok(int kt, int tile)
 {
     if (tile & kFirBit)   // FIR applied (ou_conv_desc.fir): shape (+ m-major order); one tap
-        return !(tile & ~(kFirBit | kMajBit | 0xff)) && (tile & 0xff) < kNumFTiles && kt == 1;
+        return !(tile & ~(kFirBit | kMajBit | kFirEarly | kFirDeep | 0xff)) && (tile & 0xff) < kNumFTiles && kt == 1;
     if (tile & kSsBit)   // split-image input: shape = NR - 1 (+ m-major order)
         return !(tile & ~(kSsBit | kMajBit | 0xff)) && (tile & 0xff) < kNumSTiles && (kt == 1 || kt == 3 || kt == 5);
     if (tile & kRsBit)   // register-streamed: shape id (+ K slices, m-major order); LDS and chunks checked at launch

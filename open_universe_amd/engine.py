@@ -99,6 +99,8 @@ _REC_DEVICE = None   # the recording engine's device (split-image buffers outsid
 # records the faster, 1 always the FIR-applied form, 0 always the folded one.
 FIR_RATES = (2, 3, 4, 5, 8)
 FIR_BIT = 1 << 17
+FIR_EARLY = 1 << 8   # with FIR_BIT: the up kernel's residual / bias loads issued before its main loop
+FIR_DEEP = 1 << 9    # with FIR_BIT: two input chunks in flight per thread (lean down, up)
 
 
 def fir_mode():
@@ -1068,6 +1070,10 @@ class ConvTuner:
         ksl = (0, 1 << 12, 2 << 12, 3 << 12) if d.ks_ws and small else (0,)
         if d.fir:   # the FIR-applied rate-change kernels' shapes only
             cands = [t | FIR_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | FIR_BIT)]
+            if d.fir == 2:   # up: early epilogue loads (tile bit 8) or two chunks in flight (bit 9)
+                cands += [t | FIR_EARLY for t in cands] + [t | FIR_DEEP for t in cands]
+            elif d.fir == 1 and not (d.res1 or d.res2 or d.film):   # lean down: two chunks in flight
+                cands += [t | FIR_DEEP for t in cands]
         elif d.xs:   # a split-image input: the split-image kernel's shapes only
             cands = [t | L.SS_BIT for t in range(16) if lib.ou_conv_tile_ok(d.kt, t | L.SS_BIT)]
         elif d.prec in (1, 2):

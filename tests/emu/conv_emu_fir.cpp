@@ -232,7 +232,11 @@ int main(int argc, char** argv)
                 d.res2 = c.res2 ? r2.data() : nullptr; d.r2_bstride = d.y_bstride; d.r2_cstride = out_len; d.s2 = 0.5f;
                 d.prec = prec; d.w_unscale = unscale; d.xs_shift = s;
                 d.fir = c.dir; d.fir_taps = tap.data();
-                d.tile = kFirBit | shape | (shape == 3 ? kMajBit : 0);
+                // m-major order on shape 3; the up kernel's early epilogue loads on odd shapes;
+                // two chunks in flight on shapes 2 and 6 (down: bias-only layers)
+                const bool lean = !c.res1 && !c.res2 && !c.film;
+                d.tile = kFirBit | shape | (shape == 3 ? kMajBit : 0) | (!down && shape % 2 ? kFirEarly : 0) |
+                         (shape % 4 == 2 && (!down || lean) ? kFirDeep : 0);
                 if (down && c.sy && prec == 1) {
                     img.assign((size_t)c.B * (c.cout / 32) * rows * 64, 0x7e00);
                     d.sy = img.data(); d.sy_bstride = (int64_t)(c.cout / 32) * rows * 128; d.sy_rows = rows;

@@ -87,8 +87,10 @@ def test_fir_every_tile(direction, r, prec):
     f = E.fir_desc(d)
     lib = L.load()
     n = 0
+    # up: early epilogue loads / two chunks in flight; down (bias only here): two chunks in flight
+    early = (0, E.FIR_EARLY, E.FIR_DEEP) if direction == "up" else (0, E.FIR_DEEP)
     for shape in range(16):
-        for mm in (0, L.MAJ_BIT):
+        for mm in [m | e for m in (0, L.MAJ_BIT) for e in early]:
             t = E.FIR_BIT | shape | mm
             if not lib.ou_conv_tile_ok(1, t):
                 continue
