@@ -64,9 +64,12 @@ for step in "$@"; do
             OUHIP_TUNE_CACHE="$O/tune_${TAG}_c4.json" bench "$O/bench_${TAG}_c4_b$b" 300 --config c4 --batch $b \
                 --steps 4 --warmup 1 --no-f32-pass --no-cpu-baseline --traffic-json "" || exit 1
         done ;;
-    c4u)
-        OUHIP_TUNE_CACHE="$O/tune_${TAG}_c4.json" bench "$O/bench_${TAG}_config_c4_undamped" 900 --config c4 \
-            --undamped --steps 3 --warmup 2 --no-f32-pass --no-cpu-baseline || exit 1 ;;
+    c4u)   # C4 on the undamped weights, quoting the traffic of its own PMC passes
+        BENCH_EXTRA=--undamped bash tools/gpu_profile.sh "${TAG}_pmc_c4u" c4 --steps 3 --warmup 2 --no-f32-pass \
+            --no-queued > /dev/null || exit 1
+        OUHIP_TUNE_CACHE="$O/tune_${TAG}_pmc_c4u.json" bench "$O/bench_${TAG}_config_c4_undamped" 900 --config c4 \
+            --undamped --steps 3 --warmup 2 --no-f32-pass --no-cpu-baseline \
+            --traffic-json "$O/pmc_${TAG}_pmc_c4u.json" || exit 1 ;;
     critical)
         OUHIP_TUNE_CACHE="$O/tune_${TAG}_c2.json" timeout -k 10 300 python3 tools/critical_path.py --config c2 --reps 3 \
             --ops --out "$O/cp_$TAG.json" > "$O/cp_$TAG.txt" 2>&1 || { tail -20 "$O/cp_$TAG.txt"; exit 1; }
