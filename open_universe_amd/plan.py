@@ -53,6 +53,65 @@ def edm_weights(s, level_db, data_level_db=None):
 # profiles/ab_r04_summary.txt)
 PINNED_CHECK = True
 
+# OUHIP_NOISE_GRAPH=0: draw the sampler's noise with one torch.randn call per
+# draw instead of replaying them as one captured graph
+NOISE_GRAPH = os.environ.get("OUHIP_NOISE_GRAPH", "1") != "0"
+
+
+class NoiseDraws:
+    """The sampler's n device-generator draws ``torch.randn(shape, generator=rng,
+    out=nz[k])``, k = 0..n-1 (universe.py:39-41,326,338), replayed as one
+    captured graph per generator: the graph-safe Philox path reads the
+    generator's seed / offset at replay and advances it by the draws' total,
+    so the values and the generator's state afterwards are those of the n
+    eager calls -- checked once per generator against eager draws from a copy
+    of its state (a mismatch, or a capture error, falls back to the eager
+    calls for that generator).  One launch instead of n: the draws sit between
+    two enhances, where the GPU idles while the host issues them."""
+
+    def __init__(self, nz, shape):
+        self.nz, self.shape = nz, shape
+        self.graphs = {}   # id(generator) -> (generator, graph or None)
+
+    def _eager(self, rng, out):
+        for k in range(out.shape[0]):
+            torch.randn(self.shape, generator=rng, out=out[k])
+
+    def _capture(self, rng):
+        gen = rng if rng is not None else torch.cuda.default_generators[self.nz.device.index or 0]
+        state = gen.get_state()
+        try:
+            g = torch.cuda.CUDAGraph()
+            if rng is not None:
+                g.register_generator_state(rng)
+            with torch.cuda.graph(g):
+                self._eager(rng, self.nz)
+            # the check: one replay against eager draws from a copy of the state
+            chk = torch.Generator(device=self.nz.device)
+            chk.set_state(state)
+            ref = torch.empty_like(self.nz)
+            self._eager(chk, ref)
+            g.replay()
+            ok = bool(torch.equal(ref, self.nz)) and bool(torch.equal(chk.get_state(), gen.get_state()))
+        except Exception:   # noqa: BLE001 -- any capture trouble: the eager draws
+            g, ok = None, False
+        gen.set_state(state)   # the check consumed nothing of the caller's stream
+        return g if ok else None
+
+    def draw(self, rng):
+        if not NOISE_GRAPH or self.nz.shape[0] < 2:
+            self._eager(rng, self.nz)
+            return
+        ent = self.graphs.get(id(rng))
+        if ent is None or ent[0] is not rng:
+            if len(self.graphs) >= 4:
+                self.graphs.clear()
+            ent = self.graphs[id(rng)] = (rng, self._capture(rng))
+        if ent[1] is None:
+            self._eager(rng, self.nz)
+        else:
+            ent[1].replay()
+
 
 class _PlanBase:
     def __init__(self, eng):
@@ -315,12 +374,15 @@ class EnhancePlan(_PlanBase):
         """Noise in the reference's draw order (universe.py:39-41,326,338):
         x0 first, then one z per intermediate step."""
         shape = (self.B, 1, self.Tp)
-        for k in range(self.n_noise):
-            if rng is not None and rng.device != self.NZ.device:
+        if rng is not None and rng.device != self.NZ.device:
+            for k in range(self.n_noise):
                 z = torch.randn(shape, generator=rng, device=rng.device, dtype=torch.float32)
                 self.NZ[k].copy_(z, non_blocking=False)
-            else:
-                torch.randn(shape, generator=rng, out=self.NZ[k])
+            return
+        nd = self.__dict__.get("_noise")
+        if nd is None:
+            nd = self._noise = NoiseDraws(self.NZ[: self.n_noise], shape)
+        nd.draw(rng)
 
     def __call__(self, mix, rng=None, use_graph=True, clone=False):
         out = self.submit(mix, rng, use_graph)
