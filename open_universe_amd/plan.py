@@ -71,7 +71,7 @@ class NoiseDraws:
 
     def __init__(self, nz, shape):
         self.nz, self.shape = nz, shape
-        self.graphs = {}   # id(generator) -> (generator, graph or None)
+        self.graphs = {}   # id(generator) -> (generator, graph; False: seen once; None: eager)
 
     def _eager(self, rng, out):
         for k in range(out.shape[0]):
@@ -99,13 +99,19 @@ class NoiseDraws:
         return g if ok else None
 
     def draw(self, rng):
+        """A generator's first draw is eager; its second captures the graph (a
+        generator used once never pays for a capture)."""
         if not NOISE_GRAPH or self.nz.shape[0] < 2:
             self._eager(rng, self.nz)
             return
         ent = self.graphs.get(id(rng))
-        if ent is None or ent[0] is not rng:
+        if ent is None or ent[0] is not rng:   # first sight
             if len(self.graphs) >= 4:
                 self.graphs.clear()
+            self.graphs[id(rng)] = (rng, False)
+            self._eager(rng, self.nz)
+            return
+        if ent[1] is False:   # second sight: capture (None: capture failed or mismatched)
             ent = self.graphs[id(rng)] = (rng, self._capture(rng))
         if ent[1] is None:
             self._eager(rng, self.nz)
