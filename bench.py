@@ -337,7 +337,17 @@ def main():
 
     rank, local, world = dist_env()
     if world > 1:
-        dist.init_process_group("gloo")
+        # gloo's C++ side prints its "[Gloo] Rank r is connected ..." lines to
+        # stdout; stdout carries only rank 0's JSON line, so they go to stderr
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     if world != args.gpus and rank == 0:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: reporting {world}", file=sys.stderr)
     C = CONFIGS[args.config]

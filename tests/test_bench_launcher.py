@@ -15,8 +15,10 @@ def _run(*args):
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
                        timeout=180, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    # the bench contract: stdout is rank 0's one JSON line and nothing else
+    # (gloo's connection messages and the ranks' logs go to stderr)
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
     return json.loads(lines[0])
 
 
