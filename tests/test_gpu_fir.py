@@ -134,3 +134,53 @@ def test_fir_range_flag():
     f.xs_shift = -16   # stage x 2^16: |FIR(prelu(x))| ~ 1 -> well past 2^15
     _launch(f)
     assert int(st.item()) & 1
+
+
+@pytest.mark.parametrize("rt,cin,cout", [
+    (240, 48, 768), (120, 96, 768), (40, 192, 768),    # PP24's st_convs (condition.py:53-59)
+    (160, 32, 512), (80, 64, 512), (20, 128, 512),     # PP16's
+])
+def test_st_conv_fir3_every_tile(rt, cin, cout):
+    """The conditioner's wide strided convs on the FIR down kernel without a
+    FIR (ou_conv_desc.fir 3, K in chunks of 16 channels x 8 / 4 phases), every
+    tile shape, in both epilogues: bias only (the lean one) and the st_conv
+    running sum's two residuals, against float64 (ragged length: the last
+    frame is zero-padded, as F.conv1d over the padded input)."""
+    g = torch.Generator().manual_seed(rt + cin)
+    sd = {"p.conv.weight": torch.randn(cout, cin, rt, generator=g) / np.sqrt(cin * rt),
+          "p.prelu.weight": torch.tensor([0.25]), "p.conv.bias": torch.randn(cout, generator=g)}
+    spec = E.spec_down(sd, "p", rt, False)
+    assert spec.fir is not None and spec.fir[0] == 3
+    cw = E.make_conv(spec, DEV, prec=1)
+    B, U = 2, 37
+    T = U * rt - 5
+    x = torch.randn(B, cin, T, generator=g)
+    r1, r2 = torch.randn(B, cout, U, generator=g), torch.randn(B, cout, U, generator=g)
+    xd = torch.where(x.double() >= 0, x.double(), 0.25 * x.double())
+    base = F.conv1d(F.pad(xd, (0, U * rt - T)), sd["p.conv.weight"].double(), stride=rt)
+    base = base + sd["p.conv.bias"].double()[None, :, None]
+    lib = L.load()
+    n = 0
+    for res in (False, True):
+        y = E.new_act(B, cout, U, DEV)
+        if res:
+            d = E.conv_desc(cw, E.Act(x.to(DEV)), y, res1=E.Act(r1.to(DEV)), s1=1.0,
+                            res2=E.Act(r2.to(DEV)), s2=0.5)
+            ref = (base + r1.double() + r2.double()) * 0.5
+        else:
+            d = E.conv_desc(cw, E.Act(x.to(DEV)), y)
+            ref = base
+        f = E.fir_desc(d)
+        assert f.fir == 3
+        for shape in range(16):
+            for mm in (0, L.MAJ_BIT):
+                t = E.FIR_BIT | shape | mm
+                if not lib.ou_conv_tile_ok(1, t):
+                    continue
+                y.t.fill_(float("nan"))
+                f.tile = t
+                _launch(f)
+                err = rel_rms(y.t.cpu(), ref)
+                assert err < 1e-5, (res, shape, mm, err)
+                n += 1
+    assert n >= 16
